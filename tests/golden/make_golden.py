@@ -1,0 +1,267 @@
+"""Generate the golden fixtures by running the REFERENCE in this container.
+
+Run (build container only -- the reference never travels to the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 OPENBLAS_NUM_THREADS=1 OMP_NUM_THREADS=1 \
+        python tests/golden/make_golden.py
+
+It imports fbleile/midagma from /root/reference/src (read-only) and records
+inputs + outputs of `DagmaLinear._h/_score/_adam_update/minimize/fit`
+(`src/dagma/linear.py`) and `DagmaMLP.h_func` (`src/dagma/nonlinear.py:68-86`)
+into small .npz files next to this script.  Inputs come from the build's own
+numpy SEM generator (`midagma_amd.simulate`, seeded), because the reference's
+generator needs igraph, which is not installed.
+
+BLAS is pinned to one thread: the last bits of dgemm/dgetrf depend on the
+thread count, and the oracle test demands bit-equality.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+for _v in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS"):
+    os.environ.setdefault(_v, "1")
+os.environ.setdefault("TQDM_DISABLE", "1")
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, "/root/reference/src")
+
+from threadpoolctl import threadpool_limits  # noqa: E402
+
+import dagma.linear as ref_linear  # noqa: E402
+from dagma.linear import DagmaLinear  # noqa: E402
+from midagma_amd.simulate import make_dataset  # noqa: E402
+from tests.golden.inputs import mlp_fc1  # noqa: E402
+
+
+class Recorder:
+    """Stand-in for the tqdm bar `minimize` calls `update` on (linear.py:329, 332)."""
+
+    def __init__(self):
+        self.units = 0
+        self.big = 0
+
+    def update(self, k=1):
+        if k == 1:
+            self.units += 1
+        else:
+            self.big += 1
+
+    @property
+    def iters(self):
+        return self.units + (1 if self.big else 0)
+
+
+def setup_model(X, loss="l2", lambda1=0.03, checkpoint=1000, exclude=None, include=None):
+    """Replicate fit()'s data preparation (linear.py:406-429) on a fresh model."""
+    m = DagmaLinear(loss_type=loss, verbose=False)
+    X = X.copy()
+    m.X, m.lambda1, m.checkpoint = X, lambda1, checkpoint
+    m.n, m.d = X.shape
+    m.Id = np.eye(m.d).astype(m.dtype)
+    if loss == "l2":
+        m.X -= X.mean(axis=0, keepdims=True)
+    m.exc_r = m.exc_c = m.inc_r = m.inc_c = None
+    if exclude is not None:
+        m.exc_r, m.exc_c = zip(*exclude)
+    if include is not None:
+        m.inc_r, m.inc_c = zip(*include)
+    m.cov = X.T @ X / float(m.n)
+    return m
+
+
+def run_minimize(m, W0, mu, K, s, lr, tol=-1.0):
+    rec = Recorder()
+    W, ok = m.minimize(W0.copy(), mu, K, s, lr, tol=tol, pbar=rec)
+    return W, ok, rec.iters
+
+
+def in_domain_W(d, rng, scale):
+    """A random dense W inside the M-matrix domain (spectral radius of W*W < s)."""
+    W = rng.uniform(-1, 1, size=(d, d)) * scale
+    np.fill_diagonal(W, 0.0)
+    return W
+
+
+class NoisyInv:
+    """scipy.linalg stand-in whose inv() adds 1e-16 relative noise (SURVEY.md 8c envelope)."""
+
+    def __init__(self, rng):
+        import scipy.linalg as sla
+        self._sla, self._rng = sla, rng
+
+    def inv(self, A):
+        M = self._sla.inv(A)
+        return M * (1.0 + 1e-16 * self._rng.standard_normal(M.shape))
+
+    def __getattr__(self, k):
+        return getattr(self._sla, k)
+
+
+def with_noisy_inv(fn, seed=123):
+    orig = ref_linear.sla
+    ref_linear.sla = NoisyInv(np.random.default_rng(seed))
+    try:
+        return fn()
+    finally:
+        ref_linear.sla = orig
+
+
+def gen_data():
+    X, W, B = make_dataset(20, 1000, seed=0)
+    np.savez_compressed(os.path.join(HERE, "data_d20_n1000_seed0.npz"), X=X, W_true=W, B_true=B)
+    X1, W1, B1 = make_dataset(100, 2000, seed=1)
+    Xl, Wl, Bl = make_dataset(20, 1000, seed=2, sem_type="logistic")
+    np.savez_compressed(os.path.join(HERE, "data_meta.npz"),
+                        d100_sum=X1.sum(), d100_row0=X1[0], d100_Wtrue=W1,
+                        logit_X=Xl, logit_W_true=Wl)
+    return X, X1, Xl
+
+
+def gen_blocks(X20, Xl):
+    rng = np.random.default_rng(7)
+    out = {}
+    # G1 _h
+    for d, scale in ((5, 0.3), (20, 0.12), (100, 0.05)):
+        W = in_domain_W(d, rng, scale)
+        out[f"h_W_d{d}"] = W
+        for s in (1.0, 0.9, 0.6):
+            m = setup_model(np.zeros((2, d)) + np.arange(d), "l2")
+            h, G = m._h(W, s)
+            key = f"d{d}_s{s}"
+            out[f"h_val_{key}"] = np.array(h)
+            out[f"h_grad_{key}"] = G
+    # G2 _score, l2 and logistic at d=20
+    W = in_domain_W(20, rng, 0.1)
+    out["score_W"] = W
+    m = setup_model(X20, "l2")
+    l, G = m._score(W)
+    out["score_l2_loss"], out["score_l2_grad"] = np.array(l), G
+    ml = setup_model(Xl, "logistic")
+    l, G = ml._score(W)
+    out["score_logistic_loss"], out["score_logistic_grad"] = np.array(l), G
+    # G3 _adam_update: five steps of a fixed gradient sequence
+    m.opt_m, m.opt_v = 0, 0
+    gs = rng.standard_normal((5, 20, 20))
+    out["adam_g"] = gs
+    out["adam_out"] = np.stack([m._adam_update(gs[k], k + 1, 0.99, 0.999) for k in range(5)])
+    np.savez_compressed(os.path.join(HERE, "blocks.npz"), **out)
+
+
+def gen_traj(X, tag, Ks, lr=3e-4, mu=1.0, s=1.0, loss="l2", lambda1=0.03):
+    """W after K steps (tol=-1: no early stop) + the 1e-16-noise envelope per K."""
+    out = {"Ks": np.array(Ks)}
+    d = X.shape[1]
+    W0 = np.zeros((d, d))
+    for K in Ks:
+        m = setup_model(X, loss, lambda1=lambda1)
+        W, ok, it = run_minimize(m, W0, mu, K, s, lr)
+        out[f"W_K{K}"], out[f"ok_K{K}"], out[f"it_K{K}"] = W, np.array(ok), np.array(it)
+        m2 = setup_model(X, loss, lambda1=lambda1)
+        Wn, _, _ = with_noisy_inv(lambda: run_minimize(m2, W0, mu, K, s, lr))
+        out[f"env_K{K}"] = np.array(np.abs(Wn - W).max())
+    np.savez_compressed(os.path.join(HERE, f"traj_{tag}.npz"), **out)
+
+
+def gen_branches(X):
+    out = {}
+    d = X.shape[1]
+    W0 = np.zeros((d, d))
+    # lr-halving path: large lr at s=1.0 (linear.py:234-241)
+    m = setup_model(X, "l2")
+    msgs = []
+    m.vprint = lambda *a, **k: msgs.append(" ".join(str(x) for x in a))
+    W, ok, it = run_minimize(m, W0, 1.0, 60, 1.0, 0.3)
+    out["halve_W"], out["halve_ok"], out["halve_it"] = W, np.array(ok), np.array(it)
+    out["halve_nhalvings"] = np.array(sum("Learning rate decreased" in x for x in msgs))
+    # out-of-domain at s <= 0.9 (linear.py:231-233)
+    m = setup_model(X, "l2")
+    W, ok, it = run_minimize(m, W0, 1.0, 60, 0.9, 0.3)
+    out["ood_W"], out["ood_ok"], out["ood_it"] = W, np.array(ok), np.array(it)
+    # include / exclude edge masks (linear.py:217-222, 276)
+    exc = ((0, 1), (2, 3), (5, 4))
+    inc = ((1, 0), (3, 7))
+    m = setup_model(X, "l2", exclude=exc, include=inc)
+    W, ok, it = run_minimize(m, W0, 1.0, 500, 1.0, 3e-4)
+    out["mask_W"], out["mask_exc"], out["mask_inc"] = W, np.array(exc), np.array(inc)
+    np.savez_compressed(os.path.join(HERE, "branches.npz"), **out)
+
+
+def gen_fit(X):
+    """Full default fit at d=20 with per-stage iteration counts."""
+    calls = []
+
+    class Spy(DagmaLinear):
+        def minimize(self, W, mu, max_iter, s, lr, tol=1e-6, beta_1=0.99, beta_2=0.999, pbar=None):
+            rec = Recorder()
+            Wr, ok = super().minimize(W, mu, max_iter, s, lr, tol, beta_1, beta_2, pbar=rec)
+            calls.append((mu, s, lr, max_iter, ok, rec.iters))
+            return Wr, ok
+
+        def _h(self, W, s=1.0):
+            self.last_h_W = W.copy()  # the final call (linear.py:456) sees the pre-threshold W
+            return super()._h(W, s)
+
+    def one_fit():
+        calls.clear()
+        m = Spy(loss_type="l2", verbose=False)
+        W = m.fit(X.copy(), lambda1=0.03, s=[1.0, .9, .8, .7, .6])
+        return m, W, list(calls)
+
+    m, W, c = one_fit()
+    m2, W2, c2 = with_noisy_inv(one_fit, seed=99)
+    out = {"W": W, "W_unthresholded": m.last_h_W, "calls": np.array(c, dtype=np.float64),
+           "h_final": np.array(m.h_final), "score_final": np.array(m.score_final),
+           "W_noisy": W2, "W_unthresholded_noisy": m2.last_h_W,
+           "calls_noisy": np.array(c2, dtype=np.float64)}
+    np.savez_compressed(os.path.join(HERE, "fit_d20.npz"), **out)
+
+
+def gen_mlp():
+    """DagmaMLP.h_func value and autograd gradient (nonlinear.py:68-86).
+
+    fc1 weights come from numpy (seeded) so they are regenerable; for d=200 only
+    a seeded sample of the (2000 x 200) gradient is stored to keep the file small.
+    """
+    import torch
+    from dagma.nonlinear import DagmaMLP
+    out = {}
+    for d, m1 in ((20, 10), (200, 10)):
+        model = DagmaMLP(dims=[d, m1, 1], bias=True, dtype=torch.double)
+        w = mlp_fc1(d, m1)
+        with torch.no_grad():
+            model.fc1.weight.copy_(torch.from_numpy(w))
+        pick = np.random.default_rng(5).choice(w.size, size=min(w.size, 4000), replace=False)
+        out[f"pick_d{d}"] = pick
+        for s in (1.0, 0.8):
+            model.zero_grad()
+            h = model.h_func(s)
+            h.backward()
+            g = model.fc1.weight.grad.detach().numpy().copy()
+            out[f"h_d{d}_s{s}"] = np.array(h.item())
+            out[f"gradpick_d{d}_s{s}"] = g.reshape(-1)[pick]
+            out[f"gradnorm_d{d}_s{s}"] = np.array(np.linalg.norm(g))
+    np.savez_compressed(os.path.join(HERE, "mlp_h.npz"), **out)
+
+
+def main():
+    with threadpool_limits(limits=1):
+        X20, X100, Xl = gen_data()
+        gen_blocks(X20, Xl)
+        gen_traj(X20, "d20", [1, 10, 100, 1000, 10000])
+        gen_traj(X100, "d100", [1, 10, 100, 1000])
+        gen_traj(Xl, "logistic_d20", [1, 10, 100, 1000], loss="logistic", lambda1=0.05)
+        gen_branches(X20)
+        gen_fit(X20)
+        gen_mlp()
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
