@@ -1,0 +1,133 @@
+/*
+ * midagma_hip.h -- C ABI of the MI355X-native DAGMA inner solver.
+ *
+ * The reference (fbleile/midagma) has no native code and no FFI: its hot path
+ * is the Python method `DagmaLinear.minimize` (src/dagma/linear.py:165-333)
+ * with helpers `_score` (70-94), `_h` (97-116), `_func` (118-135) and
+ * `_adam_update` (138-163), reading object state set by `fit()`
+ * (linear.py:406-429).  Each entry point below replaces one of those Python
+ * call sites; the ctypes binding that makes them a drop-in lives in
+ * `midagma_amd/_lib.py` and is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - plain C types only; host arrays are caller-owned, C-contiguous float64;
+ *     device pointers (the *_dev entry points, midagma_bind_zbuf) are borrowed.
+ *   - every function returns MIDAGMA_OK (0) or a negative error code; the
+ *     message is available from midagma_last_error(solver) (or (NULL) for
+ *     errors raised before a solver exists).  No C++ exception crosses the ABI.
+ *   - a solver is not thread-safe; one host thread drives it.
+ */
+#ifndef MIDAGMA_HIP_H_
+#define MIDAGMA_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIDAGMA_ABI_VERSION 1
+
+/* return codes */
+#define MIDAGMA_OK 0
+#define MIDAGMA_E_HIP (-1)      /* HIP runtime failure            -> RuntimeError        */
+#define MIDAGMA_E_SINGULAR (-2) /* non-finite inverse (scipy getrf info>0) -> LinAlgError */
+#define MIDAGMA_E_ARG (-3)      /* bad argument / shape            -> ValueError          */
+#define MIDAGMA_E_STATE (-4)    /* call out of sequence            -> RuntimeError        */
+
+/* loss_type (linear.py:52-53) and score mode */
+#define MIDAGMA_LOSS_L2 0
+#define MIDAGMA_LOSS_LOGISTIC 1
+#define MIDAGMA_MODE_COV 0  /* cov = X^T X / n precomputed (linear.py:428); l2 only   */
+#define MIDAGMA_MODE_DATA 1 /* X row shard resident; per-step X^T(...) + all-reduce */
+
+/* minimize outcome (midagma_result.status) */
+#define MIDAGMA_ST_RUNNING 0
+#define MIDAGMA_ST_DONE 1         /* max_iter or tolerance      -> (W, True)  linear.py:333, 330 */
+#define MIDAGMA_ST_FAILED 2       /* out of domain, iter 1 or s<=0.9 -> (W, False) linear.py:233   */
+#define MIDAGMA_ST_LR_UNDERFLOW 3 /* lr <= 1e-16               -> (W, True)  linear.py:237-238   */
+#define MIDAGMA_ST_SINGULAR 4
+
+typedef struct midagma_solver midagma_solver;
+
+typedef struct {
+  int64_t iters;         /* Adam steps applied (pbar.update total, linear.py:332)   */
+  int64_t halvings;      /* lr halvings in the domain line search (linear.py:236)   */
+  int64_t slots;         /* device step slots consumed (diagnostics)                */
+  int64_t n_checkpoints; /* objective evaluations (linear.py:279-280)               */
+  int32_t status;        /* MIDAGMA_ST_*                                            */
+  int32_t early_stop;    /* 1 if |dobj/obj| <= tol ended the call (linear.py:328)   */
+  double lr_final;
+  double obj_last, score_last, h_last, l1_last;
+} midagma_result;
+
+typedef struct {
+  int64_t iter;
+  double obj, score, h, lr, l1; /* subset of the minimize.checkpoint record (linear.py:290-326) */
+} midagma_ckpt;
+
+int midagma_abi_version(void);
+int midagma_device_count(int* n);
+const char* midagma_last_error(const midagma_solver* s);
+
+/* Replaces DagmaLinear.__init__ + the data part of fit() (linear.py:25-67, 406-429).
+ * d: number of nodes; device: HIP ordinal; stream: hipStream_t to run on, or NULL
+ * for a solver-owned stream (required for the graph-replayed minimize loop). */
+int midagma_create(midagma_solver** out, int loss, int mode, int64_t d, int device, void* stream);
+void midagma_destroy(midagma_solver* s);
+void* midagma_stream(midagma_solver* s);
+int64_t midagma_padded_dim(const midagma_solver* s);
+
+/* cov = X^T X / n (linear.py:428), host d x d with leading dimension ld. */
+int midagma_set_cov(midagma_solver* s, const double* cov, int64_t ld);
+/* mask_inc / mask_exc for the next minimize call (linear.py:217-222), host d x d or NULL. */
+int midagma_set_masks(midagma_solver* s, const double* mask_inc, const double* mask_exc);
+/* data mode: this rank's row shard of X (n_local x d, ld = d); n_global = rows over all ranks.
+ * on_device != 0: X is a device pointer (copied). */
+int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_t n_global, int on_device);
+/* data mode: zbuf <- X_k^T X_k (all-reduce it, then midagma_cov_from_zbuf(n): cov = zbuf / n). */
+int midagma_data_gram(midagma_solver* s);
+int midagma_cov_from_zbuf(midagma_solver* s, double n);
+/* The d x d (+ tail) device buffer that carries the per-step score partial Z_k.
+ * Bind an external buffer (e.g. a torch tensor that torch.distributed all-reduces). */
+int64_t midagma_zbuf_len(const midagma_solver* s);
+int midagma_bind_zbuf(midagma_solver* s, void* dev_ptr, int64_t len);
+
+/* Replaces DagmaLinear.minimize(W, mu, max_iter, s, lr, tol, beta_1, beta_2)
+ * (linear.py:165-333) with trek_reg disabled.  W: host d x d, in/out. */
+int midagma_minimize(midagma_solver* s, double* W, double mu, int64_t max_iter, double s_dom, double lr,
+                     double tol, double beta1, double beta2, double lambda1, int64_t checkpoint,
+                     midagma_result* res);
+
+/* The same loop one step at a time, for an external all-reduce between the halves
+ * (data mode on several ranks):  begin; { step_partial; allreduce(zbuf); step_finish }*; end. */
+int midagma_begin(midagma_solver* s, const double* W, double mu, int64_t max_iter, double s_dom, double lr,
+                  double tol, double beta1, double beta2, double lambda1, int64_t checkpoint);
+int midagma_step_partial(midagma_solver* s);
+/* enqueue n whole slots (part 1 + part 2) without host polling; midagma_sync waits. */
+int midagma_run_slots(midagma_solver* s, int64_t n);
+int midagma_sync(midagma_solver* s);
+int midagma_step_finish(midagma_solver* s);
+int midagma_poll(midagma_solver* s, midagma_result* res); /* synchronizes */
+int midagma_end(midagma_solver* s, double* W, midagma_result* res);
+int64_t midagma_checkpoints(midagma_solver* s, midagma_ckpt* out, int64_t cap);
+
+/* Replaces DagmaLinear._h (linear.py:97-116): h and G_h = 2 W o inv(sI - W o W)^T (G nullable). */
+int midagma_h(midagma_solver* s, const double* W, double s_dom, double* h, double* G);
+/* Replaces DagmaLinear._score (linear.py:70-94) in cov mode (l2). */
+int midagma_score(midagma_solver* s, const double* W, double* loss, double* G);
+/* _score in data mode: partial into zbuf (all-reduce it), then finish. */
+int midagma_score_partial(midagma_solver* s, const double* W);
+int midagma_score_finish(midagma_solver* s, double* loss, double* G);
+
+/* DagmaMLP.h_func kernel (nonlinear.py:68-86) on device memory:
+ * Mt = (sI - A)^{-T} (ldm) and logdet_dev[0] = log|det(sI - A)| for A (d x d, lda).
+ * Enqueued on `stream`, no host synchronization. */
+int midagma_logdet_inv_dev(const double* A, int64_t d, int64_t lda, double s_dom, double* logdet_dev,
+                           double* Mt_dev, int64_t ldm, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MIDAGMA_HIP_H_ */

@@ -1,0 +1,86 @@
+// Shared definitions for the MI355X (gfx950) DAGMA inner-solver kernels.
+//
+// Layout in HBM: every d x d matrix is stored row-major with leading dimension
+// D = round_up(d, 64), so 64 x 64 tiles are aligned and the f64 MFMA tile
+// kernels never need edge guards.  Padding is zero for W/m/v/g/cov and the
+// identity for the log-det work matrix, which keeps the padded block of the
+// inverse equal to I and its pivots equal to 1 (log 1 = 0).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace midagma {
+
+constexpr int TILE = 64;          // tile edge of every blocked kernel
+constexpr int NTHREADS = 256;     // 4 waves of 64 lanes
+constexpr int NRED = 256;         // fixed number of partial-sum slots (deterministic reduction)
+
+// LDS row strides (in doubles) that make the MFMA operand reads conflict-free:
+// the f64 16x16x4 MFMA reads A[m0 + (lane&15)][k0 + (lane>>4)] and
+// B[k0 + (lane>>4)][n0 + (lane&15)]; with ds_read_b64 a 32-lane group touches
+// rows {0..15} x k {0,1}.  [m][k] images need stride = 2 mod 32, [k][n] images
+// need stride = 16 mod 32.
+constexpr int SA = 66;            // operand image stored [m][k]
+constexpr int SB = 80;            // operand image stored [k][n] (or [k][m])
+
+enum Status : int32_t {
+  ST_RUNNING = 0,
+  ST_DONE = 1,          // max_iter reached or checkpoint tolerance met  -> (W, True)
+  ST_FAILED = 2,        // left the M-matrix domain at iter 1 or s <= 0.9 -> (W, False)
+  ST_LR_UNDERFLOW = 3,  // lr halved below 1e-16                         -> (W, True)
+  ST_SINGULAR = 4,      // non-finite inverse                            -> LinAlgError
+};
+
+enum Action : int32_t { ACT_NOOP = 0, ACT_STEP = 1, ACT_HALVE = 2, ACT_REVERT = 3 };
+
+// Per-minimize constants, uploaded once per call (linear.py:165-175, 217-222).
+struct Params {
+  double mu, s, lambda1, tol, beta1, beta2, c1, c2;  // c1 = 1 - beta1, c2 = 1 - beta2 (host)
+  double mu_l1;       // mu * lambda1, host-rounded as the reference (linear.py:248)
+  double zscale;      // G_score = zscale * Z + cscale * cov
+  double cscale;
+  double score_scale; // checkpoint score = score_scale * sum(dif * Z) (+ logistic loss term)
+  double logit_scale; // 1/n for the logistic loss partial
+  double d_log_s;     // d * log(s), host-rounded (linear.py:114)
+  int64_t max_iter, checkpoint, d, D, ld_table;
+  int32_t has_inc, has_exc, logistic, pad_;
+};
+
+// Device-resident solver state: written only by the 1-workgroup controller
+// kernel, read by every other kernel (kernel boundaries give visibility).
+struct State {
+  int64_t iter;          // Adam steps applied so far
+  int64_t halvings;
+  int64_t slots;         // slots the controller has seen (diagnostics)
+  int64_t n_ckpt;
+  int32_t status;
+  int32_t ckpt_pending;  // objective of the current W is due this slot
+  int32_t early_stop;
+  int32_t action;        // decision for this slot's fused update
+  double lr;             // current learning rate
+  double lr_a, lr_b;     // HALVE: W += lr_a*g; W -= lr_b*g.  STEP: lr_a = lr
+  double bc1, bc2;       // 1 - beta^it from the host table (bit-exact with Python)
+  double obj_prev;
+  double obj_last, score_last, h_last, l1_last;
+  int32_t flags;         // bit0: inverse has an entry < 0 after +1e-16; bit1: non-finite
+  int32_t pad_;
+};
+
+// One checkpoint record (linear.py:280-326 subset; norms are a later row).
+struct CkptRec {
+  int64_t iter;
+  double obj, score, h, lr, l1;
+};
+
+__host__ __device__ inline int64_t round_up64(int64_t x) { return (x + 63) / 64 * 64; }
+
+}  // namespace midagma
+
+#define HIP_TRY(expr)                                                     \
+  do {                                                                    \
+    hipError_t _e = (expr);                                               \
+    if (_e != hipSuccess) {                                               \
+      throw ::midagma::HipError(_e, #expr, __FILE__, __LINE__);           \
+    }                                                                     \
+  } while (0)

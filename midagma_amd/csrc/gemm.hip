@@ -1,0 +1,172 @@
+// FP64 MFMA GEMM for the score gradients (linear.py:244, 246).
+//
+//   cov mode  : rhs = ((-mu) cov) @ (I - W)                   (d x d x d)
+//   data mode : Y = X_k @ (I - W)  then  Z_k = X_k^T @ Y      (l2, row shard k)
+//   logistic  : Y = expit(X_k @ W)  then  Z_k = X_k^T @ Y      (+ loss partials)
+//
+// 64 x 64 output tile per 256-thread workgroup, 64-deep K tiles staged through
+// LDS in conflict-free images (mfma64.h); I - W is formed while staging B, the
+// sigmoid and the logistic loss are fused into the epilogue.  Long K (= rows of
+// the shard) is split over blockIdx.z into fixed slices summed in fixed order.
+#include "launch.h"
+#include "mfma64.h"
+
+namespace midagma {
+
+struct IMinus {
+  int64_t k0, n0;
+  __device__ __forceinline__ double operator()(int r, int c, double v) const {
+    return ((k0 + r) == (n0 + c) ? 1.0 : 0.0) - v;
+  }
+};
+
+// numpy.logaddexp(0, x) (npy_math: log1p/exp split on the sign of the difference)
+__device__ __forceinline__ double logaddexp0(double x) {
+  if (x == 0.0) return 0.69314718055994530942;
+  const double t = -x;
+  if (t > 0) return log1p(exp(-t));
+  return x + log1p(exp(t));
+}
+
+template <bool ATRANS, int BMODE, int EPI>
+__global__ __launch_bounds__(NTHREADS) void gemm_kernel(int64_t K, int64_t kslice, const double* __restrict__ A,
+                                                        int64_t lda, const double* __restrict__ B, int64_t ldb,
+                                                        double* __restrict__ C, int64_t ldc, int64_t slice_stride,
+                                                        double* __restrict__ loss_part, int64_t m_valid,
+                                                        int64_t n_valid, const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Ls = smem;            // [64][SA] or [64][SB] image of op(A)
+  double* Bs = smem + 64 * SB;  // [64][SB] image of op(B)
+  const int64_t bm = blockIdx.y, bn = blockIdx.x, z = blockIdx.z;
+  const int64_t k_begin = z * kslice;
+  const int64_t k_end = (k_begin + kslice < K) ? k_begin + kslice : K;
+  Quad q;
+  q.zero();
+  for (int64_t kt = k_begin; kt < k_end; kt += 64) {
+    __syncthreads();
+    if (ATRANS)
+      tile_to_lds<SB>(Ls, A + kt * lda + bm * 64, lda, Ident());
+    else
+      tile_to_lds<SA>(Ls, A + bm * 64 * lda + kt, lda, Ident());
+    if (BMODE == B_IMINUS)
+      tile_to_lds<SB>(Bs, B + kt * ldb + bn * 64, ldb, IMinus{kt, bn * 64});
+    else
+      tile_to_lds<SB>(Bs, B + kt * ldb + bn * 64, ldb, Ident());
+    __syncthreads();
+    quad_mma<ATRANS>(Ls, Bs, q);
+  }
+  double* Ct = C + z * slice_stride + bm * 64 * ldc + bn * 64;
+  if (EPI == EPI_STORE) {
+    quad_foreach(q, [&](int row, int col, double& v) { Ct[(int64_t)row * ldc + col] = v; });
+    return;
+  }
+  // EPI_SIGMOID (A = X row-major, not transposed)
+  const bool want_loss = loss_part != nullptr && (st == nullptr || st->ckpt_pending);
+  double part = 0.0;
+  quad_foreach(q, [&](int row, int col, double& v) {
+    const int64_t gi = bm * 64 + row, gj = bn * 64 + col;
+    if (want_loss && gi < m_valid && gj < n_valid) {
+      const double x = A[gi * lda + gj];
+      part += logaddexp0(v) - x * v;
+    }
+    Ct[(int64_t)row * ldc + col] = 1.0 / (1.0 + exp(-v));
+  });
+  if (!want_loss) return;
+  __shared__ double red[NTHREADS];
+  red[threadIdx.x] = part;
+  __syncthreads();
+  for (int s = NTHREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss_part[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+}
+
+constexpr size_t kGemmLds = (2 * 64 * SB) * sizeof(double);
+
+template <bool AT, int BM, int EP>
+static void set_attr() {
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<AT, BM, EP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmLds));
+}
+
+void gemm_setup_attributes() {
+  set_attr<false, B_PLAIN, EPI_STORE>();
+  set_attr<false, B_IMINUS, EPI_STORE>();
+  set_attr<true, B_PLAIN, EPI_STORE>();
+  set_attr<true, B_IMINUS, EPI_STORE>();
+  set_attr<false, B_PLAIN, EPI_SIGMOID>();
+}
+
+void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, bool a_trans, const double* B,
+                 int64_t ldb, GemmB bmode, double* C, int64_t ldc, GemmEpi epi, int split, int64_t slice_stride,
+                 double* loss_part, int64_t m_valid, int64_t n_valid, const State* st, hipStream_t stream) {
+  if (M % 64 || N % 64 || K % 64 || split < 1) throw std::invalid_argument("launch_gemm: bad shape");
+  const int64_t ktiles = K / 64;
+  const int64_t per = (ktiles + split - 1) / split;
+  const int nsplit = (int)((ktiles + per - 1) / per);
+  dim3 grid((unsigned)(N / 64), (unsigned)(M / 64), (unsigned)nsplit);
+  const int64_t kslice = per * 64;
+#define MIDAGMA_GEMM(AT, BM, EP)                                                                         \
+  hipLaunchKernelGGL((gemm_kernel<AT, BM, EP>), grid, dim3(NTHREADS), kGemmLds, stream, K, kslice, A, lda, B, \
+                     ldb, C, ldc, slice_stride, loss_part, m_valid, n_valid, st)
+  if (epi == EPI_SIGMOID) {
+    if (a_trans || bmode != B_PLAIN || nsplit != 1) throw std::invalid_argument("launch_gemm: sigmoid form");
+    MIDAGMA_GEMM(false, B_PLAIN, EPI_SIGMOID);
+  } else if (!a_trans && bmode == B_PLAIN) {
+    MIDAGMA_GEMM(false, B_PLAIN, EPI_STORE);
+  } else if (!a_trans) {
+    MIDAGMA_GEMM(false, B_IMINUS, EPI_STORE);
+  } else if (bmode == B_PLAIN) {
+    MIDAGMA_GEMM(true, B_PLAIN, EPI_STORE);
+  } else {
+    MIDAGMA_GEMM(true, B_IMINUS, EPI_STORE);
+  }
+#undef MIDAGMA_GEMM
+  HIP_TRY(hipGetLastError());
+}
+
+__global__ __launch_bounds__(NTHREADS) void sum_slices_kernel(const double* __restrict__ parts, int split,
+                                                              int64_t stride, int64_t count,
+                                                              double* __restrict__ out,
+                                                              const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  for (int64_t i = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; i < count; i += (int64_t)gridDim.x * NTHREADS) {
+    double acc = parts[i];
+    for (int z = 1; z < split; ++z) acc += parts[z * stride + i];
+    out[i] = acc;
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS) void sum_vector_kernel(const double* __restrict__ v, int64_t n,
+                                                              double* __restrict__ out,
+                                                              const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  __shared__ double red[NTHREADS];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += NTHREADS) acc += v[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = NTHREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+void launch_sum_slices(const double* parts, int split, int64_t stride, int64_t count, double* out,
+                       const State* st, hipStream_t stream) {
+  int64_t blocks = (count + NTHREADS - 1) / NTHREADS;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(sum_slices_kernel, dim3((unsigned)blocks), dim3(NTHREADS), 0, stream, parts, split, stride,
+                     count, out, st);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_sum_vector(const double* v, int64_t n, double* out, const State* st, hipStream_t stream) {
+  hipLaunchKernelGGL(sum_vector_kernel, dim3(1), dim3(NTHREADS), 0, stream, v, n, out, st);
+  HIP_TRY(hipGetLastError());
+}
+
+}  // namespace midagma

@@ -1,0 +1,71 @@
+// Host-side launchers for the kernels (all enqueue on the given stream, no sync,
+// no allocation: safe to capture into a hipGraph).
+#pragma once
+
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+
+namespace midagma {
+
+struct HipError : std::runtime_error {
+  hipError_t code;
+  HipError(hipError_t e, const char* what, const char* file, int line)
+      : std::runtime_error(std::string("HIP error ") + hipGetErrorString(e) + " at " + file + ":" +
+                           std::to_string(line) + " (" + what + ")"),
+        code(e) {}
+};
+
+struct GJWork {
+  double* P;       // 64 x 64
+  double* R;       // 64 x D
+  double* C;       // D x 64
+  double* pivlog;  // D  (log |pivot| per row, nullable)
+};
+
+// --- gj.hip -----------------------------------------------------------------
+void gj_setup_attributes();
+// At = (s*I - f(X))^T on the logical d x d block, identity padding; f = x^2 if square.
+void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int64_t D, int64_t d, double s,
+                     const State* st, hipStream_t stream);
+// In place: A <- inv(A) (unpivoted blocked Gauss-Jordan), pivot logs into w.pivlog.
+void launch_gj_inverse(double* A, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
+
+// --- gemm.hip ---------------------------------------------------------------
+enum GemmB : int { B_PLAIN = 0, B_IMINUS = 1 };
+enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1 };
+void gemm_setup_attributes();
+// C[M x N] = op(A) * op(B); op(A) = A ([m][k], lda) or, if a_trans, A stored [k][m] (lda);
+// op(B) = B or (I - B) ([k][n], ldb).  M, N, K multiples of 64.  With split > 1
+// the K range is cut into `split` slices written to C + z*slice_stride.
+// EPI_SIGMOID: C = expit(acc); if loss_part != nullptr and st->ckpt_pending,
+// per-workgroup partials of sum(logaddexp(0,acc) - X*acc) over rows < m_valid,
+// cols < n_valid go to loss_part[blockIdx.y * gridDim.x + blockIdx.x] (X = A).
+void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, bool a_trans, const double* B,
+                 int64_t ldb, GemmB bmode, double* C, int64_t ldc, GemmEpi epi, int split, int64_t slice_stride,
+                 double* loss_part, int64_t m_valid, int64_t n_valid, const State* st, hipStream_t stream);
+// out[i] = sum_z parts[z*stride + i] (fixed order) for i < count.
+void launch_sum_slices(const double* parts, int split, int64_t stride, int64_t count, double* out,
+                       const State* st, hipStream_t stream);
+// out[0] = sum(v[0..n)) in a fixed order (one workgroup).
+void launch_sum_vector(const double* v, int64_t n, double* out, const State* st, hipStream_t stream);
+
+// --- step.hip ---------------------------------------------------------------
+void launch_reduce_check(const double* Mt, const double* W, const double* Z, const Params* pr, State* st,
+                         double* partials, int64_t d, int64_t D, hipStream_t stream);
+void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
+                    const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
+                    hipStream_t stream);
+void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
+                         const double* Mt, const double* Z, const double* cov, const double* minc,
+                         const double* mexc, int64_t d, int64_t D, hipStream_t stream);
+// y = a * x elementwise over n doubles
+void launch_scale(const double* x, double a, double* y, int64_t n, hipStream_t stream);
+// G = 2 * W * Mt on the logical block (linear.py:115)
+void launch_h_grad(const double* W, const double* Mt, double* G, int64_t d, int64_t D, hipStream_t stream);
+// out[0] = sum over logical block of (I - W) * Z, out[1] = sum |W|   (one pass, fixed order)
+void launch_trace_l1(const double* W, const double* Z, double* partials, int64_t d, int64_t D,
+                     hipStream_t stream);
+
+}  // namespace midagma

@@ -1,0 +1,791 @@
+// Host orchestration + C ABI (include/midagma_hip.h).
+//
+// One "slot" = one pass of the reference's loop body (linear.py:225-331):
+//   part 1  build (sI - W∘W)^T -> blocked GJ inverse (+ log|pivots|) -> score GEMM(s)
+//   part 2  domain check / checkpoint partials -> control (1 WG) -> fused update
+// The control decision lives in device memory, so slots are replayed from a
+// hipGraph in batches with no host round trip per step; the host only polls
+// the state every batch.  Slots after termination are
+// no-ops (every kernel early-exits on the status word).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/midagma_hip.h"
+#include "launch.h"
+
+using namespace midagma;
+
+namespace {
+thread_local std::string g_global_error;
+
+struct DevBuf {
+  double* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    if (count <= n && p) return;
+    release();
+    HIP_TRY(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(double)));
+    n = count;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+}  // namespace
+
+struct midagma_solver {
+  int loss = 0, mode = 0, device = 0;
+  int64_t d = 0, D = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+
+  DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp;
+  double* zbuf = nullptr;  // d x d (+64 tail) score partial; internal or bound
+  int64_t zbuf_cap = 0;
+  // data mode
+  DevBuf X, Y, Zparts, loss_part;
+  int64_t n_local = 0, n_pad = 0, n_global = 0;
+  int split = 1;
+  int64_t loss_part_count = 0;
+
+  Params* d_params = nullptr;
+  State* d_state = nullptr;
+  CkptRec* d_ckpt = nullptr;
+  int64_t ckpt_cap = 0;
+  State* h_state = nullptr;  // pinned, 2 snapshots
+  hipEvent_t ev[2] = {nullptr, nullptr};
+
+  double bc_b1 = -1, bc_b2 = -1;
+  int64_t bc_len = 0;
+  bool has_cov = false, has_data = false, has_inc = false, has_exc = false;
+  bool begun = false;
+  double mu = 1.0;
+  Params hp{};
+
+  hipGraphExec_t g_part1 = nullptr, g_part2 = nullptr, g_full = nullptr;
+  bool graphs_valid = false;
+
+  ~midagma_solver() {
+    destroy_graphs();
+    for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
+                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part})
+      b->release();
+    if (d_params) (void)hipFree(d_params);
+    if (d_state) (void)hipFree(d_state);
+    if (d_ckpt) (void)hipFree(d_ckpt);
+    if (h_state) (void)hipHostFree(h_state);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+  }
+
+  void destroy_graphs() {
+    for (hipGraphExec_t* ge : {&g_part1, &g_part2, &g_full})
+      if (*ge) {
+        (void)hipGraphExecDestroy(*ge);
+        *ge = nullptr;
+      }
+    graphs_valid = false;
+  }
+
+  GJWork gj() { return GJWork{P.p, R.p, C.p, pivlog.p}; }
+
+  // ---- the slot -----------------------------------------------------------
+  void enqueue_part1() {
+    launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, hp.s, d_state, stream);
+    launch_gj_inverse(Mt.p, D, gj(), d_state, stream);
+    if (mode == MIDAGMA_MODE_COV) {
+      // rhs = ((-mu) cov) @ (I - W)    (linear.py:244)
+      launch_gemm(D, D, D, covs.p, D, false, W.p, D, B_IMINUS, zbuf, D, EPI_STORE, 1, 0, nullptr, 0, 0, d_state,
+                  stream);
+    } else {
+      enqueue_data_partial(W.p, d_state);
+    }
+  }
+
+  // Z_k = X_k^T (X_k (I - W))  (l2)   or   X_k^T expit(X_k W)  (logistic, + loss partial)
+  void enqueue_data_partial(const double* Wp, const State* st) {
+    if (loss == MIDAGMA_LOSS_L2) {
+      launch_gemm(n_pad, D, D, X.p, D, false, Wp, D, B_IMINUS, Y.p, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
+    } else {
+      launch_gemm(n_pad, D, D, X.p, D, false, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, 1, 0, loss_part.p, n_local, d,
+                  st, stream);
+      launch_sum_vector(loss_part.p, loss_part_count, zbuf + D * D, st, stream);
+    }
+    if (split == 1) {
+      launch_gemm(D, D, n_pad, X.p, D, true, Y.p, D, B_PLAIN, zbuf, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
+    } else {
+      launch_gemm(D, D, n_pad, X.p, D, true, Y.p, D, B_PLAIN, Zparts.p, D, EPI_STORE, split, D * D, nullptr, 0, 0,
+                  st, stream);
+      launch_sum_slices(Zparts.p, split, D * D, D * D, zbuf, st, stream);
+    }
+  }
+
+  void enqueue_part2() {
+    launch_reduce_check(Mt.p, W.p, zbuf, d_params, d_state, partials.p, d, D, stream);
+    launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, stream);
+    launch_fused_update(d_params, d_state, W.p, m.p, v.p, g.p, Mt.p, zbuf, cov.p, has_inc ? minc.p : nullptr,
+                        has_exc ? mexc.p : nullptr, d, D, stream);
+  }
+
+  hipGraphExec_t capture(int which) {
+    hipGraph_t graph = nullptr;
+    HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    try {
+      if (which & 1) enqueue_part1();
+      if (which & 2) enqueue_part2();
+    } catch (...) {
+      (void)hipStreamEndCapture(stream, &graph);
+      if (graph) (void)hipGraphDestroy(graph);
+      throw;
+    }
+    HIP_TRY(hipStreamEndCapture(stream, &graph));
+    hipGraphExec_t exec = nullptr;
+    HIP_TRY(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    HIP_TRY(hipGraphDestroy(graph));
+    return exec;
+  }
+
+  void ensure_graphs() {
+    if (graphs_valid) return;
+    destroy_graphs();
+    g_full = capture(3);
+    g_part1 = capture(1);
+    g_part2 = capture(2);
+    graphs_valid = true;
+  }
+
+  // ---- buffers -------------------------------------------------------------
+  void alloc_core() {
+    const size_t DD = (size_t)D * D;
+    for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs}) {
+      b->alloc(DD);
+      HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
+    }
+    P.alloc(64 * 64);
+    R.alloc((size_t)64 * D);
+    C.alloc((size_t)D * 64);
+    pivlog.alloc(D);
+    partials.alloc(2 * NRED);
+    zown.alloc(DD + 64);
+    HIP_TRY(hipMemsetAsync(zown.p, 0, (DD + 64) * sizeof(double), stream));
+    zbuf = zown.p;
+    zbuf_cap = (int64_t)DD + 64;
+    HIP_TRY(hipMalloc(&d_params, sizeof(Params)));
+    HIP_TRY(hipMalloc(&d_state, sizeof(State)));
+    HIP_TRY(hipHostMalloc(&h_state, 2 * sizeof(State), hipHostMallocDefault));
+    for (auto& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+
+  void upload_matrix(DevBuf& dst, const double* src, int64_t ld_src) {
+    HIP_TRY(hipMemcpy2DAsync(dst.p, D * sizeof(double), src, ld_src * sizeof(double), d * sizeof(double), d,
+                             hipMemcpyHostToDevice, stream));
+  }
+
+  void download_matrix(double* dst, const double* src) {
+    HIP_TRY(hipMemcpy2DAsync(dst, d * sizeof(double), src, D * sizeof(double), d * sizeof(double), d,
+                             hipMemcpyDeviceToHost, stream));
+  }
+
+  void ensure_bc_table(double b1, double b2, int64_t max_iter) {
+    if (b1 == bc_b1 && b2 == bc_b2 && max_iter <= bc_len) return;
+    const int64_t len = std::max<int64_t>(max_iter, 1);
+    std::vector<double> t(2 * len);
+    for (int64_t it = 1; it <= len; ++it) {  // (1 - beta ** iter) exactly as Python computes it (linear.py:160-161)
+      t[2 * (it - 1)] = 1 - ::pow(b1, (double)it);
+      t[2 * (it - 1) + 1] = 1 - ::pow(b2, (double)it);
+    }
+    bc_table.alloc(2 * len);
+    HIP_TRY(hipMemcpy(bc_table.p, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+    bc_b1 = b1;
+    bc_b2 = b2;
+    bc_len = len;
+    graphs_valid = false;  // table pointer may have changed
+  }
+
+  void ensure_ckpt(int64_t max_iter, int64_t checkpoint) {
+    const int64_t need = max_iter / std::max<int64_t>(checkpoint, 1) + 4;
+    if (need <= ckpt_cap) return;
+    if (d_ckpt) HIP_TRY(hipFree(d_ckpt));
+    HIP_TRY(hipMalloc(&d_ckpt, need * sizeof(CkptRec)));
+    ckpt_cap = need;
+    graphs_valid = false;
+  }
+
+  void begin(const double* Wh, double mu_, int64_t max_iter, double s, double lr, double tol, double b1, double b2,
+             double lambda1, int64_t checkpoint) {
+    if (mode == MIDAGMA_MODE_COV && !has_cov) throw std::invalid_argument("set_cov before minimize");
+    if (mode == MIDAGMA_MODE_DATA && !has_data) throw std::invalid_argument("set_data before minimize");
+    if (loss == MIDAGMA_LOSS_LOGISTIC && !has_cov) throw std::invalid_argument("logistic needs cov (cov_from_zbuf)");
+    if (max_iter < 1 || checkpoint < 1) throw std::invalid_argument("max_iter and checkpoint must be >= 1");
+    mu = mu_;
+    ensure_bc_table(b1, b2, max_iter);
+    ensure_ckpt(max_iter, checkpoint);
+    Params p{};
+    p.mu = mu_;
+    p.s = s;
+    p.lambda1 = lambda1;
+    p.tol = tol;
+    p.beta1 = b1;
+    p.beta2 = b2;
+    p.c1 = 1 - b1;
+    p.c2 = 1 - b2;
+    p.mu_l1 = mu_ * lambda1;
+    p.d_log_s = (double)d * std::log(s);
+    p.max_iter = max_iter;
+    p.checkpoint = checkpoint;
+    p.d = d;
+    p.D = D;
+    p.ld_table = bc_len;
+    p.has_inc = has_inc;
+    p.has_exc = has_exc;
+    p.logistic = loss == MIDAGMA_LOSS_LOGISTIC;
+    const double n = (double)n_global;
+    if (mode == MIDAGMA_MODE_COV) {
+      p.zscale = 1.0;  // Z already is ((-mu) cov) @ (I - W)
+      p.cscale = 0.0;
+      p.score_scale = 0.5 / (-mu_);
+    } else if (loss == MIDAGMA_LOSS_L2) {
+      p.zscale = -mu_ / n;
+      p.cscale = 0.0;
+      p.score_scale = 0.5 / n;
+    } else {
+      p.zscale = mu_ / n;
+      p.cscale = -mu_;
+      p.score_scale = 0.0;
+      p.logit_scale = 1.0 / n;
+    }
+    hp = p;
+    HIP_TRY(hipMemcpyAsync(d_params, &hp, sizeof(Params), hipMemcpyHostToDevice, stream));
+    State st{};
+    st.status = ST_RUNNING;
+    st.lr = lr;
+    st.obj_prev = 1e16;
+    h_state[0] = st;
+    HIP_TRY(hipMemcpyAsync(d_state, &h_state[0], sizeof(State), hipMemcpyHostToDevice, stream));
+    if (mode == MIDAGMA_MODE_COV) launch_scale(cov.p, -mu_, covs.p, D * D, stream);  // (-mu) * cov
+    upload_matrix(W, Wh, d);
+    const size_t DD = (size_t)D * D;
+    for (DevBuf* b : {&m, &v, &g}) HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
+    HIP_TRY(hipStreamSynchronize(stream));  // h_state[0] reused as a snapshot slot below
+    begun = true;
+  }
+
+  void snapshot(int slot) {
+    HIP_TRY(hipMemcpyAsync(&h_state[slot], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipEventRecord(ev[slot], stream));
+  }
+
+  static bool terminal(const State& s) { return s.status != ST_RUNNING; }
+
+  void run_loop(int64_t max_iter, int64_t checkpoint) {
+    ensure_graphs();
+    const int64_t cap = max_iter + max_iter / std::max<int64_t>(checkpoint, 1) + 512;
+    int64_t launched = 0, known_iter = 0;
+    int cur = 0, pending = -1;
+    bool stop = false;
+    while (!stop) {
+      int64_t B = std::min<int64_t>(64, std::max<int64_t>(2, max_iter - known_iter + 2));
+      for (int64_t b = 0; b < B; ++b) HIP_TRY(hipGraphLaunch(g_full, stream));
+      launched += B;
+      snapshot(cur);
+      if (pending >= 0) {
+        HIP_TRY(hipEventSynchronize(ev[pending]));
+        known_iter = h_state[pending].iter;
+        if (terminal(h_state[pending])) stop = true;
+      }
+      pending = cur;
+      cur ^= 1;
+      if (!stop && launched > cap) throw std::runtime_error("minimize: slot budget exceeded (controller stuck)");
+    }
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
+
+  void finish(double* Wh, midagma_result* res) {
+    HIP_TRY(hipMemcpyAsync(&h_state[0], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
+    download_matrix(Wh, W.p);
+    HIP_TRY(hipStreamSynchronize(stream));
+    fill_result(h_state[0], res);
+    begun = false;
+  }
+
+  static void fill_result(const State& s, midagma_result* res) {
+    if (!res) return;
+    res->iters = s.iter;
+    res->halvings = s.halvings;
+    res->slots = s.slots;
+    res->n_checkpoints = s.n_ckpt;
+    res->status = s.status;
+    res->early_stop = s.early_stop;
+    res->lr_final = s.lr;
+    res->obj_last = s.obj_last;
+    res->score_last = s.score_last;
+    res->h_last = s.h_last;
+    res->l1_last = s.l1_last;
+  }
+};
+
+namespace {
+
+__global__ void div_kernel(const double* __restrict__ x, double n, double* __restrict__ y, int64_t count) {
+  for (int64_t i = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; i < count; i += (int64_t)gridDim.x * NTHREADS)
+    y[i] = x[i] / n;
+}
+
+int fail(midagma_solver* s, int code, const std::string& msg) {
+  if (s)
+    s->err = msg;
+  else
+    g_global_error = msg;
+  return code;
+}
+
+template <class F>
+int guarded(midagma_solver* s, F&& f) {
+  try {
+    if (s) HIP_TRY(hipSetDevice(s->device));
+    return f();
+  } catch (const HipError& e) {
+    return fail(s, MIDAGMA_E_HIP, e.what());
+  } catch (const std::invalid_argument& e) {
+    return fail(s, MIDAGMA_E_ARG, e.what());
+  } catch (const std::exception& e) {
+    return fail(s, MIDAGMA_E_STATE, e.what());
+  }
+}
+
+std::once_flag g_attr_once;
+void setup_attributes_once() {
+  std::call_once(g_attr_once, [] {
+    gj_setup_attributes();
+    gemm_setup_attributes();
+  });
+}
+
+}  // namespace
+
+extern "C" {
+
+int midagma_abi_version(void) { return MIDAGMA_ABI_VERSION; }
+
+int midagma_device_count(int* n) {
+  return guarded(nullptr, [&] {
+    HIP_TRY(hipGetDeviceCount(n));
+    return MIDAGMA_OK;
+  });
+}
+
+const char* midagma_last_error(const midagma_solver* s) { return s ? s->err.c_str() : g_global_error.c_str(); }
+
+int midagma_create(midagma_solver** out, int loss, int mode, int64_t d, int device, void* stream) {
+  if (!out || d < 1 || (loss != 0 && loss != 1) || (mode != 0 && mode != 1) ||
+      (loss == MIDAGMA_LOSS_LOGISTIC && mode == MIDAGMA_MODE_COV))
+    return fail(nullptr, MIDAGMA_E_ARG, "midagma_create: bad arguments (logistic needs data mode)");
+  midagma_solver* s = new midagma_solver();
+  s->loss = loss;
+  s->mode = mode;
+  s->d = d;
+  s->D = round_up64(d);
+  s->device = device;
+  int rc = guarded(s, [&] {
+    setup_attributes_once();
+    if (stream) {
+      s->stream = reinterpret_cast<hipStream_t>(stream);
+    } else {
+      HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+      s->own_stream = true;
+    }
+    s->alloc_core();
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
+  if (rc != MIDAGMA_OK) {
+    g_global_error = s->err;
+    delete s;
+    return rc;
+  }
+  *out = s;
+  return MIDAGMA_OK;
+}
+
+void midagma_destroy(midagma_solver* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  delete s;
+}
+
+void* midagma_stream(midagma_solver* s) { return s ? reinterpret_cast<void*>(s->stream) : nullptr; }
+int64_t midagma_padded_dim(const midagma_solver* s) { return s ? s->D : 0; }
+
+int midagma_set_cov(midagma_solver* s, const double* cov, int64_t ld) {
+  if (!s || !cov || ld < s->d) return fail(s, MIDAGMA_E_ARG, "set_cov: bad arguments");
+  return guarded(s, [&] {
+    s->upload_matrix(s->cov, cov, ld);
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->has_cov = true;
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_set_masks(midagma_solver* s, const double* mask_inc, const double* mask_exc) {
+  if (!s) return fail(s, MIDAGMA_E_ARG, "set_masks: null solver");
+  return guarded(s, [&] {
+    const size_t DD = (size_t)s->D * s->D;
+    const bool inc = mask_inc != nullptr, exc = mask_exc != nullptr;
+    if (inc) {
+      s->minc.alloc(DD);
+      HIP_TRY(hipMemsetAsync(s->minc.p, 0, DD * sizeof(double), s->stream));
+      s->upload_matrix(s->minc, mask_inc, s->d);
+    }
+    if (exc) {
+      s->mexc.alloc(DD);
+      HIP_TRY(hipMemsetAsync(s->mexc.p, 0, DD * sizeof(double), s->stream));
+      s->upload_matrix(s->mexc, mask_exc, s->d);
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (inc != s->has_inc || exc != s->has_exc) s->graphs_valid = false;
+    s->has_inc = inc;
+    s->has_exc = exc;
+    s->graphs_valid = false;  // buffer pointers may have changed
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_t n_global, int on_device) {
+  if (!s || !X || n_local < 1 || n_global < n_local || s->mode != MIDAGMA_MODE_DATA)
+    return fail(s, MIDAGMA_E_ARG, "set_data: bad arguments (data mode only)");
+  return guarded(s, [&] {
+    const int64_t D = s->D;
+    s->n_local = n_local;
+    s->n_global = n_global;
+    s->n_pad = round_up64(n_local);
+    const size_t nx = (size_t)s->n_pad * D;
+    s->X.alloc(nx);
+    s->Y.alloc(nx);
+    HIP_TRY(hipMemsetAsync(s->X.p, 0, nx * sizeof(double), s->stream));
+    HIP_TRY(hipMemcpy2DAsync(s->X.p, D * sizeof(double), X, s->d * sizeof(double), s->d * sizeof(double), n_local,
+                             on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s->stream));
+    // split-K over the rows so the X^T Y GEMM fills the chip: (D/64)^2 tiles x split >= ~1024 workgroups
+    const int64_t tiles = (D / 64) * (D / 64);
+    const int64_t ktiles = s->n_pad / 64;
+    int split = (int)std::max<int64_t>(1, std::min<int64_t>(ktiles / 8, (1024 + tiles - 1) / tiles));
+    s->split = std::min(split, 32);
+    if (s->split > 1) s->Zparts.alloc((size_t)s->split * D * D);
+    s->loss_part_count = (s->n_pad / 64) * (D / 64);
+    if (s->loss == MIDAGMA_LOSS_LOGISTIC) {
+      s->loss_part.alloc(s->loss_part_count);
+      HIP_TRY(hipMemsetAsync(s->loss_part.p, 0, s->loss_part_count * sizeof(double), s->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->has_data = true;
+    s->graphs_valid = false;
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_data_gram(midagma_solver* s) {
+  if (!s || !s->has_data) return fail(s, MIDAGMA_E_STATE, "data_gram: set_data first");
+  return guarded(s, [&] {
+    const int64_t D = s->D;
+    if (s->split == 1)
+      launch_gemm(D, D, s->n_pad, s->X.p, D, true, s->X.p, D, B_PLAIN, s->zbuf, D, EPI_STORE, 1, 0, nullptr, 0, 0,
+                  nullptr, s->stream);
+    else {
+      launch_gemm(D, D, s->n_pad, s->X.p, D, true, s->X.p, D, B_PLAIN, s->Zparts.p, D, EPI_STORE, s->split, D * D,
+                  nullptr, 0, 0, nullptr, s->stream);
+      launch_sum_slices(s->Zparts.p, s->split, D * D, D * D, s->zbuf, nullptr, s->stream);
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_cov_from_zbuf(midagma_solver* s, double n) {
+  if (!s || !(n > 0)) return fail(s, MIDAGMA_E_ARG, "cov_from_zbuf: n must be > 0");
+  return guarded(s, [&] {
+    // cov = (X^T X) / float(n), a division as in linear.py:428
+    const int64_t DD = s->D * s->D;
+    hipLaunchKernelGGL(div_kernel, dim3(4096), dim3(NTHREADS), 0, s->stream, s->zbuf, n, s->cov.p, DD);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->has_cov = true;
+    return MIDAGMA_OK;
+  });
+}
+
+int64_t midagma_zbuf_len(const midagma_solver* s) { return s ? s->D * s->D + 64 : 0; }
+
+int midagma_bind_zbuf(midagma_solver* s, void* dev_ptr, int64_t len) {
+  if (!s || len < s->D * s->D + 64) return fail(s, MIDAGMA_E_ARG, "bind_zbuf: buffer too small");
+  return guarded(s, [&] {
+    s->zbuf = dev_ptr ? static_cast<double*>(dev_ptr) : s->zown.p;
+    s->graphs_valid = false;
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_minimize(midagma_solver* s, double* W, double mu, int64_t max_iter, double s_dom, double lr, double tol,
+                     double beta1, double beta2, double lambda1, int64_t checkpoint, midagma_result* res) {
+  if (!s || !W) return fail(s, MIDAGMA_E_ARG, "minimize: null argument");
+  int rc = guarded(s, [&] {
+    s->begin(W, mu, max_iter, s_dom, lr, tol, beta1, beta2, lambda1, checkpoint);
+    s->run_loop(max_iter, checkpoint);
+    s->finish(W, res);
+    return MIDAGMA_OK;
+  });
+  if (rc == MIDAGMA_OK && res && res->status == MIDAGMA_ST_SINGULAR)
+    return fail(s, MIDAGMA_E_SINGULAR, "singular matrix: inverse of sI - W*W is not finite");
+  return rc;
+}
+
+int midagma_begin(midagma_solver* s, const double* W, double mu, int64_t max_iter, double s_dom, double lr,
+                  double tol, double beta1, double beta2, double lambda1, int64_t checkpoint) {
+  if (!s || !W) return fail(s, MIDAGMA_E_ARG, "begin: null argument");
+  return guarded(s, [&] {
+    s->begin(W, mu, max_iter, s_dom, lr, tol, beta1, beta2, lambda1, checkpoint);
+    s->ensure_graphs();
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_run_slots(midagma_solver* s, int64_t n) {
+  if (!s || !s->begun || n < 0) return fail(s, MIDAGMA_E_STATE, "run_slots: call begin first");
+  return guarded(s, [&] {
+    for (int64_t i = 0; i < n; ++i) HIP_TRY(hipGraphLaunch(s->g_full, s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_sync(midagma_solver* s) {
+  if (!s) return fail(s, MIDAGMA_E_ARG, "null solver");
+  return guarded(s, [&] {
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_step_partial(midagma_solver* s) {
+  if (!s || !s->begun) return fail(s, MIDAGMA_E_STATE, "step_partial: call begin first");
+  return guarded(s, [&] {
+    HIP_TRY(hipGraphLaunch(s->g_part1, s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_step_finish(midagma_solver* s) {
+  if (!s || !s->begun) return fail(s, MIDAGMA_E_STATE, "step_finish: call begin first");
+  return guarded(s, [&] {
+    HIP_TRY(hipGraphLaunch(s->g_part2, s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_poll(midagma_solver* s, midagma_result* res) {
+  if (!s) return fail(s, MIDAGMA_E_ARG, "null solver");
+  return guarded(s, [&] {
+    HIP_TRY(hipMemcpyAsync(&s->h_state[1], s->d_state, sizeof(State), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    midagma_solver::fill_result(s->h_state[1], res);
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_end(midagma_solver* s, double* W, midagma_result* res) {
+  if (!s || !W || !s->begun) return fail(s, MIDAGMA_E_STATE, "end: call begin first");
+  int rc = guarded(s, [&] {
+    s->finish(W, res);
+    return MIDAGMA_OK;
+  });
+  if (rc == MIDAGMA_OK && res && res->status == MIDAGMA_ST_SINGULAR)
+    return fail(s, MIDAGMA_E_SINGULAR, "singular matrix: inverse of sI - W*W is not finite");
+  return rc;
+}
+
+int64_t midagma_checkpoints(midagma_solver* s, midagma_ckpt* out, int64_t cap) {
+  if (!s || !s->d_ckpt) return 0;
+  int64_t n = 0;
+  int rc = guarded(s, [&] {
+    State st{};
+    HIP_TRY(hipMemcpy(&st, s->d_state, sizeof(State), hipMemcpyDeviceToHost));
+    n = std::min<int64_t>(std::min<int64_t>(st.n_ckpt, s->ckpt_cap), cap);
+    static_assert(sizeof(midagma_ckpt) == sizeof(CkptRec), "ckpt layout");
+    if (n > 0 && out) HIP_TRY(hipMemcpy(out, s->d_ckpt, n * sizeof(CkptRec), hipMemcpyDeviceToHost));
+    return MIDAGMA_OK;
+  });
+  return rc == MIDAGMA_OK ? n : rc;
+}
+
+int midagma_h(midagma_solver* s, const double* W, double s_dom, double* h, double* G) {
+  if (!s || !W || !h) return fail(s, MIDAGMA_E_ARG, "h: null argument");
+  return guarded(s, [&] {
+    const int64_t D = s->D, d = s->d, DD = D * D;
+    s->scratch.alloc(DD);
+    HIP_TRY(hipMemsetAsync(s->scratch.p, 0, DD * sizeof(double), s->stream));
+    s->upload_matrix(s->scratch, W, d);
+    DevBuf work;
+    work.alloc(DD);
+    launch_build_at(s->scratch.p, D, true, work.p, D, d, s_dom, nullptr, s->stream);
+    launch_gj_inverse(work.p, D, s->gj(), nullptr, s->stream);
+    std::vector<double> pl(D);
+    HIP_TRY(hipMemcpyAsync(pl.data(), s->pivlog.p, D * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    if (G) {
+      s->Gtmp.alloc((size_t)d * d);
+      launch_h_grad(s->scratch.p, work.p, s->Gtmp.p, d, D, s->stream);
+      HIP_TRY(hipMemcpyAsync(G, s->Gtmp.p, (size_t)d * d * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    work.release();
+    double ld = 0.0;
+    for (int64_t i = 0; i < d; ++i) ld += pl[i];
+    *h = -ld + (double)d * std::log(s_dom);
+    return MIDAGMA_OK;
+  });
+}
+
+static void host_trace_l1(midagma_solver* s, const double* Wd, const double* Z, double* sd, double* l1) {
+  launch_trace_l1(Wd, Z, s->partials.p, s->d, s->D, s->stream);
+  std::vector<double> part(2 * NRED);
+  HIP_TRY(hipMemcpyAsync(part.data(), s->partials.p, part.size() * sizeof(double), hipMemcpyDeviceToHost,
+                         s->stream));
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  double a = 0.0, b = 0.0;
+  for (int i = 0; i < NRED; ++i) {
+    a += part[2 * i];
+    b += part[2 * i + 1];
+  }
+  *sd = a;
+  if (l1) *l1 = b;
+}
+
+int midagma_score(midagma_solver* s, const double* W, double* loss, double* G) {
+  if (!s || !W || !loss) return fail(s, MIDAGMA_E_ARG, "score: null argument");
+  if (s->mode != MIDAGMA_MODE_COV || !s->has_cov) return fail(s, MIDAGMA_E_STATE, "score: cov mode with set_cov");
+  return guarded(s, [&] {
+    const int64_t D = s->D, d = s->d, DD = D * D;
+    s->scratch.alloc(DD);
+    HIP_TRY(hipMemsetAsync(s->scratch.p, 0, DD * sizeof(double), s->stream));
+    s->upload_matrix(s->scratch, W, d);
+    DevBuf rhs;
+    rhs.alloc(DD);
+    launch_gemm(D, D, D, s->cov.p, D, false, s->scratch.p, D, B_IMINUS, rhs.p, D, EPI_STORE, 1, 0, nullptr, 0, 0,
+                nullptr, s->stream);  // rhs = cov @ (I - W)   (linear.py:85-86)
+    double sd = 0;
+    host_trace_l1(s, s->scratch.p, rhs.p, &sd, nullptr);
+    *loss = 0.5 * sd;
+    if (G) {
+      s->Gtmp.alloc((size_t)d * d);
+      launch_scale(rhs.p, -1.0, rhs.p, DD, s->stream);  // G_loss = -rhs
+      s->download_matrix(G, rhs.p);
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    rhs.release();
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_score_partial(midagma_solver* s, const double* W) {
+  if (!s || !W || s->mode != MIDAGMA_MODE_DATA || !s->has_data)
+    return fail(s, MIDAGMA_E_STATE, "score_partial: data mode with set_data");
+  return guarded(s, [&] {
+    const int64_t DD = s->D * s->D;
+    s->scratch.alloc(DD);
+    HIP_TRY(hipMemsetAsync(s->scratch.p, 0, DD * sizeof(double), s->stream));
+    s->upload_matrix(s->scratch, W, s->d);
+    HIP_TRY(hipMemsetAsync(s->zbuf + DD, 0, 64 * sizeof(double), s->stream));
+    // Force loss partials: pass no state (st == nullptr computes them unconditionally).
+    s->enqueue_data_partial(s->scratch.p, nullptr);
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_score_finish(midagma_solver* s, double* loss, double* G) {
+  if (!s || !loss || s->mode != MIDAGMA_MODE_DATA) return fail(s, MIDAGMA_E_STATE, "score_finish: data mode");
+  return guarded(s, [&] {
+    const int64_t D = s->D, d = s->d, DD = D * D;
+    const double n = (double)s->n_global;
+    if (s->loss == MIDAGMA_LOSS_L2) {
+      // loss = 0.5 tr((I-W)^T cov (I-W)) with cov (I-W) = Z / n ; G = -Z / n
+      double sd = 0;
+      host_trace_l1(s, s->scratch.p, s->zbuf, &sd, nullptr);
+      *loss = 0.5 * (sd / n);
+      if (G) {
+        std::vector<double> z((size_t)d * d);
+        s->download_matrix(z.data(), s->zbuf);
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (size_t i = 0; i < z.size(); ++i) G[i] = -(z[i] / n);
+      }
+    } else {
+      double tail = 0;
+      HIP_TRY(hipMemcpyAsync(&tail, s->zbuf + DD, sizeof(double), hipMemcpyDeviceToHost, s->stream));
+      HIP_TRY(hipStreamSynchronize(s->stream));
+      *loss = 1.0 / n * tail;
+      if (G) {
+        std::vector<double> z((size_t)d * d), c((size_t)d * d);
+        s->download_matrix(z.data(), s->zbuf);
+        s->download_matrix(c.data(), s->cov.p);
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (size_t i = 0; i < z.size(); ++i) G[i] = (1.0 / n) * z[i] - c[i];
+      }
+    }
+    return MIDAGMA_OK;
+  });
+}
+
+}  // extern "C"
+
+// ---- device-pointer log-det / inverse for torch (DagmaMLP.h_func) ------------
+namespace {
+struct LogdetWorkspace {
+  int device = -1;
+  int64_t D = 0;
+  DevBuf A, P, R, C, piv;
+};
+std::mutex g_ws_mu;
+std::vector<LogdetWorkspace*> g_ws;
+}  // namespace
+
+extern "C" int midagma_logdet_inv_dev(const double* A, int64_t d, int64_t lda, double s_dom, double* logdet_dev,
+                                      double* Mt_dev, int64_t ldm, void* stream) {
+  if (!A || d < 1 || lda < d || (Mt_dev && ldm < d))
+    return fail(nullptr, MIDAGMA_E_ARG, "logdet_inv_dev: bad arguments");
+  return guarded(nullptr, [&] {
+    setup_attributes_once();
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    const int64_t D = round_up64(d);
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    LogdetWorkspace* ws = nullptr;
+    for (auto* w : g_ws)
+      if (w->device == dev && w->D == D) ws = w;
+    if (!ws) {
+      ws = new LogdetWorkspace();
+      ws->device = dev;
+      ws->D = D;
+      ws->A.alloc((size_t)D * D);
+      ws->P.alloc(64 * 64);
+      ws->R.alloc((size_t)64 * D);
+      ws->C.alloc((size_t)D * 64);
+      ws->piv.alloc(D);
+      g_ws.push_back(ws);
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    launch_build_at(A, lda, false, ws->A.p, D, d, s_dom, nullptr, st);
+    launch_gj_inverse(ws->A.p, D, GJWork{ws->P.p, ws->R.p, ws->C.p, ws->piv.p}, nullptr, st);
+    if (logdet_dev) launch_sum_vector(ws->piv.p, d, logdet_dev, nullptr, st);
+    if (Mt_dev)
+      HIP_TRY(hipMemcpy2DAsync(Mt_dev, ldm * sizeof(double), ws->A.p, D * sizeof(double), d * sizeof(double), d,
+                               hipMemcpyDeviceToDevice, st));
+    return MIDAGMA_OK;
+  });
+}

@@ -1,0 +1,276 @@
+// Per-step control and the fused elementwise update (linear.py:224-331).
+//
+// reduce_check : domain test any(inv + 1e-16 < 0) (linear.py:226-230) and, on
+//                checkpoint slots, the score / L1 partial sums (linear.py:85-87, 129)
+// control      : one workgroup; deterministic sums, checkpoint objective and
+//                tolerance test (linear.py:279-331), the out-of-domain branch
+//                with lr halving (linear.py:230-241), Adam bias terms
+// fused_update : G_obj (linear.py:248) -> Adam (138-163) -> W -= lr g; W *= mask
+//                (275-276), or the line-search W += lr g; W -= (lr/2) g.
+// Elementwise arithmetic keeps numpy's operation order; the library is built
+// with -ffp-contract=off so no multiply-add is fused behind our back.
+#include "launch.h"
+
+namespace midagma {
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = NTHREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(NTHREADS) void reduce_check_kernel(const double* __restrict__ Mt,
+                                                                const double* __restrict__ W,
+                                                                const double* __restrict__ Z,
+                                                                State* __restrict__ st,
+                                                                double* __restrict__ partials, int64_t d,
+                                                                int64_t D) {
+  if (st->status != ST_RUNNING) return;
+  __shared__ double red[NTHREADS];
+  __shared__ int flag_sh;
+  if (threadIdx.x == 0) flag_sh = 0;
+  const bool ck = st->ckpt_pending != 0;
+  int flag = 0;
+  double sd = 0.0, l1 = 0.0;
+  for (int64_t i = blockIdx.x; i < d; i += gridDim.x) {
+    for (int64_t j = threadIdx.x; j < d; j += NTHREADS) {
+      const int64_t idx = i * D + j;
+      const double m = Mt[idx];
+      if (m + 1e-16 < 0.0) flag |= 1;
+      if (!isfinite(m)) flag |= 2;
+      if (ck) {
+        const double w = W[idx];
+        sd += (((i == j) ? 1.0 : 0.0) - w) * Z[idx];
+        l1 += fabs(w);
+      }
+    }
+  }
+  __syncthreads();
+  if (flag) atomicOr(&flag_sh, flag);
+  const double s_sd = block_sum(sd, red);
+  const double s_l1 = block_sum(l1, red);
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = s_sd;
+    partials[2 * blockIdx.x + 1] = s_l1;
+    if (flag_sh) atomicOr(&st->flags, flag_sh);
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restrict__ pr, State* __restrict__ st,
+                                                           const double* __restrict__ partials,
+                                                           const double* __restrict__ pivlog,
+                                                           const double* __restrict__ loss_total,
+                                                           const double* __restrict__ bc_table,
+                                                           CkptRec* __restrict__ ckpt, int64_t ckpt_cap) {
+  if (st->status != ST_RUNNING) {
+    if (threadIdx.x == 0) st->action = ACT_NOOP;
+    return;
+  }
+  __shared__ double red[NTHREADS];
+  const bool ck = st->ckpt_pending != 0;
+  double sd = 0.0, l1 = 0.0, ld = 0.0;
+  if (ck) {
+    for (int i = threadIdx.x; i < NRED; i += NTHREADS) {
+      sd += partials[2 * i];
+      l1 += partials[2 * i + 1];
+    }
+    for (int64_t i = threadIdx.x; i < pr->d; i += NTHREADS) ld += pivlog[i];
+    sd = block_sum(sd, red);
+    l1 = block_sum(l1, red);
+    ld = block_sum(ld, red);
+  }
+  if (threadIdx.x != 0) return;
+  st->slots += 1;
+  const int flags = st->flags;
+  st->flags = 0;
+  if (ck) {
+    st->ckpt_pending = 0;
+    const double h = -ld + pr->d_log_s;
+    const double score = pr->logistic ? loss_total[0] * pr->logit_scale : pr->score_scale * sd;
+    const double obj = pr->mu * (score + pr->lambda1 * l1) + h;
+    if (st->n_ckpt < ckpt_cap) {
+      CkptRec& r = ckpt[st->n_ckpt];
+      r.iter = st->iter;
+      r.obj = obj;
+      r.score = score;
+      r.h = h;
+      r.lr = st->lr;
+      r.l1 = l1;
+    }
+    st->n_ckpt += 1;
+    st->obj_last = obj;
+    st->score_last = score;
+    st->h_last = h;
+    st->l1_last = l1;
+    if (fabs((st->obj_prev - obj) / st->obj_prev) <= pr->tol) {
+      st->status = ST_DONE;
+      st->early_stop = 1;
+      st->action = ACT_NOOP;
+      return;
+    }
+    st->obj_prev = obj;
+    if (st->iter >= pr->max_iter) {
+      st->status = ST_DONE;
+      st->action = ACT_NOOP;
+      return;
+    }
+  }
+  if (flags & 2) {
+    st->status = ST_SINGULAR;
+    st->action = ACT_NOOP;
+    return;
+  }
+  if (flags & 1) {  // sI - W∘W is not an M-matrix (linear.py:230-241)
+    if (st->iter == 0 || pr->s <= 0.9) {
+      st->status = ST_FAILED;
+      st->action = ACT_NOOP;
+      return;
+    }
+    const double lr_old = st->lr;
+    st->lr = lr_old * .5;
+    st->halvings += 1;
+    st->lr_a = lr_old;
+    st->lr_b = st->lr;
+    if (st->lr <= 1e-16) {
+      st->status = ST_LR_UNDERFLOW;
+      st->action = ACT_REVERT;
+      return;
+    }
+    st->action = ACT_HALVE;
+    return;
+  }
+  const int64_t it = st->iter + 1;
+  st->bc1 = bc_table[2 * (it - 1)];
+  st->bc2 = bc_table[2 * (it - 1) + 1];
+  st->lr_a = st->lr;
+  st->action = ACT_STEP;
+  st->iter = it;
+  if (it % pr->checkpoint == 0 || it == pr->max_iter) st->ckpt_pending = 1;
+}
+
+__device__ __forceinline__ double sign_of(double w) { return w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : w); }
+
+__global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
+    const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
+    double* __restrict__ v, double* __restrict__ g, const double* __restrict__ Mt, const double* __restrict__ Z,
+    const double* __restrict__ cov, const double* __restrict__ minc, const double* __restrict__ mexc, int64_t d,
+    int64_t D) {
+  const int act = st->action;
+  if (act == ACT_NOOP) return;
+  const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (j >= d) return;
+  const int64_t idx = i * D + j;
+  if (act == ACT_STEP) {
+    const double w = W[idx];
+    const double mt = Mt[idx] + 1e-16;
+    double gs = pr->zscale * Z[idx];
+    if (pr->logistic) gs = gs + pr->cscale * cov[idx];
+    const double sg = sign_of(w);
+    double gobj = gs + pr->mu_l1 * sg;
+    gobj = gobj + (2.0 * w) * mt;
+    if (pr->has_inc) gobj = gobj + minc[idx] * sg;
+    const double mm = m[idx] * pr->beta1 + pr->c1 * gobj;
+    const double vv = v[idx] * pr->beta2 + pr->c2 * (gobj * gobj);
+    const double mh = mm / st->bc1;
+    const double vh = vv / st->bc2;
+    const double gd = mh / (sqrt(vh) + 1e-8);
+    double wn = w - st->lr_a * gd;
+    if (pr->has_exc) wn = wn * mexc[idx];
+    m[idx] = mm;
+    v[idx] = vv;
+    g[idx] = gd;
+    W[idx] = wn;
+  } else if (act == ACT_HALVE) {
+    const double gd = g[idx];
+    double wn = W[idx] + st->lr_a * gd;
+    W[idx] = wn - st->lr_b * gd;
+  } else {  // ACT_REVERT
+    W[idx] = W[idx] + st->lr_a * g[idx];
+  }
+}
+
+__global__ void scale_kernel(const double* __restrict__ x, double a, double* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTHREADS)
+    y[i] = a * x[i];
+}
+
+__global__ void h_grad_kernel(const double* __restrict__ W, const double* __restrict__ Mt, double* __restrict__ G,
+                              int64_t d, int64_t D) {
+  const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (j >= d) return;
+  G[i * d + j] = (2.0 * W[i * D + j]) * Mt[i * D + j];
+}
+
+__global__ __launch_bounds__(NTHREADS) void trace_l1_kernel(const double* __restrict__ W,
+                                                            const double* __restrict__ Z,
+                                                            double* __restrict__ partials, int64_t d,
+                                                            int64_t D) {
+  __shared__ double red[NTHREADS];
+  double sd = 0.0, l1 = 0.0;
+  for (int64_t i = blockIdx.x; i < d; i += gridDim.x)
+    for (int64_t j = threadIdx.x; j < d; j += NTHREADS) {
+      const int64_t idx = i * D + j;
+      const double w = W[idx];
+      sd += (((i == j) ? 1.0 : 0.0) - w) * Z[idx];
+      l1 += fabs(w);
+    }
+  sd = block_sum(sd, red);
+  l1 = block_sum(l1, red);
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = sd;
+    partials[2 * blockIdx.x + 1] = l1;
+  }
+}
+
+void launch_reduce_check(const double* Mt, const double* W, const double* Z, const Params*, State* st,
+                         double* partials, int64_t d, int64_t D, hipStream_t stream) {
+  hipLaunchKernelGGL(reduce_check_kernel, dim3(NRED), dim3(NTHREADS), 0, stream, Mt, W, Z, st, partials, d, D);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
+                    const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
+                    hipStream_t stream) {
+  hipLaunchKernelGGL(control_kernel, dim3(1), dim3(NTHREADS), 0, stream, pr, st, partials, pivlog, loss_total,
+                     bc_table, ckpt, ckpt_cap);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
+                         const double* Mt, const double* Z, const double* cov, const double* minc,
+                         const double* mexc, int64_t d, int64_t D, hipStream_t stream) {
+  dim3 grid((unsigned)((d + NTHREADS - 1) / NTHREADS), (unsigned)d);
+  hipLaunchKernelGGL(fused_update_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, g, Mt, Z, cov, minc,
+                     mexc, d, D);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_scale(const double* x, double a, double* y, int64_t n, hipStream_t stream) {
+  int64_t blocks = (n + NTHREADS - 1) / NTHREADS;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(scale_kernel, dim3((unsigned)blocks), dim3(NTHREADS), 0, stream, x, a, y, n);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_h_grad(const double* W, const double* Mt, double* G, int64_t d, int64_t D, hipStream_t stream) {
+  dim3 grid((unsigned)((d + NTHREADS - 1) / NTHREADS), (unsigned)d);
+  hipLaunchKernelGGL(h_grad_kernel, grid, dim3(NTHREADS), 0, stream, W, Mt, G, d, D);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_trace_l1(const double* W, const double* Z, double* partials, int64_t d, int64_t D,
+                     hipStream_t stream) {
+  hipLaunchKernelGGL(trace_l1_kernel, dim3(NRED), dim3(NTHREADS), 0, stream, W, Z, partials, d, D);
+  HIP_TRY(hipGetLastError());
+}
+
+}  // namespace midagma

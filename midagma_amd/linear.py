@@ -1,0 +1,248 @@
+"""`DagmaLinear` with the reference's API, backed by the MI355X HIP inner solver.
+
+Drop-in for `dagma.linear.DagmaLinear` (fbleile/midagma, src/dagma/linear.py):
+the constructor, `fit()` (linear.py:335-462) and the path-following outer loop
+stay in Python exactly as the reference has them; `minimize()`
+(linear.py:165-333), `_h` (97-116) and `_score` (70-94) run on the GPU through
+the C ABI.  Extra keyword-only constructor arguments:
+
+* ``score_mode``  'cov' (default for l2: cov = X^T X / n precomputed, as the
+  reference does at linear.py:428) or 'data' (X row-sharded on the GPU(s),
+  score gradient X^T(...) every step; required for 'logistic').
+* ``device``      HIP device ordinal (default: LOCAL_RANK or 0).
+* ``process_group``  a torch.distributed group: in data mode each rank keeps
+  its row shard of X and the per-step score partial is all-reduced over it.
+
+The trek regularizer (`trek_reg`, linear.py:251-258) is out of scope for the
+GPU path; passing an enabled one raises.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+import typing
+
+import numpy as np
+
+from .solver import HipSolver, run_allreduce_minimize
+
+__all__ = ["DagmaLinear"]
+
+_log = logging.getLogger("midagma_amd")
+
+
+class _NullBar:
+    def update(self, n=1):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _progress(total):
+    try:
+        from tqdm.auto import tqdm
+        return tqdm(total=total)
+    except Exception:  # pragma: no cover
+        return _NullBar()
+
+
+class DagmaLinear:
+    """DAGMA for linear SEMs: the reference's interface, the GPU inner loop."""
+
+    def __init__(self, loss_type: str, verbose: bool = False, dtype: type = np.float64, *,
+                 trek_reg=None, logger=None, log_cfg=None, score_mode: str | None = None,
+                 device: int | None = None, process_group=None) -> None:
+        losses = ["l2", "logistic"]
+        assert loss_type in losses, f"loss_type should be one of {losses}"
+        if dtype is not np.float64:
+            raise ValueError("the HIP inner solver computes in float64 only (as the reference's cov/X)")
+        if trek_reg is not None and getattr(trek_reg, "enabled", lambda: True)():
+            raise NotImplementedError("trek regularizers are not implemented on the GPU path")
+        self.loss_type = loss_type
+        self.dtype = dtype
+        self.vprint = print if verbose else (lambda *a, **k: None)
+        self.trek_reg = trek_reg
+        self._logger = logger or _log
+        self._log_cfg = log_cfg
+        self.score_mode = score_mode or ("cov" if loss_type == "l2" else "data")
+        if self.loss_type == "logistic" and self.score_mode != "data":
+            raise ValueError("logistic loss needs score_mode='data' (the gradient depends on X every step)")
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        self.device = device
+        self.process_group = process_group
+        self._solver: HipSolver | None = None
+        self.minimize_log: list = []
+
+    # ------------------------------------------------------------------ helpers
+    def _world(self):
+        if self.score_mode != "data":
+            return 1, 0
+        try:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                return dist.get_world_size(self.process_group), dist.get_rank(self.process_group)
+        except Exception:  # pragma: no cover
+            pass
+        return 1, 0
+
+    def _setup_solver(self):
+        world, rank = self._world()
+        s = HipSolver(self.d, self.loss_type, self.score_mode, device=self.device)
+        if self.score_mode == "data":
+            lo, hi = _row_range(self.n, world, rank)
+            s.set_data(np.ascontiguousarray(self.X[lo:hi]), n_global=self.n)
+            if world > 1:
+                import torch
+                import torch.distributed as dist
+                ext = torch.cuda.ExternalStream(s.stream, device=torch.device("cuda", self.device))
+                zt = torch.zeros(s.zbuf_len, dtype=torch.float64, device=torch.device("cuda", self.device))
+                s.bind_zbuf(zt.data_ptr(), zt.numel())
+                pg = self.process_group
+
+                def _allreduce():
+                    with torch.cuda.stream(ext):
+                        dist.all_reduce(zt, group=pg)
+
+                self._allreduce, self._zt = _allreduce, zt
+            else:
+                self._allreduce = None
+        s.set_cov(self.cov)
+        self._solver = s
+
+    # ------------------------------------------------------- reference methods
+    def _score(self, W: np.ndarray) -> typing.Tuple[float, np.ndarray]:
+        """loss and gradient of the score (linear.py:70-94), on the GPU."""
+        if self.score_mode == "cov":
+            return self._solver.score_value(W)
+        self._solver.score_partial(W)
+        if getattr(self, "_allreduce", None) is not None:
+            self._allreduce()
+        return self._solver.score_finish()
+
+    def _h(self, W: np.ndarray, s: float = 1.0) -> typing.Tuple[float, np.ndarray]:
+        """log-det acyclicity value and gradient (linear.py:97-116), on the GPU."""
+        return self._solver.h_value(W, s, grad=True)
+
+    def _func(self, W: np.ndarray, mu: float, s: float = 1.0):
+        """objective at W (linear.py:118-135); trek term is 0 (regularizer disabled)."""
+        score, _ = self._score(W)
+        h, _ = self._h(W, s)
+        obj = mu * (score + self.lambda1 * np.abs(W).sum()) + h
+        return obj, score, h, 0.0
+
+    def _adam_update(self, grad: np.ndarray, iter: int, beta_1: float, beta_2: float) -> np.ndarray:
+        """API-compatibility helper (linear.py:138-163).  Not used by `minimize`, whose
+        Adam step is fused into the GPU update kernel."""
+        self.opt_m = self.opt_m * beta_1 + (1 - beta_1) * grad
+        self.opt_v = self.opt_v * beta_2 + (1 - beta_2) * (grad ** 2)
+        m_hat = self.opt_m / (1 - beta_1 ** iter)
+        v_hat = self.opt_v / (1 - beta_2 ** iter)
+        return m_hat / (np.sqrt(v_hat) + 1e-8)
+
+    def _masks(self, mu: float):
+        """linear.py:217-222"""
+        mask_inc = mask_exc = None
+        if self.inc_c is not None:
+            mask_inc = np.zeros((self.d, self.d))
+            mask_inc[self.inc_r, self.inc_c] = -2 * mu * self.lambda1
+        if self.exc_c is not None:
+            mask_exc = np.ones((self.d, self.d), dtype=self.dtype)
+            mask_exc[self.exc_r, self.exc_c] = 0.
+        return mask_inc, mask_exc
+
+    def minimize(self, W: np.ndarray, mu: float, max_iter: int, s: float, lr: float, tol: float = 1e-6,
+                 beta_1: float = 0.99, beta_2: float = 0.999, pbar=None) -> typing.Tuple[np.ndarray, bool]:
+        """Solves argmin_{W in W^s} mu*Q(W; X) + h(W) by Adam (linear.py:165-333), on the GPU."""
+        t0 = time.time()
+        self.vprint(f'\n\nMinimize with -- mu:{mu} -- lr: {lr} -- s: {s} -- l1: {self.lambda1} '
+                    f'for {max_iter} max iterations')
+        W = np.ascontiguousarray(W, dtype=np.float64)
+        mask_inc, mask_exc = self._masks(mu)
+        self._solver.set_masks(mask_inc, mask_exc)
+        if self.score_mode == "data" and getattr(self, "_allreduce", None) is not None:
+            res = run_allreduce_minimize(self._solver, W, mu, max_iter, s, lr, tol, beta_1, beta_2,
+                                         self.lambda1, self.checkpoint, allreduce=self._allreduce)
+        else:
+            res = self._solver.minimize(W, mu, max_iter, s, lr, tol, beta_1, beta_2, self.lambda1,
+                                        self.checkpoint)
+        if res.halvings:
+            self.vprint(f'Learning rate decreased {res.halvings} time(s) to lr: {res.lr_final}')
+        if not res.success:
+            self.vprint(f'W went out of domain for s={s} at iteration {res.iters + 1}')
+        self.minimize_log.append(dict(mu=mu, s=s, lr=lr, max_iter=max_iter, iters=res.iters,
+                                      success=res.success, early_stop=res.early_stop,
+                                      halvings=res.halvings, seconds=time.time() - t0))
+        if pbar is not None:  # the reference ticks once per iteration (linear.py:329, 332)
+            pbar.update(int(max_iter) if res.early_stop else res.iters)
+        return W, res.success
+
+    def fit(self, X: np.ndarray, lambda1: float = 0.03, w_threshold: float = 0.3, T: int = 5,
+            mu_init: float = 1.0, mu_factor: float = 0.1,
+            s: typing.Union[typing.List[float], float] = [1.0, .9, .8, .7, .6],
+            warm_iter: int = 3e4, max_iter: int = 6e4, lr: float = 0.0003, checkpoint: int = 1000,
+            beta_1: float = 0.99, beta_2: float = 0.999,
+            exclude_edges: typing.Optional[typing.List[typing.Tuple[int, int]]] = None,
+            include_edges: typing.Optional[typing.List[typing.Tuple[int, int]]] = None) -> np.ndarray:
+        """Runs DAGMA and returns the thresholded weighted adjacency (linear.py:335-462)."""
+        self.X, self.lambda1, self.checkpoint = X, lambda1, checkpoint
+        self.n, self.d = X.shape
+        self.Id = np.eye(self.d).astype(self.dtype)
+        if self.loss_type == 'l2':
+            self.X -= X.mean(axis=0, keepdims=True)
+        self.exc_r, self.exc_c = None, None
+        self.inc_r, self.inc_c = None, None
+        if exclude_edges is not None:
+            if type(exclude_edges) is tuple and type(exclude_edges[0]) is tuple and \
+                    np.all(np.array([len(e) for e in exclude_edges]) == 2):
+                self.exc_r, self.exc_c = zip(*exclude_edges)
+            else:
+                ValueError("blacklist should be a tuple of edges, e.g., ((1,2), (2,3))")
+        if include_edges is not None:
+            if type(include_edges) is tuple and type(include_edges[0]) is tuple and \
+                    np.all(np.array([len(e) for e in include_edges]) == 2):
+                self.inc_r, self.inc_c = zip(*include_edges)
+            else:
+                ValueError("whitelist should be a tuple of edges, e.g., ((1,2), (2,3))")
+        self.cov = X.T @ X / float(self.n)
+        self.W_est = np.zeros((self.d, self.d)).astype(self.dtype)
+        self._setup_solver()
+        mu = mu_init
+        if type(s) == list:
+            if len(s) < T:
+                self.vprint(f"Length of s is {len(s)}, using last value in s for iteration t >= {len(s)}")
+                s = s + (T - len(s)) * [s[-1]]
+        elif type(s) in [int, float]:
+            s = T * [s]
+        else:
+            ValueError("s should be a list, int, or float.")
+        with _progress((T - 1) * warm_iter + max_iter) as pbar:
+            for i in range(int(T)):
+                self.vprint(f'\nIteration -- {i+1}:')
+                lr_adam, success = lr, False
+                inner_iters = int(max_iter) if i == T - 1 else int(warm_iter)
+                while success is False:
+                    W_temp, success = self.minimize(self.W_est.copy(), mu, inner_iters, s[i], lr=lr_adam,
+                                                    beta_1=beta_1, beta_2=beta_2, pbar=pbar)
+                    if success is False:
+                        self.vprint('Retrying with larger s')
+                        lr_adam *= 0.5
+                        s[i] += 0.1
+                self.W_est = W_temp
+                mu *= mu_factor
+        self.h_final, _ = self._h(self.W_est)
+        self.score_final, _ = self._score(self.W_est)
+        self.W_est[np.abs(self.W_est) < w_threshold] = 0
+        return self.W_est
+
+
+def _row_range(n: int, world: int, rank: int):
+    """Even row split of X over ranks (first n % world ranks take one extra row)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)

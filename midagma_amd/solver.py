@@ -1,0 +1,220 @@
+"""Python handle over the C ABI: one `HipSolver` per (fit, device).
+
+`HipSolver.minimize` is the single-process hot path (the whole inner loop runs
+on the GPU from replayed hipGraphs).  `run_allreduce_minimize` is the
+multi-rank data-parallel loop: every step the GPU computes this rank's score
+partial Z_k = X_k^T(...), the caller's all-reduce sums it over ranks
+(torch.distributed -> RCCL over xGMI), and the GPU finishes the step.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, dptr
+
+__all__ = ["HipSolver", "MinimizeResult", "run_allreduce_minimize", "device_count"]
+
+
+@dataclass
+class MinimizeResult:
+    iters: int
+    success: bool
+    status: int
+    halvings: int
+    early_stop: bool
+    lr_final: float
+    slots: int
+    obj_last: float
+    score_last: float
+    h_last: float
+    checkpoints: list = field(default_factory=list)
+
+    @classmethod
+    def from_c(cls, r: _lib.MidagmaResult, ckpts=()):
+        return cls(iters=int(r.iters), success=r.status != _lib.ST_FAILED, status=int(r.status),
+                   halvings=int(r.halvings), early_stop=bool(r.early_stop), lr_final=float(r.lr_final),
+                   slots=int(r.slots), obj_last=float(r.obj_last), score_last=float(r.score_last),
+                   h_last=float(r.h_last), checkpoints=list(ckpts))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(_lib.lib().midagma_device_count(C.byref(n)), None, "device_count")
+    return int(n.value)
+
+
+def _as_f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class HipSolver:
+    """Owns device buffers for one d and one score mode on one GPU."""
+
+    def __init__(self, d: int, loss: str = "l2", mode: str = "cov", device: int = 0, stream: int | None = None):
+        self.L = _lib.lib()
+        self.d = int(d)
+        self.loss = loss
+        self.mode = mode
+        lt = {"l2": _lib.LOSS_L2, "logistic": _lib.LOSS_LOGISTIC}[loss]
+        md = {"cov": _lib.MODE_COV, "data": _lib.MODE_DATA}[mode]
+        h = C.c_void_p()
+        check(self.L.midagma_create(C.byref(h), lt, md, self.d, int(device), stream), None, "midagma_create")
+        self.h = h
+        self.device = device
+        self.D = int(self.L.midagma_padded_dim(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.midagma_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return int(self.L.midagma_stream(self.h) or 0)
+
+    # -- data -----------------------------------------------------------------
+    def set_cov(self, cov: np.ndarray):
+        cov = _as_f64(cov)
+        check(self.L.midagma_set_cov(self.h, dptr(cov), cov.shape[1]), self.h, "set_cov")
+
+    def set_masks(self, mask_inc: np.ndarray | None, mask_exc: np.ndarray | None):
+        mi = None if mask_inc is None else _as_f64(mask_inc)
+        me = None if mask_exc is None else _as_f64(mask_exc)
+        check(self.L.midagma_set_masks(self.h, dptr(mi), dptr(me)), self.h, "set_masks")
+
+    def set_data(self, X, n_global: int | None = None):
+        """X: host ndarray (n_local x d) or a torch CUDA tensor (copied)."""
+        if hasattr(X, "data_ptr"):
+            X = X.contiguous()
+            n_local = X.shape[0]
+            check(self.L.midagma_set_data(self.h, C.c_void_p(X.data_ptr()), n_local, int(n_global or n_local), 1),
+                  self.h, "set_data")
+            self._keep = X
+        else:
+            X = _as_f64(X)
+            n_local = X.shape[0]
+            check(self.L.midagma_set_data(self.h, X.ctypes.data_as(C.c_void_p), n_local,
+                                          int(n_global or n_local), 0), self.h, "set_data")
+
+    def data_gram(self):
+        check(self.L.midagma_data_gram(self.h), self.h, "data_gram")
+
+    def cov_from_zbuf(self, n: float):
+        check(self.L.midagma_cov_from_zbuf(self.h, float(n)), self.h, "cov_from_zbuf")
+
+    @property
+    def zbuf_len(self) -> int:
+        return int(self.L.midagma_zbuf_len(self.h))
+
+    def bind_zbuf(self, ptr: int | None, length: int):
+        check(self.L.midagma_bind_zbuf(self.h, C.c_void_p(ptr) if ptr else None, int(length)), self.h, "bind_zbuf")
+
+    # -- the inner loop ---------------------------------------------------------
+    def minimize(self, W: np.ndarray, mu: float, max_iter: int, s: float, lr: float, tol: float = 1e-6,
+                 beta_1: float = 0.99, beta_2: float = 0.999, lambda1: float = 0.03,
+                 checkpoint: int = 1000, want_checkpoints: bool = False):
+        """Runs linear.py:165-333 on the GPU.  W (d x d float64) is updated in place."""
+        assert W.shape == (self.d, self.d) and W.dtype == np.float64 and W.flags.c_contiguous
+        res = _lib.MidagmaResult()
+        check(self.L.midagma_minimize(self.h, dptr(W), float(mu), int(max_iter), float(s), float(lr), float(tol),
+                                      float(beta_1), float(beta_2), float(lambda1), int(checkpoint),
+                                      C.byref(res)), self.h, "minimize")
+        return MinimizeResult.from_c(res, self.checkpoints() if want_checkpoints else ())
+
+    def begin(self, W, mu, max_iter, s, lr, tol=1e-6, beta_1=0.99, beta_2=0.999, lambda1=0.03, checkpoint=1000):
+        W = _as_f64(W)
+        check(self.L.midagma_begin(self.h, dptr(W), float(mu), int(max_iter), float(s), float(lr), float(tol),
+                                   float(beta_1), float(beta_2), float(lambda1), int(checkpoint)), self.h, "begin")
+
+    def run_slots(self, n: int):
+        check(self.L.midagma_run_slots(self.h, int(n)), self.h, "run_slots")
+
+    def sync(self):
+        check(self.L.midagma_sync(self.h), self.h, "sync")
+
+    def step_partial(self):
+        check(self.L.midagma_step_partial(self.h), self.h, "step_partial")
+
+    def step_finish(self):
+        check(self.L.midagma_step_finish(self.h), self.h, "step_finish")
+
+    def poll(self) -> _lib.MidagmaResult:
+        r = _lib.MidagmaResult()
+        check(self.L.midagma_poll(self.h, C.byref(r)), self.h, "poll")
+        return r
+
+    def end(self, W: np.ndarray) -> MinimizeResult:
+        r = _lib.MidagmaResult()
+        check(self.L.midagma_end(self.h, dptr(W), C.byref(r)), self.h, "end")
+        return MinimizeResult.from_c(r)
+
+    def checkpoints(self):
+        cap = 1 << 16
+        buf = (_lib.MidagmaCkpt * cap)()
+        n = self.L.midagma_checkpoints(self.h, buf, cap)
+        check(n, self.h, "checkpoints")
+        return [(int(c.iter), c.obj, c.score, c.h, c.lr, c.l1) for c in buf[:n]]
+
+    # -- helpers of the reference API ----------------------------------------------
+    def h_value(self, W: np.ndarray, s: float = 1.0, grad: bool = True):
+        W = _as_f64(W)
+        h = C.c_double()
+        G = np.empty((self.d, self.d)) if grad else None
+        check(self.L.midagma_h(self.h, dptr(W), float(s), C.byref(h), dptr(G)), self.h, "h")
+        return float(h.value), G
+
+    def score_value(self, W: np.ndarray):
+        W = _as_f64(W)
+        loss = C.c_double()
+        G = np.empty((self.d, self.d))
+        check(self.L.midagma_score(self.h, dptr(W), C.byref(loss), dptr(G)), self.h, "score")
+        return float(loss.value), G
+
+    def score_partial(self, W: np.ndarray):
+        W = _as_f64(W)
+        check(self.L.midagma_score_partial(self.h, dptr(W)), self.h, "score_partial")
+
+    def score_finish(self):
+        loss = C.c_double()
+        G = np.empty((self.d, self.d))
+        check(self.L.midagma_score_finish(self.h, C.byref(loss), dptr(G)), self.h, "score_finish")
+        return float(loss.value), G
+
+
+def run_allreduce_minimize(backend, W, mu, max_iter, s, lr, tol=1e-6, beta_1=0.99, beta_2=0.999,
+                           lambda1=0.03, checkpoint=1000, allreduce=None, batch: int = 32):
+    """Data-parallel inner loop over ranks.
+
+    ``backend`` exposes begin/step_partial/step_finish/poll/end (HipSolver, or a
+    test double); ``allreduce()`` sums the backend's score partial over ranks
+    in place.  Termination is decided on the device by the controller kernel;
+    the host polls every ``batch`` steps, extra steps after termination are
+    no-ops, so every rank runs the same number of all-reduces.
+    """
+    backend.begin(W, mu, max_iter, s, lr, tol, beta_1, beta_2, lambda1, checkpoint)
+    slots = 0
+    cap = int(max_iter) + int(max_iter) // max(int(checkpoint), 1) + 512
+    while True:
+        last = backend.poll()
+        if last.status != _lib.ST_RUNNING:
+            break
+        if slots > cap:
+            raise _lib.HipSolverError("allreduce_minimize: slot budget exceeded")
+        nb = max(1, min(batch, int(max_iter) - int(last.iters) + 2))
+        for _ in range(nb):
+            backend.step_partial()
+            if allreduce is not None:
+                allreduce()
+            backend.step_finish()
+        slots += nb
+    return backend.end(W)

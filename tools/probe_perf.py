@@ -1,0 +1,62 @@
+"""Quick GPU timing probe (development tool): steps/s of the slot at several sizes."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch  # noqa: F401
+
+from midagma_amd.simulate import make_dataset
+from midagma_amd.solver import HipSolver
+
+
+def cov_case(d, n, warm, K):
+    X, _, _ = make_dataset(d, n, seed=0)
+    X -= X.mean(0)
+    cov = X.T @ X / n
+    s = HipSolver(d, "l2", "cov")
+    s.set_cov(cov)
+    s.begin(np.zeros((d, d)), 1.0, warm + K + 10, 1.0, 3e-4, tol=-1.0)
+    s.run_slots(warm)
+    s.sync()
+    t0 = time.perf_counter()
+    s.run_slots(K)
+    s.sync()
+    dt = time.perf_counter() - t0
+    r = s.poll()
+    print(f"cov d={d}: {K / dt:.1f} steps/s  ({dt / K * 1e3:.3f} ms/step)  iters={r.iters} status={r.status}",
+          flush=True)
+    s.close()
+
+
+def data_case(d, n, warm, K, loss="l2"):
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((n, d))
+    s = HipSolver(d, loss, "data")
+    s.set_data(X, n_global=n)
+    if loss == "logistic":
+        s.set_cov(X.T @ X / n)
+    s.begin(np.zeros((d, d)), 1.0, warm + K + 10, 1.0, 3e-4, tol=-1.0)
+    s.run_slots(warm)
+    s.sync()
+    t0 = time.perf_counter()
+    s.run_slots(K)
+    s.sync()
+    dt = time.perf_counter() - t0
+    r = s.poll()
+    print(f"data {loss} d={d} n={n}: {K / dt:.2f} steps/s ({dt / K * 1e3:.2f} ms/step) iters={r.iters}", flush=True)
+    s.close()
+
+
+if __name__ == "__main__":
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "small"):
+        cov_case(20, 1000, 50, 2000)
+        cov_case(200, 2000, 20, 500)
+    if which in ("all", "d1000"):
+        cov_case(1000, 2000, 10, 300)
+    if which in ("all", "d5000"):
+        cov_case(5000, 6000, 2, 10)
+    if which in ("all", "data"):
+        data_case(1000, 100000, 2, 10)
