@@ -107,6 +107,10 @@ int midagma_step_partial(midagma_solver* s);
 /* enqueue n whole slots (part 1 + part 2) without host polling; midagma_sync waits. */
 int midagma_run_slots(midagma_solver* s, int64_t n);
 int midagma_sync(midagma_solver* s);
+/* Diagnostics: average device time (hipEvents on the solver stream, `reps` launches each)
+ * of the slot's parts: [0] build (sI-WoW)^T, [1] GJ inverse, [2] score GEMM(s), [3] whole
+ * slot, [4] data-mode X(I-W) GEMM, [5] data-mode X^T Y GEMM.  Advances the state by reps slots. */
+int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out);
 int midagma_step_finish(midagma_solver* s);
 int midagma_poll(midagma_solver* s, midagma_result* res); /* synchronizes */
 int midagma_end(midagma_solver* s, double* W, midagma_result* res);

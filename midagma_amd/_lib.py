@@ -69,6 +69,7 @@ EXPORTED = {
     "midagma_step_partial": (_int, [_vp]),
     "midagma_run_slots": (_int, [_vp, _i64]),
     "midagma_sync": (_int, [_vp]),
+    "midagma_profile_parts": (_int, [_vp, _int, _dp]),
     "midagma_step_finish": (_int, [_vp]),
     "midagma_poll": (_int, [_vp, C.POINTER(MidagmaResult)]),
     "midagma_end": (_int, [_vp, _dp, C.POINTER(MidagmaResult)]),

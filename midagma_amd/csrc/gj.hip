@@ -23,8 +23,11 @@ namespace midagma {
 template <bool SQUARE>
 __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __restrict__ X, int64_t ldx,
                                                             double* __restrict__ At, int64_t D, int64_t d,
-                                                            double s, const State* __restrict__ st) {
+                                                            double s_arg, const Params* __restrict__ pr,
+                                                            const State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
+  // s comes from device Params when given: graph replays must see each call's s
+  const double s = pr ? pr->s : s_arg;
   __shared__ double tile[64][65];
   const int bi = blockIdx.y, bj = blockIdx.x;  // source tile (rows bi, cols bj)
   const int tid = threadIdx.x;
@@ -176,13 +179,13 @@ void gj_setup_attributes() {
 }
 
 void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int64_t D, int64_t d, double s,
-                     const State* st, hipStream_t stream) {
+                     const Params* pr, const State* st, hipStream_t stream) {
   const int K = (int)(D / 64);
   dim3 grid(K, K);
   if (square)
-    hipLaunchKernelGGL(build_at_kernel<true>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, st);
+    hipLaunchKernelGGL(build_at_kernel<true>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, pr, st);
   else
-    hipLaunchKernelGGL(build_at_kernel<false>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, st);
+    hipLaunchKernelGGL(build_at_kernel<false>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, pr, st);
   HIP_TRY(hipGetLastError());
 }
 

@@ -68,6 +68,8 @@ struct midagma_solver {
   int64_t bc_len = 0;
   bool has_cov = false, has_data = false, has_inc = false, has_exc = false;
   bool begun = false;
+  const double* cap_minc = nullptr;  // mask pointers baked into the captured graphs
+  const double* cap_mexc = nullptr;
   double mu = 1.0;
   Params hp{};
 
@@ -101,7 +103,7 @@ struct midagma_solver {
 
   // ---- the slot -----------------------------------------------------------
   void enqueue_part1() {
-    launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, hp.s, d_state, stream);
+    launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, 0.0, d_params, d_state, stream);
     launch_gj_inverse(Mt.p, D, gj(), d_state, stream);
     if (mode == MIDAGMA_MODE_COV) {
       // rhs = ((-mu) cov) @ (I - W)    (linear.py:244)
@@ -453,10 +455,13 @@ int midagma_set_masks(midagma_solver* s, const double* mask_inc, const double* m
       s->upload_matrix(s->mexc, mask_exc, s->d);
     }
     HIP_TRY(hipStreamSynchronize(s->stream));
-    if (inc != s->has_inc || exc != s->has_exc) s->graphs_valid = false;
+    const double* pi = inc ? s->minc.p : nullptr;
+    const double* pe = exc ? s->mexc.p : nullptr;
+    if (pi != s->cap_minc || pe != s->cap_mexc) s->graphs_valid = false;  // captured pointers changed
+    s->cap_minc = pi;
+    s->cap_mexc = pe;
     s->has_inc = inc;
     s->has_exc = exc;
-    s->graphs_valid = false;  // buffer pointers may have changed
     return MIDAGMA_OK;
   });
 }
@@ -574,6 +579,61 @@ int midagma_sync(midagma_solver* s) {
   });
 }
 
+int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
+  if (!s || !s->begun || reps < 1 || !ms_out) return fail(s, MIDAGMA_E_STATE, "profile_parts: call begin first");
+  return guarded(s, [&] {
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    auto timed = [&](auto&& body) {
+      HIP_TRY(hipEventRecord(a, s->stream));
+      for (int r = 0; r < reps; ++r) body();
+      HIP_TRY(hipEventRecord(b, s->stream));
+      HIP_TRY(hipEventSynchronize(b));
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, a, b));
+      return (double)ms / reps;
+    };
+    const int64_t D = s->D;
+    // [0] build (sI - W o W)^T   [1] GJ inverse   [2] score GEMM(s)   [3] whole slot (graph)
+    // data mode: [4] Y = X (I - W) GEMM   [5] Z = X^T Y GEMM (+ slice sum)
+    ms_out[0] = timed([&] { launch_build_at(s->W.p, D, true, s->Mt.p, D, s->d, 0.0, s->d_params, s->d_state,
+                                            s->stream); });
+    ms_out[1] = timed([&] { launch_gj_inverse(s->Mt.p, D, s->gj(), s->d_state, s->stream); });
+    if (s->mode == MIDAGMA_MODE_COV) {
+      ms_out[2] = timed([&] {
+        launch_gemm(D, D, D, s->covs.p, D, false, s->W.p, D, B_IMINUS, s->zbuf, D, EPI_STORE, 1, 0, nullptr, 0, 0,
+                    s->d_state, s->stream);
+      });
+      ms_out[4] = ms_out[5] = 0.0;
+    } else {
+      ms_out[2] = timed([&] { s->enqueue_data_partial(s->W.p, s->d_state); });
+      ms_out[4] = timed([&] {
+        if (s->loss == MIDAGMA_LOSS_L2)
+          launch_gemm(s->n_pad, D, D, s->X.p, D, false, s->W.p, D, B_IMINUS, s->Y.p, D, EPI_STORE, 1, 0, nullptr, 0,
+                      0, s->d_state, s->stream);
+        else
+          launch_gemm(s->n_pad, D, D, s->X.p, D, false, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID, 1, 0,
+                      s->loss_part.p, s->n_local, s->d, s->d_state, s->stream);
+      });
+      ms_out[5] = timed([&] {
+        if (s->split == 1)
+          launch_gemm(D, D, s->n_pad, s->X.p, D, true, s->Y.p, D, B_PLAIN, s->zbuf, D, EPI_STORE, 1, 0, nullptr, 0, 0,
+                      s->d_state, s->stream);
+        else {
+          launch_gemm(D, D, s->n_pad, s->X.p, D, true, s->Y.p, D, B_PLAIN, s->Zparts.p, D, EPI_STORE, s->split,
+                      D * D, nullptr, 0, 0, s->d_state, s->stream);
+          launch_sum_slices(s->Zparts.p, s->split, D * D, D * D, s->zbuf, s->d_state, s->stream);
+        }
+      });
+    }
+    ms_out[3] = timed([&] { HIP_TRY(hipGraphLaunch(s->g_full, s->stream)); });
+    HIP_TRY(hipEventDestroy(a));
+    HIP_TRY(hipEventDestroy(b));
+    return MIDAGMA_OK;
+  });
+}
+
 int midagma_step_partial(midagma_solver* s) {
   if (!s || !s->begun) return fail(s, MIDAGMA_E_STATE, "step_partial: call begin first");
   return guarded(s, [&] {
@@ -634,7 +694,7 @@ int midagma_h(midagma_solver* s, const double* W, double s_dom, double* h, doubl
     s->upload_matrix(s->scratch, W, d);
     DevBuf work;
     work.alloc(DD);
-    launch_build_at(s->scratch.p, D, true, work.p, D, d, s_dom, nullptr, s->stream);
+    launch_build_at(s->scratch.p, D, true, work.p, D, d, s_dom, nullptr, nullptr, s->stream);
     launch_gj_inverse(work.p, D, s->gj(), nullptr, s->stream);
     std::vector<double> pl(D);
     HIP_TRY(hipMemcpyAsync(pl.data(), s->pivlog.p, D * sizeof(double), hipMemcpyDeviceToHost, s->stream));
@@ -780,7 +840,7 @@ extern "C" int midagma_logdet_inv_dev(const double* A, int64_t d, int64_t lda, d
       g_ws.push_back(ws);
     }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    launch_build_at(A, lda, false, ws->A.p, D, d, s_dom, nullptr, st);
+    launch_build_at(A, lda, false, ws->A.p, D, d, s_dom, nullptr, nullptr, st);
     launch_gj_inverse(ws->A.p, D, GJWork{ws->P.p, ws->R.p, ws->C.p, ws->piv.p}, nullptr, st);
     if (logdet_dev) launch_sum_vector(ws->piv.p, d, logdet_dev, nullptr, st);
     if (Mt_dev)

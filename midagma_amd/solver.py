@@ -142,6 +142,13 @@ class HipSolver:
     def sync(self):
         check(self.L.midagma_sync(self.h), self.h, "sync")
 
+    def profile_parts(self, reps: int = 10) -> dict:
+        """Average device ms per launch group, measured with hipEvents on the solver stream."""
+        out = np.zeros(8)
+        check(self.L.midagma_profile_parts(self.h, int(reps), dptr(out)), self.h, "profile_parts")
+        keys = ["build_at", "gj_inverse", "score", "slot", "gemm_xw", "gemm_xty"]
+        return {k: float(out[i]) for i, k in enumerate(keys)}
+
     def step_partial(self):
         check(self.L.midagma_step_partial(self.h), self.h, "step_partial")
 
