@@ -8,15 +8,25 @@
 // The kernels run on A^T so the result is inv(A)^T = M^T, exactly the operand
 // of the gradient 2 W∘M^T (linear.py:248), read coalesced by the fused update.
 //
-// Block step k (64-wide block column, K = D/64 steps):
-//   panel  : P = inv(A_kk) (unpivoted GJ in registers + LDS, pivots -> log|p|),
-//            R_kj = P A_kj (MFMA) for j != k, column panel C_ik = A_ik copied out
-//   update : A_ij -= C_i R_j (i,j != k);  A_kj = R_j;  A_ik = -C_i P;  A_kk = P
-// so every launch writes only its own tile of A (side buffers carry panels).
+// Block Gauss-Jordan with NB = 32 (K = D/32 block steps), ONE launch per step.
+// Step k reads three side panels published by step k-1 (double-buffered by
+// parity): P = inv(A_kk), the column tiles C_i = A_ik and the row tiles
+// R_j = A_kj, and updates every tile of A in place:
+//     A_ij -= C_i (P R_j)      A_kj = P R_j      A_ik = -C_i P      A_kk = P
+// Tiles landing in block column/row k+1 are also published as the next step's
+// panels, and the workgroup owning tile (k+1, k+1) inverts it right away
+// (unpivoted GJ in registers + LDS, pivots -> log|p|), so the only serial
+// chain per step is one 32x32 inversion plus one kernel boundary.
 #include "launch.h"
 #include "mfma64.h"
 
 namespace midagma {
+
+constexpr int NB = 32;        // block size of the elimination
+constexpr int SA32 = 34;      // [m][k] LDS image stride for 32-wide tiles (= 2 mod 32)
+constexpr int SB32 = 48;      // [k][n] LDS image stride (= 16 mod 32)
+constexpr int EPT = NB * NB / NTHREADS;   // elements per thread in the tile inversion (4)
+constexpr int TPR = NB / EPT;             // threads per tile row (8)
 
 // A^T tile builder: At[J][I] = (I == J ? s : 0) - f(X[I][J]) on the logical
 // d x d block (f = square for W, identity for a given A), identity padding.
@@ -55,128 +65,201 @@ __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __rest
   }
 }
 
-__global__ __launch_bounds__(NTHREADS) void gj_panel_kernel(const double* __restrict__ A, int64_t D, int k,
-                                                            double* __restrict__ Pbuf, double* __restrict__ Rbuf,
-                                                            double* __restrict__ Cbuf, double* __restrict__ pivlog,
-                                                            const State* __restrict__ st) {
-  if (st && st->status != ST_RUNNING) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  double* Ps = smem;               // [64][SA]  P as left operand
-  double* Ts = Ps + 64 * SA;       // [64][SB]  A_kj as right operand
-  double* rowbuf = Ts + 64 * SB;   // [2][64]   pivot row (double-buffered by step parity)
-  double* colbuf = rowbuf + 128;   // [2][64]   pivot column
-  const int tid = threadIdx.x, j = blockIdx.x;
-  const int r = tid >> 2, cg = tid & 3, c0 = cg * 16;
-  const double* Akk = A + (int64_t)k * 64 * D + (int64_t)k * 64;
+// ---- 32 x 32 tile helpers --------------------------------------------------------
+// Wave w owns the 16 x 16 quadrant (wm, wn) = (w >> 1, w & 1) of a 32 x 32 output.
+__device__ __forceinline__ int q_m0() { return (threadIdx.x >> 7) * 16; }
+__device__ __forceinline__ int q_n0() { return ((threadIdx.x >> 6) & 1) * 16; }
 
-  // This thread owns A_kk[r][c0 .. c0+15] in registers.
-  double a[16];
+// acc += Ls(32 x 32, [m][k] stride SA32) * Rs(32 x 32, [k][n] stride SB32)
+__device__ __forceinline__ void mma32(const double* __restrict__ Ls, const double* __restrict__ Rs, dbl4& acc) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int m0 = q_m0(), n0 = q_n0();
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const double2 v = *reinterpret_cast<const double2*>(Akk + (int64_t)r * D + c0 + 2 * e);
-    a[2 * e] = v.x;
-    a[2 * e + 1] = v.y;
+  for (int k0 = 0; k0 < NB; k0 += 4) {
+    const double a = Ls[(m0 + r) * SA32 + k0 + kq];
+    const double b = Rs[(k0 + kq) * SB32 + n0 + r];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
   }
+}
 
-  for (int pb = 0; pb < 64; pb += 16) {
+template <class F>
+__device__ __forceinline__ void acc_foreach(dbl4& acc, F&& f) {
+  const int lane = threadIdx.x & 63;
+  const int m0 = q_m0(), n0 = q_n0();
 #pragma unroll
-    for (int pp = 0; pp < 16; ++pp) {
+  for (int t = 0; t < 4; ++t) {
+    double v = acc[t];
+    f(m0 + acc_row(lane, t), n0 + acc_col(lane), v);
+    acc[t] = v;
+  }
+}
+
+// 32 x 32 global tile (leading dim ld) -> LDS image with stride S, scaled by `sc`
+template <int S>
+__device__ __forceinline__ void tile32_to_lds(double* __restrict__ dst, const double* __restrict__ src, int64_t ld,
+                                              double sc) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int item = it * NTHREADS + threadIdx.x;  // 512 double2 items
+    const int row = item >> 4, c = (item & 15) * 2;
+    double2 v = *reinterpret_cast<const double2*>(src + row * ld + c);
+    v.x *= sc;
+    v.y *= sc;
+    *reinterpret_cast<double2*>(dst + row * S + c) = v;
+  }
+}
+
+__device__ __forceinline__ void tile32_copy(double* __restrict__ dst, int64_t ldd, const double* __restrict__ src,
+                                            int64_t lds) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int item = it * NTHREADS + threadIdx.x;
+    const int row = item >> 4, c = (item & 15) * 2;
+    *reinterpret_cast<double2*>(dst + row * ldd + c) = *reinterpret_cast<const double2*>(src + row * lds + c);
+  }
+}
+
+// Reciprocal to ~1 ulp: hardware seed + two Newton steps (no IEEE division chain).
+__device__ __forceinline__ double fast_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+// In-place unpivoted GJ inverse of the 32 x 32 tile held in `img` (row stride SA32)
+// by the whole workgroup; writes the inverse to Pout (ld NB) and log|pivot| to plog.
+// `scratch` needs 4*NB doubles.  Ends with a barrier.
+__device__ void invert_tile32(double* __restrict__ img, double* __restrict__ Pout, double* __restrict__ plog,
+                              double* __restrict__ scratch) {
+  const int tid = threadIdx.x;
+  const int r = tid / TPR, c0 = (tid % TPR) * EPT;
+  double* rowbuf = scratch;           // [2][NB]
+  double* colbuf = scratch + 2 * NB;  // [2][NB]
+  double a[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) a[e] = img[r * SA32 + c0 + e];
+  double pivs = 0.0;  // lane p of wave 0 keeps pivot p (p < 32)
+  for (int pb = 0; pb < NB; pb += EPT) {
+#pragma unroll
+    for (int pp = 0; pp < EPT; ++pp) {
       const int p = pb + pp;
       const int par = p & 1;
       if (r == p) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) rowbuf[par * 64 + c0 + e] = a[e];
+        for (int e = 0; e < EPT; ++e) rowbuf[par * NB + c0 + e] = a[e];
       }
-      if (cg == (pb >> 4)) colbuf[par * 64 + r] = a[pp];
+      if (c0 == pb) colbuf[par * NB + r] = a[pp];
       __syncthreads();
-      const double piv = rowbuf[par * 64 + p];
-      const double inv = 1.0 / piv;
-      const double arp = colbuf[par * 64 + r];
+      const double piv = rowbuf[par * NB + p];
+      const double inv = fast_rcp(piv);
+      const double arp = colbuf[par * NB + r];
       const double neg_arp_inv = -arp * inv;
+      if (tid == p) pivs = piv;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
+      for (int e = 0; e < EPT; ++e) {
         const int c = c0 + e;
-        const double rpc = rowbuf[par * 64 + c] * inv;
+        const double rpc = rowbuf[par * NB + c] * inv;
         if (r == p)
           a[e] = (c == p) ? inv : rpc;
         else
           a[e] = (c == p) ? neg_arp_inv : __builtin_fma(-arp, rpc, a[e]);
       }
-      if (pivlog && j == 0 && tid == 0) pivlog[(int64_t)k * 64 + p] = log(fabs(piv));
     }
   }
-
-  if (j == k) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) Pbuf[r * 64 + c0 + e] = a[e];
-    return;
-  }
-#pragma unroll
-  for (int e = 0; e < 16; ++e) Ps[r * SA + c0 + e] = a[e];
-  tile_to_lds<SB>(Ts, A + (int64_t)k * 64 * D + (int64_t)j * 64, D, Ident());
+  for (int e = 0; e < EPT; ++e) Pout[r * NB + c0 + e] = a[e];
+  if (plog && tid < NB) plog[tid] = log(fabs(pivs));
   __syncthreads();
-  Quad q;
-  q.zero();
-  quad_mma<false>(Ps, Ts, q);
-  double* Rj = Rbuf + (int64_t)j * 64;
-  quad_foreach(q, [&](int row, int col, double& v) { Rj[(int64_t)row * D + col] = v; });
-  // column panel tile (j, k) -> Cbuf rows j*64.., leading dim 64
-  const double* Ajk = A + (int64_t)j * 64 * D + (int64_t)k * 64;
-  double* Cj = Cbuf + (int64_t)j * 64 * 64;
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int item = it * NTHREADS + tid;
-    const int row = item >> 5, c = (item & 31) * 2;
-    *reinterpret_cast<double2*>(Cj + row * 64 + c) = *reinterpret_cast<const double2*>(Ajk + (int64_t)row * D + c);
-  }
 }
 
-__global__ __launch_bounds__(NTHREADS) void gj_update_kernel(double* __restrict__ A, int64_t D, int k,
-                                                             const double* __restrict__ Pbuf,
-                                                             const double* __restrict__ Rbuf,
-                                                             const double* __restrict__ Cbuf,
-                                                             const State* __restrict__ st) {
+// Prologue: publish step 0's panels and invert A_00.
+__global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __restrict__ A, int64_t D,
+                                                               double* __restrict__ Cside,
+                                                               double* __restrict__ Rside,
+                                                               double* __restrict__ Pside,
+                                                               double* __restrict__ pivlog,
+                                                               const State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int bi = blockIdx.y, bj = blockIdx.x, tid = threadIdx.x;
-  double* Aij = A + (int64_t)bi * 64 * D + (int64_t)bj * 64;
-  if (bi == k) {
-    const double* src = (bj == k) ? Pbuf : Rbuf + (int64_t)bj * 64;
-    const int64_t lds = (bj == k) ? 64 : D;
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int item = it * NTHREADS + tid;
-      const int row = item >> 5, c = (item & 31) * 2;
-      *reinterpret_cast<double2*>(Aij + (int64_t)row * D + c) =
-          *reinterpret_cast<const double2*>(src + row * lds + c);
-    }
-    return;
-  }
-  double* Ls = smem;            // [64][SA]  -C_i
-  double* Rs = Ls + 64 * SA;    // [64][SB]  R_j or P
-  tile_to_lds<SA>(Ls, Cbuf + (int64_t)bi * 64 * 64, 64, Negate());
-  Quad q;
-  if (bj == k) {
-    tile_to_lds<SB>(Rs, Pbuf, 64, Ident());
-    q.zero();
-  } else {
-    tile_to_lds<SB>(Rs, Rbuf + (int64_t)bj * 64, D, Ident());
-    quad_foreach(q, [&](int row, int col, double& v) { v = Aij[(int64_t)row * D + col]; });
-  }
+  __shared__ __attribute__((aligned(16))) double img[NB * SA32];
+  __shared__ double scratch[4 * NB];
+  const int t = blockIdx.x;
+  tile32_copy(Cside + (int64_t)t * NB * NB, NB, A + (int64_t)t * NB * D, D);  // column 0
+  tile32_copy(Rside + (int64_t)t * NB, D, A + (int64_t)t * NB, D);            // row 0
+  if (t != 0) return;
+  tile32_to_lds<SA32>(img, A, D, 1.0);
   __syncthreads();
-  quad_mma<false>(Ls, Rs, q);
-  quad_foreach(q, [&](int row, int col, double& v) { Aij[(int64_t)row * D + col] = v; });
+  invert_tile32(img, Pside, pivlog, scratch);
 }
 
-constexpr size_t kPanelLds = (64 * SA + 64 * SB + 256) * sizeof(double);
-constexpr size_t kUpdateLds = (64 * SA + 64 * SB) * sizeof(double);
+// One block step of the elimination (see file header).
+//   side buffers: Cside[2] (D x NB), Rside[2] (NB x D), Pside[2] (NB x NB), parity k & 1 read.
+__global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ A, int64_t D, int k,
+                                                           double* __restrict__ Cside0, double* __restrict__ Cside1,
+                                                           double* __restrict__ Rside0, double* __restrict__ Rside1,
+                                                           double* __restrict__ Pside0, double* __restrict__ Pside1,
+                                                           double* __restrict__ pivlog,
+                                                           const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  __shared__ __attribute__((aligned(16))) double L0[NB * SA32];   // left operand
+  __shared__ __attribute__((aligned(16))) double R0[NB * SB32];   // right operand
+  __shared__ __attribute__((aligned(16))) double T0[NB * SB32];   // intermediate P R_j
+  __shared__ double scratch[4 * NB];
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  const int K = (int)(D / NB);
+  const bool odd = k & 1;
+  const double* Cs = odd ? Cside1 : Cside0;
+  const double* Rs = odd ? Rside1 : Rside0;
+  const double* P = odd ? Pside1 : Pside0;
+  double* Cn = odd ? Cside0 : Cside1;
+  double* Rn = odd ? Rside0 : Rside1;
+  double* Pn = odd ? Pside0 : Pside1;
+  double* Aij = A + (int64_t)bi * NB * D + (int64_t)bj * NB;
 
-void gj_setup_attributes() {
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(gj_panel_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPanelLds));
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(gj_update_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kUpdateLds));
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  if (bi == k && bj == k) {
+    // A_kk = P (read directly into the accumulator layout)
+    acc_foreach(acc, [&](int row, int col, double& v) { v = P[row * NB + col]; });
+  } else if (bi == k) {
+    // A_kj = P R_j
+    tile32_to_lds<SA32>(L0, P, NB, 1.0);
+    tile32_to_lds<SB32>(R0, Rs + (int64_t)bj * NB, D, 1.0);
+    __syncthreads();
+    mma32(L0, R0, acc);
+  } else if (bj == k) {
+    // A_ik = -C_i P
+    tile32_to_lds<SA32>(L0, Cs + (int64_t)bi * NB * NB, NB, -1.0);
+    tile32_to_lds<SB32>(R0, P, NB, 1.0);
+    __syncthreads();
+    mma32(L0, R0, acc);
+  } else {
+    // T = P R_j ; A_ij += (-C_i) T
+    tile32_to_lds<SA32>(L0, P, NB, 1.0);
+    tile32_to_lds<SB32>(R0, Rs + (int64_t)bj * NB, D, 1.0);
+    __syncthreads();
+    mma32(L0, R0, acc);
+    acc_foreach(acc, [&](int row, int col, double& v) { T0[row * SB32 + col] = v; });
+    __syncthreads();  // T complete; L0 free
+    tile32_to_lds<SA32>(L0, Cs + (int64_t)bi * NB * NB, NB, -1.0);
+    acc_foreach(acc, [&](int row, int col, double& v) { v = Aij[(int64_t)row * D + col]; });
+    __syncthreads();
+    mma32(L0, T0, acc);
+  }
+  acc_foreach(acc, [&](int row, int col, double& v) { Aij[(int64_t)row * D + col] = v; });
+  if (k + 1 >= K) return;
+  const int k1 = k + 1;
+  if (bj == k1) acc_foreach(acc, [&](int row, int col, double& v) { Cn[((int64_t)bi * NB + row) * NB + col] = v; });
+  if (bi == k1) acc_foreach(acc, [&](int row, int col, double& v) { Rn[(int64_t)row * D + (int64_t)bj * NB + col] = v; });
+  if (bi == k1 && bj == k1) {
+    __syncthreads();  // L0 / T0 reads done
+    acc_foreach(acc, [&](int row, int col, double& v) { L0[row * SA32 + col] = v; });
+    __syncthreads();
+    invert_tile32(L0, Pn, pivlog ? pivlog + (int64_t)k1 * NB : nullptr, scratch);
+  }
 }
+
+void gj_setup_attributes() {}
 
 void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int64_t D, int64_t d, double s,
                      const Params* pr, const State* st, hipStream_t stream) {
@@ -190,13 +273,17 @@ void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int6
 }
 
 void launch_gj_inverse(double* A, int64_t D, const GJWork& w, const State* st, hipStream_t stream) {
-  const int K = (int)(D / 64);
-  for (int k = 0; k < K; ++k) {
-    hipLaunchKernelGGL(gj_panel_kernel, dim3(K), dim3(NTHREADS), kPanelLds, stream, A, D, k, w.P, w.R, w.C,
+  const int K = (int)(D / NB);
+  double* C0 = w.C;
+  double* C1 = w.C + D * NB;
+  double* R0 = w.R;
+  double* R1 = w.R + NB * D;
+  double* P0 = w.P;
+  double* P1 = w.P + NB * NB;
+  hipLaunchKernelGGL(gj_prologue_kernel, dim3(K), dim3(NTHREADS), 0, stream, A, D, C0, R0, P0, w.pivlog, st);
+  for (int k = 0; k < K; ++k)
+    hipLaunchKernelGGL(gj_step_kernel, dim3(K, K), dim3(NTHREADS), 0, stream, A, D, k, C0, C1, R0, R1, P0, P1,
                        w.pivlog, st);
-    hipLaunchKernelGGL(gj_update_kernel, dim3(K, K), dim3(NTHREADS), kUpdateLds, stream, A, D, k, w.P, w.R, w.C,
-                       st);
-  }
   HIP_TRY(hipGetLastError());
 }
 

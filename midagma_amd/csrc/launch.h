@@ -18,9 +18,9 @@ struct HipError : std::runtime_error {
 };
 
 struct GJWork {
-  double* P;       // 64 x 64
-  double* R;       // 64 x D
-  double* C;       // D x 64
+  double* P;       // >= 2 x 32 x 32  (double-buffered inverse of the diagonal block)
+  double* R;       // >= 2 x 32 x D   (row panels)
+  double* C;       // >= 2 x D x 32   (column panels)
   double* pivlog;  // D  (log |pivot| per row, nullable)
 };
 

@@ -143,18 +143,46 @@ def test_branches(hip, golden):
 
 
 def test_full_fit_d20(hip, golden):
+    """Default fit (T=5, s=[1,.9,.8,.7,.6]).  Stages 1-4 must take the reference's
+    iteration counts.  The last stage (mu=1e-4, s=0.6) is chaotic: from identical
+    starting W, GPU and reference separate by O(lr) within 2000 steps, and whether the
+    relative objective change at a checkpoint is below tol=1e-6 varies (the reference
+    itself shows 2.8e-7 at its stopping checkpoint) -- so only a one-checkpoint slack
+    is allowed there ('or documented when an early-stop lands differently')."""
     from midagma_amd import DagmaLinear
     f = golden("fit_d20.npz")
     X = golden("data_d20_n1000_seed0.npz")["X"].copy()
     m = DagmaLinear("l2")
     W = m.fit(X, lambda1=0.03, s=[1.0, .9, .8, .7, .6])
     iters = [e["iters"] for e in m.minimize_log]
-    assert iters == [int(c[5]) for c in f["calls"]]
+    ref_iters = [int(c[5]) for c in f["calls"]]
+    assert iters[:4] == ref_iters[:4]
+    assert abs(iters[4] - ref_iters[4]) <= 1000
     env = float(np.abs(f["W_unthresholded"] - f["W_unthresholded_noisy"]).max())
     assert np.array_equal(W != 0, f["W"] != 0)
     assert np.abs(W - f["W"]).max() <= max(2 * env, 1e-5)
     assert abs(m.h_final - f["h_final"]) <= 1e-6 * abs(float(f["h_final"])) + 1e-12
     assert abs(m.score_final - f["score_final"]) <= 1e-6 * abs(float(f["score_final"]))
+
+
+def test_fit_stages_from_reference_start(hip, golden):
+    """Each stage restarted from the oracle's own starting W: identical iteration
+    counts in all five stages, W within 1e-9 for the non-chaotic stages."""
+    from midagma_amd.solver import HipSolver
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    o = _oracle(X)
+    sol = HipSolver(20)
+    sol.set_cov(o.cov)
+    W, mu = np.zeros((20, 20)), 1.0
+    for i, s in enumerate([1.0, .9, .8, .7, .6]):
+        K = 30000 if i < 4 else 60000
+        Wg = W.copy()
+        res = sol.minimize(Wg, mu, K, s, 3e-4, tol=1e-6, lambda1=0.03)
+        W, tr = o.minimize(W.copy(), mu, K, s, 3e-4)
+        assert res.iters == tr.iters and res.early_stop == tr.early_stop
+        if i < 4:
+            assert np.abs(Wg - W).max() <= 1e-9
+        mu *= 0.1
 
 
 def test_checkpoint_early_stop_matches_oracle(hip, golden):
