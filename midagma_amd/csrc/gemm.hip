@@ -83,6 +83,164 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(int64_t K, int64_t kslic
   if (threadIdx.x == 0) loss_part[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
 }
 
+// ---- 128 x 128 tile GEMM (the data-mode and large-d workhorse) ---------------------------
+// 4 waves in 2 x 2, each owning a 64 x 64 sub-tile = 4 x 4 accumulators of 16 x 16 (64 f64
+// accumulator values per lane).  BK = 16, LDS double-buffered with register prefetch of the
+// next k-tile (one barrier per k-tile).  LDS images (strides in doubles, conflict-free for
+// the MFMA fragment reads of a 32-lane group):
+//   op(A) from A[m][k] : [m][k] image, stride 18  (36 r mod 64 distinct for r < 16)
+//   op(A) from A[k][m] : [k][m] image, stride 144 (= 16 mod 32)
+//   op(B)              : [k][n] image, stride 144
+// Workgroups are remapped so consecutive tiles (which share an A panel) run on one XCD.
+constexpr int G_BM = 128, G_BN = 128, G_BK = 16;
+constexpr int G_SMK = 18, G_SKM = 144;
+constexpr int G_IMG = 128 * 18;  // doubles per operand image (== 16 * 144)
+
+__device__ __forceinline__ int xcd_remap(int w, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = w % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
+}
+
+template <bool ATRANS, int BMODE, int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t kslice, int tiles_m, int tiles_n,
+                                                              const double* __restrict__ A, int64_t lda,
+                                                              const double* __restrict__ B, int64_t ldb,
+                                                              double* __restrict__ C, int64_t ldc,
+                                                              int64_t slice_stride, double* __restrict__ loss_part,
+                                                              int64_t m_valid, int64_t n_valid,
+                                                              const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nwg = gridDim.x;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int per_slice = tiles_m * tiles_n;
+  const int z = t / per_slice, rem = t % per_slice;
+  const int bm = rem / tiles_n, bn = rem % tiles_n;
+  const int64_t m0 = (int64_t)bm * G_BM, n0 = (int64_t)bn * G_BN;
+  const int64_t k_begin = (int64_t)z * kslice;
+  const int64_t k_end = (k_begin + kslice < K) ? k_begin + kslice : K;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+  const int mb = (w >> 1) * 64, nbs = (w & 1) * 64;
+
+  double2 ra[4], rb[4];
+  auto load = [&](int64_t kt) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int i = it * NTHREADS + tid;
+      if (ATRANS) {
+        const int krow = i >> 6, c2 = i & 63;
+        ra[it] = *reinterpret_cast<const double2*>(A + (kt + krow) * lda + m0 + 2 * c2);
+      } else {
+        const int mrow = i >> 3, k2 = i & 7;
+        ra[it] = *reinterpret_cast<const double2*>(A + (m0 + mrow) * lda + kt + 2 * k2);
+      }
+      const int krow = i >> 6, c2 = i & 63;
+      double2 v = *reinterpret_cast<const double2*>(B + (kt + krow) * ldb + n0 + 2 * c2);
+      if (BMODE == B_IMINUS) {
+        const int64_t kg = kt + krow, ng = n0 + 2 * c2;
+        v.x = (kg == ng ? 1.0 : 0.0) - v.x;
+        v.y = (kg == ng + 1 ? 1.0 : 0.0) - v.y;
+      }
+      rb[it] = v;
+    }
+  };
+  auto store = [&](int buf) {
+    double* As = smem + buf * 2 * G_IMG;
+    double* Bs = As + G_IMG;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int i = it * NTHREADS + tid;
+      if (ATRANS) {
+        const int krow = i >> 6, c2 = i & 63;
+        *reinterpret_cast<double2*>(As + krow * G_SKM + 2 * c2) = ra[it];
+      } else {
+        const int mrow = i >> 3, k2 = i & 7;
+        *reinterpret_cast<double2*>(As + mrow * G_SMK + 2 * k2) = ra[it];
+      }
+      const int krow = i >> 6, c2 = i & 63;
+      *reinterpret_cast<double2*>(Bs + krow * G_SKM + 2 * c2) = rb[it];
+    }
+  };
+
+  dbl4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  int buf = 0;
+  if (k_begin < k_end) {
+    load(k_begin);
+    store(0);
+  }
+  __syncthreads();
+  for (int64_t kt = k_begin; kt < k_end; kt += G_BK) {
+    const bool more = kt + G_BK < k_end;
+    if (more) load(kt + G_BK);
+    const double* As = smem + buf * 2 * G_IMG;
+    const double* Bs = As + G_IMG;
+#pragma unroll
+    for (int kk = 0; kk < G_BK / 4; ++kk) {
+      const int k = kk * 4 + kq;
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = ATRANS ? As[k * G_SKM + mb + i * 16 + r] : As[(mb + i * 16 + r) * G_SMK + k];
+        b[i] = Bs[k * G_SKM + nbs + i * 16 + r];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  double* Ct = C + (int64_t)z * slice_stride;
+  if (EPI == EPI_STORE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const int64_t row = m0 + mb + i * 16 + acc_row(lane, tt);
+          const int64_t col = n0 + nbs + j * 16 + acc_col(lane);
+          Ct[row * ldc + col] = acc[i][j][tt];
+        }
+    return;
+  }
+  const bool want_loss = loss_part != nullptr && (st == nullptr || st->ckpt_pending);
+  double part = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int64_t row = m0 + mb + i * 16 + acc_row(lane, tt);
+        const int64_t col = n0 + nbs + j * 16 + acc_col(lane);
+        const double v = acc[i][j][tt];
+        if (want_loss && row < m_valid && col < n_valid) part += logaddexp0(v) - A[row * lda + col] * v;
+        Ct[row * ldc + col] = 1.0 / (1.0 + exp(-v));
+      }
+  if (!want_loss) return;
+  __syncthreads();
+  double* red = smem;
+  red[tid] = part;
+  __syncthreads();
+  for (int s2 = NTHREADS / 2; s2 > 0; s2 >>= 1) {
+    if (tid < s2) red[tid] += red[tid + s2];
+    __syncthreads();
+  }
+  if (tid == 0) loss_part[blockIdx.x] = red[0];
+}
+
+constexpr size_t kGemm128Lds = 4 * G_IMG * sizeof(double);
+
 constexpr size_t kGemmLds = (2 * 64 * SB) * sizeof(double);
 
 template <bool AT, int BM, int EP>
@@ -91,7 +249,18 @@ static void set_attr() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmLds));
 }
 
+template <bool AT, int BM, int EP>
+static void set_attr128() {
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm128_kernel<AT, BM, EP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemm128Lds));
+}
+
 void gemm_setup_attributes() {
+  set_attr128<false, B_PLAIN, EPI_STORE>();
+  set_attr128<false, B_IMINUS, EPI_STORE>();
+  set_attr128<true, B_PLAIN, EPI_STORE>();
+  set_attr128<true, B_IMINUS, EPI_STORE>();
+  set_attr128<false, B_PLAIN, EPI_SIGMOID>();
   set_attr<false, B_PLAIN, EPI_STORE>();
   set_attr<false, B_IMINUS, EPI_STORE>();
   set_attr<true, B_PLAIN, EPI_STORE>();
@@ -103,6 +272,32 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
                  int64_t ldb, GemmB bmode, double* C, int64_t ldc, GemmEpi epi, int split, int64_t slice_stride,
                  double* loss_part, int64_t m_valid, int64_t n_valid, const State* st, hipStream_t stream) {
   if (M % 64 || N % 64 || K % 64 || split < 1) throw std::invalid_argument("launch_gemm: bad shape");
+  if (M % 128 == 0 && N % 128 == 0 && K % 128 == 0) {
+    const int64_t ktiles16 = K / G_BK;
+    const int64_t per16 = (ktiles16 + split - 1) / split;
+    const int nsplit = (int)((ktiles16 + per16 - 1) / per16);
+    const int tm = (int)(M / G_BM), tn = (int)(N / G_BN);
+    const int64_t nwg = (int64_t)tm * tn * nsplit;
+    const int64_t kslice = per16 * G_BK;
+#define MIDAGMA_GEMM128(AT, BM, EP)                                                                       \
+  hipLaunchKernelGGL((gemm128_kernel<AT, BM, EP>), dim3((unsigned)nwg), dim3(NTHREADS), kGemm128Lds, stream, K, \
+                     kslice, tm, tn, A, lda, B, ldb, C, ldc, slice_stride, loss_part, m_valid, n_valid, st)
+    if (epi == EPI_SIGMOID) {
+      if (a_trans || bmode != B_PLAIN || nsplit != 1) throw std::invalid_argument("launch_gemm: sigmoid form");
+      MIDAGMA_GEMM128(false, B_PLAIN, EPI_SIGMOID);
+    } else if (!a_trans && bmode == B_PLAIN) {
+      MIDAGMA_GEMM128(false, B_PLAIN, EPI_STORE);
+    } else if (!a_trans) {
+      MIDAGMA_GEMM128(false, B_IMINUS, EPI_STORE);
+    } else if (bmode == B_PLAIN) {
+      MIDAGMA_GEMM128(true, B_PLAIN, EPI_STORE);
+    } else {
+      MIDAGMA_GEMM128(true, B_IMINUS, EPI_STORE);
+    }
+#undef MIDAGMA_GEMM128
+    HIP_TRY(hipGetLastError());
+    return;
+  }
   const int64_t ktiles = K / 64;
   const int64_t per = (ktiles + split - 1) / split;
   const int nsplit = (int)((ktiles + per - 1) / per);

@@ -52,7 +52,8 @@ struct midagma_solver {
   double* zbuf = nullptr;  // d x d (+64 tail) score partial; internal or bound
   int64_t zbuf_cap = 0;
   // data mode
-  DevBuf X, Y, Zparts, loss_part;
+  DevBuf X, Y, Zparts, loss_part, cov_parts;
+  int cov_split = 1;
   int64_t n_local = 0, n_pad = 0, n_global = 0;
   int split = 1;
   int64_t loss_part_count = 0;
@@ -79,7 +80,7 @@ struct midagma_solver {
   ~midagma_solver() {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
-                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part})
+                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts})
       b->release();
     if (d_params) (void)hipFree(d_params);
     if (d_state) (void)hipFree(d_state);
@@ -107,10 +108,21 @@ struct midagma_solver {
     launch_gj_inverse(Mt.p, D, gj(), d_state, stream);
     if (mode == MIDAGMA_MODE_COV) {
       // rhs = ((-mu) cov) @ (I - W)    (linear.py:244)
-      launch_gemm(D, D, D, covs.p, D, false, W.p, D, B_IMINUS, zbuf, D, EPI_STORE, 1, 0, nullptr, 0, 0, d_state,
-                  stream);
+      enqueue_cov_gemm(covs.p, W.p, zbuf, d_state);
     } else {
       enqueue_data_partial(W.p, d_state);
+    }
+  }
+
+  // out = Cm @ (I - Wp) on the d x d problem; split-K over fixed slices when the tile grid
+  // alone cannot fill the chip (summed in fixed order: deterministic)
+  void enqueue_cov_gemm(const double* Cm, const double* Wp, double* out, const State* st) {
+    if (cov_split > 1) {
+      launch_gemm(D, D, D, Cm, D, false, Wp, D, B_IMINUS, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
+                  0, st, stream);
+      launch_sum_slices(cov_parts.p, cov_split, D * D, D * D, out, st, stream);
+    } else {
+      launch_gemm(D, D, D, Cm, D, false, Wp, D, B_IMINUS, out, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
     }
   }
 
@@ -178,6 +190,10 @@ struct midagma_solver {
     C.alloc((size_t)D * 64);
     pivlog.alloc(D);
     partials.alloc(2 * NRED);
+    if (D % 128 == 0 && (D / 128) * (D / 128) < 256) {
+      cov_split = (int)std::min<int64_t>(4, D / 128);
+      if (cov_split > 1) cov_parts.alloc((size_t)cov_split * DD);
+    }
     zown.alloc(DD + 64);
     HIP_TRY(hipMemsetAsync(zown.p, 0, (DD + 64) * sizeof(double), stream));
     zbuf = zown.p;
@@ -396,7 +412,7 @@ int midagma_create(midagma_solver** out, int loss, int mode, int64_t d, int devi
   s->loss = loss;
   s->mode = mode;
   s->d = d;
-  s->D = round_up64(d);
+  s->D = d > 192 ? (d + 127) / 128 * 128 : round_up64(d);  // 128-multiples feed the 128x128 GEMM tiles
   s->device = device;
   int rc = guarded(s, [&] {
     setup_attributes_once();
@@ -473,7 +489,7 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     const int64_t D = s->D;
     s->n_local = n_local;
     s->n_global = n_global;
-    s->n_pad = round_up64(n_local);
+    s->n_pad = (n_local + 127) / 128 * 128;
     const size_t nx = (size_t)s->n_pad * D;
     s->X.alloc(nx);
     s->Y.alloc(nx);
@@ -481,7 +497,7 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     HIP_TRY(hipMemcpy2DAsync(s->X.p, D * sizeof(double), X, s->d * sizeof(double), s->d * sizeof(double), n_local,
                              on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s->stream));
     // split-K over the rows so the X^T Y GEMM fills the chip: (D/64)^2 tiles x split >= ~1024 workgroups
-    const int64_t tiles = (D / 64) * (D / 64);
+    const int64_t tiles = (D % 128 == 0) ? (D / 128) * (D / 128) : (D / 64) * (D / 64);
     const int64_t ktiles = s->n_pad / 64;
     int split = (int)std::max<int64_t>(1, std::min<int64_t>(ktiles / 8, (1024 + tiles - 1) / tiles));
     s->split = std::min(split, 32);
@@ -601,10 +617,7 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
                                             s->stream); });
     ms_out[1] = timed([&] { launch_gj_inverse(s->Mt.p, D, s->gj(), s->d_state, s->stream); });
     if (s->mode == MIDAGMA_MODE_COV) {
-      ms_out[2] = timed([&] {
-        launch_gemm(D, D, D, s->covs.p, D, false, s->W.p, D, B_IMINUS, s->zbuf, D, EPI_STORE, 1, 0, nullptr, 0, 0,
-                    s->d_state, s->stream);
-      });
+      ms_out[2] = timed([&] { s->enqueue_cov_gemm(s->covs.p, s->W.p, s->zbuf, s->d_state); });
       ms_out[4] = ms_out[5] = 0.0;
     } else {
       ms_out[2] = timed([&] { s->enqueue_data_partial(s->W.p, s->d_state); });
@@ -737,8 +750,7 @@ int midagma_score(midagma_solver* s, const double* W, double* loss, double* G) {
     s->upload_matrix(s->scratch, W, d);
     DevBuf rhs;
     rhs.alloc(DD);
-    launch_gemm(D, D, D, s->cov.p, D, false, s->scratch.p, D, B_IMINUS, rhs.p, D, EPI_STORE, 1, 0, nullptr, 0, 0,
-                nullptr, s->stream);  // rhs = cov @ (I - W)   (linear.py:85-86)
+    s->enqueue_cov_gemm(s->cov.p, s->scratch.p, rhs.p, nullptr);  // rhs = cov @ (I - W)   (linear.py:85-86)
     double sd = 0;
     host_trace_l1(s, s->scratch.p, rhs.p, &sd, nullptr);
     *loss = 0.5 * sd;

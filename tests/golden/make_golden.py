@@ -219,6 +219,7 @@ def gen_fit(X):
     out = {"W": W, "W_unthresholded": m.last_h_W, "calls": np.array(c, dtype=np.float64),
            "h_final": np.array(m.h_final), "score_final": np.array(m.score_final),
            "W_noisy": W2, "W_unthresholded_noisy": m2.last_h_W,
+           "h_final_noisy": np.array(m2.h_final), "score_final_noisy": np.array(m2.score_final),
            "calls_noisy": np.array(c2, dtype=np.float64)}
     np.savez_compressed(os.path.join(HERE, "fit_d20.npz"), **out)
 

@@ -26,7 +26,7 @@ def cov_case(d, n, warm, K):
     dt = time.perf_counter() - t0
     r = s.poll()
     print(f"cov d={d}: {K / dt:.1f} steps/s  ({dt / K * 1e3:.3f} ms/step)  iters={r.iters} status={r.status}",
-          flush=True)
+          {k: round(v, 4) for k, v in s.profile_parts(5).items()}, flush=True)
     s.close()
 
 
@@ -45,7 +45,11 @@ def data_case(d, n, warm, K, loss="l2"):
     s.sync()
     dt = time.perf_counter() - t0
     r = s.poll()
-    print(f"data {loss} d={d} n={n}: {K / dt:.2f} steps/s ({dt / K * 1e3:.2f} ms/step) iters={r.iters}", flush=True)
+    pp = s.profile_parts(2)
+    f = 2.0 * n * d * d
+    print(f"data {loss} d={d} n={n}: {K / dt:.2f} steps/s ({dt / K * 1e3:.2f} ms/step) iters={r.iters}",
+          {k: round(v, 4) for k, v in pp.items()},
+          f"TF xw={f / pp['gemm_xw'] / 1e9:.1f} xty={f / pp['gemm_xty'] / 1e9:.1f}", flush=True)
     s.close()
 
 
