@@ -64,7 +64,7 @@ struct State {
   double obj_prev;
   double obj_last, score_last, h_last, l1_last;
   int32_t flags;         // bit0: inverse has an entry < 0 after +1e-16; bit1: non-finite
-  int32_t pad_;
+  int32_t warm_valid;    // Pstore holds the diagonal-block inverses of the previous slot
 };
 
 // One checkpoint record (linear.py:280-326 subset; norms are a later row).

@@ -174,37 +174,122 @@ __device__ void invert_tile32(double* __restrict__ img, double* __restrict__ Pou
   __syncthreads();
 }
 
+// Warm-started Newton-Schulz inverse of the 32 x 32 tile S (LDS image Sl, [m][k] stride SA32):
+//   X <- X + X (I - S X), starting from X0 = the same block's inverse one Adam step earlier
+//   (W moves by ~lr per step, so ||I - S X0|| is ~1e-3).  ||R_new|| <= ||R||^2, so once
+//   32 max|R_ij| (>= ||R||_inf) <= 1e-8 the update lands at residual <= 1e-16 and we stop.
+// Returns false (caller falls back to Gauss-Jordan) if the start is too far or does not
+// converge in 4 updates.  On success the inverse is in `x` (accumulator layout).
+// LDS: Xl [m][k] (SA32), Xr / Rr [k][n] (SB32), red[4].  All threads must call it.
+__device__ bool ns_invert_tile32(const double* __restrict__ Sl, const double* __restrict__ X0, double* Xl,
+                                 double* Xr, double* Rr, double* red, dbl4& x) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  acc_foreach(x, [&](int row, int col, double& v) {
+    v = X0[row * NB + col];
+    Xl[row * SA32 + col] = v;
+    Xr[row * SB32 + col] = v;
+  });
+  __syncthreads();
+  for (int it = 0; it < 5; ++it) {
+    dbl4 sx = {0.0, 0.0, 0.0, 0.0};
+    mma32(Sl, Xr, sx);
+    double amax = 0.0;
+    acc_foreach(sx, [&](int row, int col, double& v) {
+      v = (row == col ? 1.0 : 0.0) - v;  // R = I - S X
+      amax = fmax(amax, fabs(v)) + (isfinite(v) ? 0.0 : 1e300);
+      Rr[row * SB32 + col] = v;
+    });
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) amax = fmax(amax, __shfl_xor(amax, off));
+    if (lane == 0) red[w] = amax;
+    __syncthreads();  // Rr complete, red complete
+    const double rho = 32.0 * fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    if (!(rho <= 0.25)) return false;  // too far from the warm start (or NaN)
+    dbl4 xr = {0.0, 0.0, 0.0, 0.0};
+    mma32(Xl, Rr, xr);
+    __syncthreads();  // all reads of Xl / Xr / Rr / red done
+#pragma unroll
+    for (int t = 0; t < 4; ++t) x[t] = x[t] + xr[t];
+    if (rho <= 1e-8) return true;
+    if (it == 4) return false;
+    acc_foreach(x, [&](int row, int col, double& v) {
+      Xl[row * SA32 + col] = v;
+      Xr[row * SB32 + col] = v;
+    });
+    __syncthreads();
+  }
+  return false;
+}
+
+// Invert the 32 x 32 tile `acc` (accumulator layout) into Pn (+ Pstore), Gauss-Jordan when
+// pivots are wanted or no warm start exists, else warm-started Newton-Schulz.
+__device__ void invert_diag_tile(dbl4& acc, double* __restrict__ Pn, double* __restrict__ Pstore,
+                                 double* __restrict__ plog, bool want_gj, double* L0, double* L1, double* R0,
+                                 double* T0, double* scratch) {
+  __syncthreads();  // operand images of the caller are free
+  acc_foreach(acc, [&](int row, int col, double& v) { L0[row * SA32 + col] = v; });
+  __syncthreads();
+  if (!want_gj) {
+    dbl4 x;
+    if (ns_invert_tile32(L0, Pstore, L1, R0, T0, scratch, x)) {
+      acc_foreach(x, [&](int row, int col, double& v) {
+        Pn[row * NB + col] = v;
+        Pstore[row * NB + col] = v;
+      });
+      return;
+    }
+    __syncthreads();
+  }
+  invert_tile32(L0, Pn, plog, scratch);
+  if (Pstore) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int it = 0; it < NB * NB / NTHREADS; ++it) {
+      const int e = it * NTHREADS + tid;
+      Pstore[e] = Pn[e];
+    }
+  }
+}
+
 // Prologue: publish step 0's panels and invert A_00.
 __global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __restrict__ A, int64_t D,
                                                                double* __restrict__ Cside,
                                                                double* __restrict__ Rside,
                                                                double* __restrict__ Pside,
                                                                double* __restrict__ pivlog,
+                                                               double* __restrict__ Pstore,
                                                                const State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
-  __shared__ __attribute__((aligned(16))) double img[NB * SA32];
+  __shared__ __attribute__((aligned(16))) double L0[NB * SA32];
+  __shared__ __attribute__((aligned(16))) double L1[NB * SA32];
+  __shared__ __attribute__((aligned(16))) double R0[NB * SB32];
+  __shared__ __attribute__((aligned(16))) double T0[NB * SB32];
   __shared__ double scratch[4 * NB];
   const int t = blockIdx.x;
   tile32_copy(Cside + (int64_t)t * NB * NB, NB, A + (int64_t)t * NB * D, D);  // column 0
   tile32_copy(Rside + (int64_t)t * NB, D, A + (int64_t)t * NB, D);            // row 0
   if (t != 0) return;
-  tile32_to_lds<SA32>(img, A, D, 1.0);
-  __syncthreads();
-  invert_tile32(img, Pside, pivlog, scratch);
+  dbl4 acc;
+  acc_foreach(acc, [&](int row, int col, double& v) { v = A[(int64_t)row * D + col]; });
+  const bool want_gj = st == nullptr || Pstore == nullptr || st->ckpt_pending || !st->warm_valid;
+  invert_diag_tile(acc, Pside, Pstore, pivlog, want_gj, L0, L1, R0, T0, scratch);
 }
 
 // One block step of the elimination (see file header).
 //   side buffers: Cside[2] (D x NB), Rside[2] (NB x D), Pside[2] (NB x NB), parity k & 1 read.
+//   Every operand is requested from memory at kernel entry, so each step pays one
+//   global-load latency before its MFMA chain.
 __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ A, int64_t D, int k,
                                                            double* __restrict__ Cside0, double* __restrict__ Cside1,
                                                            double* __restrict__ Rside0, double* __restrict__ Rside1,
                                                            double* __restrict__ Pside0, double* __restrict__ Pside1,
-                                                           double* __restrict__ pivlog,
+                                                           double* __restrict__ pivlog, double* __restrict__ Pstore,
                                                            const State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
-  __shared__ __attribute__((aligned(16))) double L0[NB * SA32];   // left operand
-  __shared__ __attribute__((aligned(16))) double R0[NB * SB32];   // right operand
-  __shared__ __attribute__((aligned(16))) double T0[NB * SB32];   // intermediate P R_j
+  __shared__ __attribute__((aligned(16))) double L0[NB * SA32];   // P   ([m][k])
+  __shared__ __attribute__((aligned(16))) double L1[NB * SA32];   // -C_i ([m][k])
+  __shared__ __attribute__((aligned(16))) double R0[NB * SB32];   // R_j or P ([k][n])
+  __shared__ __attribute__((aligned(16))) double T0[NB * SB32];   // P R_j ([k][n])
   __shared__ double scratch[4 * NB];
   const int bi = blockIdx.y, bj = blockIdx.x;
   const int K = (int)(D / NB);
@@ -219,32 +304,31 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
 
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   if (bi == k && bj == k) {
-    // A_kk = P (read directly into the accumulator layout)
-    acc_foreach(acc, [&](int row, int col, double& v) { v = P[row * NB + col]; });
+    acc_foreach(acc, [&](int row, int col, double& v) { v = P[row * NB + col]; });  // A_kk = P
   } else if (bi == k) {
-    // A_kj = P R_j
-    tile32_to_lds<SA32>(L0, P, NB, 1.0);
+    tile32_to_lds<SA32>(L0, P, NB, 1.0);  // A_kj = P R_j
     tile32_to_lds<SB32>(R0, Rs + (int64_t)bj * NB, D, 1.0);
     __syncthreads();
     mma32(L0, R0, acc);
   } else if (bj == k) {
-    // A_ik = -C_i P
-    tile32_to_lds<SA32>(L0, Cs + (int64_t)bi * NB * NB, NB, -1.0);
+    tile32_to_lds<SA32>(L1, Cs + (int64_t)bi * NB * NB, NB, -1.0);  // A_ik = -C_i P
     tile32_to_lds<SB32>(R0, P, NB, 1.0);
     __syncthreads();
-    mma32(L0, R0, acc);
+    mma32(L1, R0, acc);
   } else {
-    // T = P R_j ; A_ij += (-C_i) T
+    // T = P R_j ; A_ij += (-C_i) T        (all four operands requested up front)
     tile32_to_lds<SA32>(L0, P, NB, 1.0);
     tile32_to_lds<SB32>(R0, Rs + (int64_t)bj * NB, D, 1.0);
+    tile32_to_lds<SA32>(L1, Cs + (int64_t)bi * NB * NB, NB, -1.0);
+    dbl4 a_old;
+    acc_foreach(a_old, [&](int row, int col, double& v) { v = Aij[(int64_t)row * D + col]; });
     __syncthreads();
-    mma32(L0, R0, acc);
-    acc_foreach(acc, [&](int row, int col, double& v) { T0[row * SB32 + col] = v; });
-    __syncthreads();  // T complete; L0 free
-    tile32_to_lds<SA32>(L0, Cs + (int64_t)bi * NB * NB, NB, -1.0);
-    acc_foreach(acc, [&](int row, int col, double& v) { v = Aij[(int64_t)row * D + col]; });
+    dbl4 tq = {0.0, 0.0, 0.0, 0.0};
+    mma32(L0, R0, tq);
+    acc_foreach(tq, [&](int row, int col, double& v) { T0[row * SB32 + col] = v; });
     __syncthreads();
-    mma32(L0, T0, acc);
+    acc = a_old;
+    mma32(L1, T0, acc);
   }
   acc_foreach(acc, [&](int row, int col, double& v) { Aij[(int64_t)row * D + col] = v; });
   if (k + 1 >= K) return;
@@ -252,10 +336,9 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
   if (bj == k1) acc_foreach(acc, [&](int row, int col, double& v) { Cn[((int64_t)bi * NB + row) * NB + col] = v; });
   if (bi == k1) acc_foreach(acc, [&](int row, int col, double& v) { Rn[(int64_t)row * D + (int64_t)bj * NB + col] = v; });
   if (bi == k1 && bj == k1) {
-    __syncthreads();  // L0 / T0 reads done
-    acc_foreach(acc, [&](int row, int col, double& v) { L0[row * SA32 + col] = v; });
-    __syncthreads();
-    invert_tile32(L0, Pn, pivlog ? pivlog + (int64_t)k1 * NB : nullptr, scratch);
+    const bool want_gj = st == nullptr || Pstore == nullptr || st->ckpt_pending || !st->warm_valid;
+    invert_diag_tile(acc, Pn, Pstore ? Pstore + (int64_t)k1 * NB * NB : nullptr,
+                     pivlog ? pivlog + (int64_t)k1 * NB : nullptr, want_gj, L0, L1, R0, T0, scratch);
   }
 }
 
@@ -280,10 +363,11 @@ void launch_gj_inverse(double* A, int64_t D, const GJWork& w, const State* st, h
   double* R1 = w.R + NB * D;
   double* P0 = w.P;
   double* P1 = w.P + NB * NB;
-  hipLaunchKernelGGL(gj_prologue_kernel, dim3(K), dim3(NTHREADS), 0, stream, A, D, C0, R0, P0, w.pivlog, st);
+  hipLaunchKernelGGL(gj_prologue_kernel, dim3(K), dim3(NTHREADS), 0, stream, A, D, C0, R0, P0, w.pivlog, w.Pstore,
+                     st);
   for (int k = 0; k < K; ++k)
     hipLaunchKernelGGL(gj_step_kernel, dim3(K, K), dim3(NTHREADS), 0, stream, A, D, k, C0, C1, R0, R1, P0, P1,
-                       w.pivlog, st);
+                       w.pivlog, w.Pstore, st);
   HIP_TRY(hipGetLastError());
 }
 

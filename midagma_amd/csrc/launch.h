@@ -22,6 +22,7 @@ struct GJWork {
   double* R;       // >= 2 x 32 x D   (row panels)
   double* C;       // >= 2 x D x 32   (column panels)
   double* pivlog;  // D  (log |pivot| per row, nullable)
+  double* Pstore = nullptr;  // D x 32: last inverse of every diagonal block (warm starts), nullable
 };
 
 // --- gj.hip -----------------------------------------------------------------

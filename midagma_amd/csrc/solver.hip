@@ -48,7 +48,7 @@ struct midagma_solver {
   bool own_stream = false;
   std::string err;
 
-  DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp;
+  DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
   double* zbuf = nullptr;  // d x d (+64 tail) score partial; internal or bound
   int64_t zbuf_cap = 0;
   // data mode
@@ -80,7 +80,7 @@ struct midagma_solver {
   ~midagma_solver() {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
-                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts})
+                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore})
       b->release();
     if (d_params) (void)hipFree(d_params);
     if (d_state) (void)hipFree(d_state);
@@ -100,7 +100,7 @@ struct midagma_solver {
     graphs_valid = false;
   }
 
-  GJWork gj() { return GJWork{P.p, R.p, C.p, pivlog.p}; }
+  GJWork gj() { return GJWork{P.p, R.p, C.p, pivlog.p, Pstore.p}; }
 
   // ---- the slot -----------------------------------------------------------
   void enqueue_part1() {
@@ -189,6 +189,7 @@ struct midagma_solver {
     R.alloc((size_t)64 * D);
     C.alloc((size_t)D * 64);
     pivlog.alloc(D);
+    Pstore.alloc((size_t)D * 32);
     partials.alloc(2 * NRED);
     if (D % 128 == 0 && (D / 128) * (D / 128) < 256) {
       cov_split = (int)std::min<int64_t>(4, D / 128);
@@ -708,7 +709,9 @@ int midagma_h(midagma_solver* s, const double* W, double s_dom, double* h, doubl
     DevBuf work;
     work.alloc(DD);
     launch_build_at(s->scratch.p, D, true, work.p, D, d, s_dom, nullptr, nullptr, s->stream);
-    launch_gj_inverse(work.p, D, s->gj(), nullptr, s->stream);
+    GJWork gw = s->gj();
+    gw.Pstore = nullptr;
+    launch_gj_inverse(work.p, D, gw, nullptr, s->stream);
     std::vector<double> pl(D);
     HIP_TRY(hipMemcpyAsync(pl.data(), s->pivlog.p, D * sizeof(double), hipMemcpyDeviceToHost, s->stream));
     if (G) {

@@ -87,6 +87,7 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
   }
   if (threadIdx.x != 0) return;
   st->slots += 1;
+  st->warm_valid = 1;  // this slot's GJ pass stored every diagonal-block inverse
   const int flags = st->flags;
   st->flags = 0;
   if (ck) {
