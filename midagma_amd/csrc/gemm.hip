@@ -123,45 +123,52 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
   const int r = lane & 15, kq = lane >> 4;
   const int mb = (w >> 1) * 64, nbs = (w & 1) * 64;
 
-  double2 ra[4], rb[4];
-  auto load = [&](int64_t kt) {
+  // Register prefetch of the next k-tile.  Straight-line code (no lambdas, no conditional
+  // loads) so the staging registers stay in VGPRs; the last iteration re-loads its own
+  // tile into the idle buffer, which is harmless.
+  double2 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
+  // tile-invariant per-thread offsets (32-bit) and uniform tile bases
+  const double* Ablk = ATRANS ? A + m0 : A + m0 * lda;
+  const int64_t a_kstride = ATRANS ? lda : 1;
+  const double* Bblk = B + n0;
+  int offA[4], offB[4];
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int i = it * NTHREADS + tid;
-      if (ATRANS) {
-        const int krow = i >> 6, c2 = i & 63;
-        ra[it] = *reinterpret_cast<const double2*>(A + (kt + krow) * lda + m0 + 2 * c2);
-      } else {
-        const int mrow = i >> 3, k2 = i & 7;
-        ra[it] = *reinterpret_cast<const double2*>(A + (m0 + mrow) * lda + kt + 2 * k2);
-      }
-      const int krow = i >> 6, c2 = i & 63;
-      double2 v = *reinterpret_cast<const double2*>(B + (kt + krow) * ldb + n0 + 2 * c2);
-      if (BMODE == B_IMINUS) {
-        const int64_t kg = kt + krow, ng = n0 + 2 * c2;
-        v.x = (kg == ng ? 1.0 : 0.0) - v.x;
-        v.y = (kg == ng + 1 ? 1.0 : 0.0) - v.y;
-      }
-      rb[it] = v;
-    }
-  };
-  auto store = [&](int buf) {
-    double* As = smem + buf * 2 * G_IMG;
-    double* Bs = As + G_IMG;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int i = it * NTHREADS + tid;
-      if (ATRANS) {
-        const int krow = i >> 6, c2 = i & 63;
-        *reinterpret_cast<double2*>(As + krow * G_SKM + 2 * c2) = ra[it];
-      } else {
-        const int mrow = i >> 3, k2 = i & 7;
-        *reinterpret_cast<double2*>(As + mrow * G_SMK + 2 * k2) = ra[it];
-      }
-      const int krow = i >> 6, c2 = i & 63;
-      *reinterpret_cast<double2*>(Bs + krow * G_SKM + 2 * c2) = rb[it];
-    }
-  };
+  for (int it = 0; it < 4; ++it) {
+    const int i_ = it * NTHREADS + tid;
+    offA[it] = ATRANS ? (i_ >> 6) * (int)lda + 2 * (i_ & 63) : (i_ >> 3) * (int)lda + 2 * (i_ & 7);
+    offB[it] = (i_ >> 6) * (int)ldb + 2 * (i_ & 63);
+  }
+#define G128_LOAD1(IT, RA, RB, KT)                                                              \
+  {                                                                                             \
+    const int i_ = (IT) * NTHREADS + tid;                                                       \
+    RA = *reinterpret_cast<const double2*>(Ablk + (KT) * a_kstride + offA[IT]);                 \
+    double2 v_ = *reinterpret_cast<const double2*>(Bblk + (KT) * ldb + offB[IT]);               \
+    if (BMODE == B_IMINUS) {                                                                    \
+      const int64_t kg_ = (KT) + (i_ >> 6), ng_ = n0 + 2 * (i_ & 63);                            \
+      v_.x = (kg_ == ng_ ? 1.0 : 0.0) - v_.x;                                                    \
+      v_.y = (kg_ == ng_ + 1 ? 1.0 : 0.0) - v_.y;                                                \
+    }                                                                                           \
+    RB = v_;                                                                                    \
+  }
+#define G128_STORE1(IT, RA, RB, AS, BS)                                                        \
+  {                                                                                             \
+    const int i_ = (IT) * NTHREADS + tid;                                                       \
+    if (ATRANS)                                                                                 \
+      *reinterpret_cast<double2*>((AS) + (i_ >> 6) * G_SKM + 2 * (i_ & 63)) = RA;               \
+    else                                                                                        \
+      *reinterpret_cast<double2*>((AS) + (i_ >> 3) * G_SMK + 2 * (i_ & 7)) = RA;                \
+    *reinterpret_cast<double2*>((BS) + (i_ >> 6) * G_SKM + 2 * (i_ & 63)) = RB;                 \
+  }
+#define G128_LOAD(KT)                 \
+  G128_LOAD1(0, ra0, rb0, KT)         \
+  G128_LOAD1(1, ra1, rb1, KT)         \
+  G128_LOAD1(2, ra2, rb2, KT)         \
+  G128_LOAD1(3, ra3, rb3, KT)
+#define G128_STORE(AS, BS)            \
+  G128_STORE1(0, ra0, rb0, AS, BS)    \
+  G128_STORE1(1, ra1, rb1, AS, BS)    \
+  G128_STORE1(2, ra2, rb2, AS, BS)    \
+  G128_STORE1(3, ra3, rb3, AS, BS)
 
   dbl4 acc[4][4];
 #pragma unroll
@@ -169,17 +176,18 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
 
-  int buf = 0;
+  double* As0 = smem;
+  double* As1 = smem + 2 * G_IMG;
   if (k_begin < k_end) {
-    load(k_begin);
-    store(0);
+    G128_LOAD(k_begin)
+    G128_STORE(As0, As0 + G_IMG)
   }
   __syncthreads();
   for (int64_t kt = k_begin; kt < k_end; kt += G_BK) {
-    const bool more = kt + G_BK < k_end;
-    if (more) load(kt + G_BK);
-    const double* As = smem + buf * 2 * G_IMG;
-    const double* Bs = As + G_IMG;
+    const int64_t kn = (kt + G_BK < k_end) ? kt + G_BK : kt;
+    G128_LOAD(kn)
+    const double* As = As0;
+    const double* Bs = As0 + G_IMG;
 #pragma unroll
     for (int kk = 0; kk < G_BK / 4; ++kk) {
       const int k = kk * 4 + kq;
@@ -194,10 +202,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store(buf ^ 1);
+    G128_STORE(As1, As1 + G_IMG)
     __syncthreads();
-    buf ^= 1;
+    double* tmp = As0;
+    As0 = As1;
+    As1 = tmp;
   }
+#undef G128_LOAD
+#undef G128_STORE
+#undef G128_LOAD1
+#undef G128_STORE1
 
   double* Ct = C + (int64_t)z * slice_stride;
   if (EPI == EPI_STORE) {
