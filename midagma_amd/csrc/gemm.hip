@@ -186,6 +186,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
   for (int64_t kt = k_begin; kt < k_end; kt += G_BK) {
     const int64_t kn = (kt + G_BK < k_end) ? kt + G_BK : kt;
     G128_LOAD(kn)
+    // keep the prefetch issued ahead of the MFMA block (hipcc otherwise sinks the loads next to
+    // their LDS stores, serializing memory latency and compute)
+    __builtin_amdgcn_sched_barrier(0);
     const double* As = As0;
     const double* Bs = As0 + G_IMG;
 #pragma unroll
