@@ -275,6 +275,27 @@ def cpu_baseline(args, cov):
     return res
 
 
+_PMC_KERNEL = {"gemm_xw": "midagma::gemm128_kernel<false, 1, 0>", "gemm_xty": "midagma::gemm128_kernel<true, 0, 0>"}
+
+
+def _pmc_traffic(kernel, d, n, world):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this exact
+    workload (profiles/*_pmc_bench_data_*.json; FETCH_SIZE x2 + WRITE_SIZE), else None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_bench_data_*.json")), reverse=True):
+        try:
+            j = json.load(open(f))
+            w = j.get("workload", {})
+            if (w.get("d"), w.get("n"), w.get("world")) != (d, n, world):
+                continue
+            k = j["kernels"].get(_PMC_KERNEL.get(kernel, ""))
+            if k:
+                return k["hbm_bytes_corrected"], os.path.relpath(f, REPO)
+        except Exception:  # noqa: BLE001
+            continue
+    return None, None
+
+
 def main():
     args = parse()
     import torch
@@ -300,8 +321,11 @@ def main():
             cfg = {"workload": f"config4: d={d}, n={args.n} linear-Gaussian SEM, l2, data mode, rows sharded over "
                                f"{world} GPU(s)", "d": d, "n": args.n, "n_per_gpu": n_k,
                    "parallelism": f"dp{world} (row shards, W replicated)"}
+            traffic, traffic_src = _pmc_traffic(dom, d, args.n, world)
             roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                    "frac": (ach / FP64_MFMA_PEAK_TF) if ach else None, "traffic": None,
+                    "frac": (ach / FP64_MFMA_PEAK_TF) if ach else None, "traffic": traffic,
+                    "traffic_source": traffic_src,
+                    "algorithmic_bytes_per_launch": 8.0 * 2 * n_k * d + 8.0 * d * d,
                     "algorithmic_per_launch": f"2*n_k*d^2 = {gemm_flops:.3e} flop",
                     "kernel_ms": {k: round(v, 4) for k, v in prof.items()}}
             verified = res["verified"]
