@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-cov", action="store_true")
     p.add_argument("--profile-reps", type=int, default=3)
+    p.add_argument("--no-fit", action="store_true", help="skip the full-fit wall-clock leg (config 2)")
     return p.parse_args()
 
 
@@ -230,6 +231,23 @@ def _cpu_runs(mode, d, extra, cands, env_base):
     return out
 
 
+def bench_fit(args, device):
+    """Full-fit wall-clock (BASELINE metric, second half): DagmaLinear.fit with the reference's
+    defaults (T=5, warm 3e4, max 6e4, s=[1,.9,.8,.7,.6], lr 3e-4, lambda1 0.03) at config 2."""
+    from midagma_amd import DagmaLinear
+    from midagma_amd.simulate import count_accuracy, make_dataset
+    X, W_true, B_true = make_dataset(args.d, args.cov_n, seed=args.seed)
+    m = DagmaLinear("l2", device=device)
+    t0 = time.perf_counter()
+    W = m.fit(X.copy(), lambda1=0.03)
+    wall = time.perf_counter() - t0
+    iters = [e["iters"] for e in m.minimize_log]
+    acc = count_accuracy(B_true, W != 0)
+    return dict(wall_s=wall, total_iters=int(sum(iters)), stage_iters=iters,
+                calls=[{k: e[k] for k in ("mu", "s", "lr", "iters", "success", "early_stop")} for e in m.minimize_log],
+                accuracy=acc, h_final=float(m.h_final), score_final=float(m.score_final))
+
+
 def cpu_baseline(args, cov):
     """CPU oracle (numpy/scipy restatement of the reference, bit-identical at 1 thread) on the
     host cores, each thread count in an isolated child process (no GPU):
@@ -304,6 +322,9 @@ def main():
     cov_res = None
     if rank == 0 and (args.workload == "cov" or (world == 1 and not args.no_cov)):
         cov_res = bench_cov(args, local)
+    fit_res = None
+    if rank == 0 and world == 1 and not args.no_fit:
+        fit_res = bench_fit(args, local)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and cov_res is not None:
         cpu = cpu_baseline(args, cov_res["cov"])
@@ -366,6 +387,16 @@ def main():
             if "reference_algorithm" in cpu and cov_res is not None:
                 line["cpu_reference_algorithm"] = cpu["reference_algorithm"]
                 line["cov_mode_vs_cpu_reference_algorithm"] = cov_res["value"] / cpu["reference_algorithm"]["value"]
+        if fit_res is not None:
+            fr = dict(fit_res)
+            fr["workload"] = f"config2: DagmaLinear('l2').fit(X) defaults, d={d}, n={args.cov_n}, 1 GPU (cov mode)"
+            if cpu and "reference_algorithm" in cpu:
+                ref_v = cpu["reference_algorithm"]["value"]
+                fr["cpu_projected_wall_s"] = fr["total_iters"] / ref_v
+                fr["cpu_projection"] = ("GPU fit's total Adam steps / CPU reference-algorithm steps/s "
+                                        "(SURVEY 8d: a d=1000 CPU fit is too long to run)")
+                fr["vs_cpu_projected"] = fr["cpu_projected_wall_s"] / fr["wall_s"]
+            line["full_fit"] = fr
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

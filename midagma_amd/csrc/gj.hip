@@ -23,8 +23,28 @@
 namespace midagma {
 
 constexpr int NB = 32;        // block size of the elimination
-constexpr int SA32 = 34;      // [m][k] LDS image stride for 32-wide tiles (= 2 mod 32)
-constexpr int SB32 = 48;      // [k][n] LDS image stride (= 16 mod 32)
+
+#ifdef MIDAGMA_STAMPS
+// Diagnostic build only: s_memtime stamps of the diagonal-owner workgroup per block step.
+__device__ unsigned long long g_stamps[256][16];
+#define STAMP(k, slot)                                                                     \
+  do {                                                                                     \
+    if (threadIdx.x == 0) {                                                                \
+      unsigned long long t_;                                                               \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+      g_stamps[(k) & 255][slot] = t_;                                                      \
+    }                                                                                      \
+  } while (0)
+#else
+#define STAMP(k, slot) \
+  do {                 \
+  } while (0)
+#endif
+// Every 32 x 32 LDS image has row stride ST = 34 (= 2 mod 32 doubles): conflict-free as
+// an MFMA A operand ([m][k], lanes walk rows) and 2-way on one ds_read_b64 lane group as
+// a B operand ([k][n], lanes walk columns) -- one image then serves both roles, which the
+// Newton-Schulz iteration needs (X is the B operand of S X and the A operand of X R).
+constexpr int ST = 34;
 constexpr int EPT = NB * NB / NTHREADS;   // elements per thread in the tile inversion (4)
 constexpr int TPR = NB / EPT;             // threads per tile row (8)
 
@@ -70,16 +90,24 @@ __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __rest
 __device__ __forceinline__ int q_m0() { return (threadIdx.x >> 7) * 16; }
 __device__ __forceinline__ int q_n0() { return ((threadIdx.x >> 6) & 1) * 16; }
 
-// acc += Ls(32 x 32, [m][k] stride SA32) * Rs(32 x 32, [k][n] stride SB32)
+// acc += Ls * Rs, both 32 x 32 LDS images (row stride ST).  Four independent MFMA
+// chains (k mod 16) summed at the end: a dependent chain leaves the SIMD's matrix pipe
+// idle between its MFMAs, and co-resident workgroups' MFMAs take those slots -- with
+// independent chains a high-priority wave (the diagonal owner) keeps the pipe.
 __device__ __forceinline__ void mma32(const double* __restrict__ Ls, const double* __restrict__ Rs, dbl4& acc) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
-  const int m0 = q_m0(), n0 = q_n0();
-#pragma unroll
-  for (int k0 = 0; k0 < NB; k0 += 4) {
-    const double a = Ls[(m0 + r) * SA32 + k0 + kq];
-    const double b = Rs[(k0 + kq) * SB32 + n0 + r];
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-  }
+  const double* La = Ls + (q_m0() + r) * ST + kq;
+  const double* Rb = Rs + kq * ST + q_n0() + r;
+  const dbl4 z = {0.0, 0.0, 0.0, 0.0};
+  dbl4 c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[0], Rb[0], acc, 0, 0, 0);
+  dbl4 c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[4], Rb[4 * ST], z, 0, 0, 0);
+  dbl4 c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[8], Rb[8 * ST], z, 0, 0, 0);
+  dbl4 c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[12], Rb[12 * ST], z, 0, 0, 0);
+  c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[16], Rb[16 * ST], c0, 0, 0, 0);
+  c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[20], Rb[20 * ST], c1, 0, 0, 0);
+  c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[24], Rb[24 * ST], c2, 0, 0, 0);
+  c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[28], Rb[28 * ST], c3, 0, 0, 0);
+  acc = (c0 + c1) + (c2 + c3);
 }
 
 template <class F>
@@ -94,8 +122,7 @@ __device__ __forceinline__ void acc_foreach(dbl4& acc, F&& f) {
   }
 }
 
-// 32 x 32 global tile (leading dim ld) -> LDS image with stride S, scaled by `sc`
-template <int S>
+// 32 x 32 global tile (leading dim ld) -> LDS image (stride ST), scaled by `sc`
 __device__ __forceinline__ void tile32_to_lds(double* __restrict__ dst, const double* __restrict__ src, int64_t ld,
                                               double sc) {
 #pragma unroll
@@ -105,7 +132,7 @@ __device__ __forceinline__ void tile32_to_lds(double* __restrict__ dst, const do
     double2 v = *reinterpret_cast<const double2*>(src + row * ld + c);
     v.x *= sc;
     v.y *= sc;
-    *reinterpret_cast<double2*>(dst + row * S + c) = v;
+    *reinterpret_cast<double2*>(dst + row * ST + c) = v;
   }
 }
 
@@ -119,6 +146,47 @@ __device__ __forceinline__ void tile32_copy(double* __restrict__ dst, int64_t ld
   }
 }
 
+// Store for data the NEXT launch reads: write-through (sc1), so the tile does not sit
+// dirty in this XCD's L2 and the kernel boundary has nothing of it to write back
+// (MI355X_MICROARCH.md price list: a boundary pays dirty bytes / ~6 TB/s).
+__device__ __forceinline__ void st_wt(double* p, double v) {
+#ifdef MIDAGMA_GJ_PLAIN_STORES
+  *p = v;
+#else
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
+// max over the 64 lanes of a wave of a non-negative float: DPP within each row of 16
+// (quad swaps, half-row and row mirrors: single v_max_f32_dpp ops), then the four row
+// results by readlane.  No LDS round trip.
+template <int CTRL>
+__device__ __forceinline__ float dpp_max(float v) {
+  return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false)));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = dpp_max<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = dpp_max<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = dpp_max<0x141>(v);  // row_half_mirror
+  v = dpp_max<0x140>(v);  // row_mirror
+  const int b = __float_as_int(v);
+  return fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(b, 0)), __int_as_float(__builtin_amdgcn_readlane(b, 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(b, 32)), __int_as_float(__builtin_amdgcn_readlane(b, 48))));
+}
+
+// Two independent 32 x 32 products in one pass (their MFMA chains interleave):
+//   c1 += A1 * B1,  c2 += A2 * B2   (LDS images, stride ST)
+__device__ __forceinline__ void mma32x2(const double* __restrict__ A1, const double* __restrict__ B1, dbl4& c1,
+                                        const double* __restrict__ A2, const double* __restrict__ B2, dbl4& c2) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int ao = (q_m0() + r) * ST + kq, bo = kq * ST + q_n0() + r;
+#pragma unroll
+  for (int k0 = 0; k0 < NB; k0 += 4) {
+    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(A1[ao + k0], B1[bo + k0 * ST], c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(A2[ao + k0], B2[bo + k0 * ST], c2, 0, 0, 0);
+  }
+}
+
 // Reciprocal to ~1 ulp: hardware seed + two Newton steps (no IEEE division chain).
 __device__ __forceinline__ double fast_rcp(double x) {
   double r = __builtin_amdgcn_rcp(x);
@@ -128,10 +196,10 @@ __device__ __forceinline__ double fast_rcp(double x) {
   return __builtin_fma(r, e, r);
 }
 
-// In-place unpivoted GJ inverse of the 32 x 32 tile held in `img` (row stride SA32)
+// In-place unpivoted GJ inverse of the 32 x 32 tile held in `img` (row stride ST)
 // by the whole workgroup; writes the inverse to Pout (ld NB) and log|pivot| to plog.
 // `scratch` needs 4*NB doubles.  Ends with a barrier.
-__device__ void invert_tile32(double* __restrict__ img, double* __restrict__ Pout, double* __restrict__ plog,
+__device__ __forceinline__ void invert_tile32(double* __restrict__ img, double* __restrict__ Pout, double* __restrict__ plog,
                               double* __restrict__ scratch) {
   const int tid = threadIdx.x;
   const int r = tid / TPR, c0 = (tid % TPR) * EPT;
@@ -139,7 +207,7 @@ __device__ void invert_tile32(double* __restrict__ img, double* __restrict__ Pou
   double* colbuf = scratch + 2 * NB;  // [2][NB]
   double a[EPT];
 #pragma unroll
-  for (int e = 0; e < EPT; ++e) a[e] = img[r * SA32 + c0 + e];
+  for (int e = 0; e < EPT; ++e) a[e] = img[r * ST + c0 + e];
   double pivs = 0.0;  // lane p of wave 0 keeps pivot p (p < 32)
   for (int pb = 0; pb < NB; pb += EPT) {
 #pragma unroll
@@ -174,73 +242,90 @@ __device__ void invert_tile32(double* __restrict__ img, double* __restrict__ Pou
   __syncthreads();
 }
 
-// Warm-started Newton-Schulz inverse of the 32 x 32 tile S (LDS image Sl, [m][k] stride SA32):
-//   X <- X + X (I - S X), starting from X0 = the same block's inverse one Adam step earlier
-//   (W moves by ~lr per step, so ||I - S X0|| is ~1e-3).  ||R_new|| <= ||R||^2, so once
-//   32 max|R_ij| (>= ||R||_inf) <= 1e-8 the update lands at residual <= 1e-16 and we stop.
-// Returns false (caller falls back to Gauss-Jordan) if the start is too far or does not
-// converge in 4 updates.  On success the inverse is in `x` (accumulator layout).
-// LDS: Xl [m][k] (SA32), Xr / Rr [k][n] (SB32), red[4].  All threads must call it.
-__device__ bool ns_invert_tile32(const double* __restrict__ Sl, const double* __restrict__ X0, double* Xl,
-                                 double* Xr, double* Rr, double* red, dbl4& x) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  acc_foreach(x, [&](int row, int col, double& v) {
-    v = X0[row * NB + col];
-    Xl[row * SA32 + col] = v;
-    Xr[row * SB32 + col] = v;
-  });
-  __syncthreads();
-  for (int it = 0; it < 5; ++it) {
-    dbl4 sx = {0.0, 0.0, 0.0, 0.0};
-    mma32(Sl, Xr, sx);
-    double amax = 0.0;
-    acc_foreach(sx, [&](int row, int col, double& v) {
-      v = (row == col ? 1.0 : 0.0) - v;  // R = I - S X
-      amax = fmax(amax, fabs(v)) + (isfinite(v) ? 0.0 : 1e300);
-      Rr[row * SB32 + col] = v;
-    });
+// Warm-started inverse of the 32 x 32 tile S by a product-form Neumann series.
+//   X0 = the same block's inverse one Adam step earlier (W moves by ~lr per step),
+//   R = I - S X0 (small), and  S^-1 = X0 (I - R)^-1 = X0 (I + R)(I + R^2)(I + R^4)...
+// Pass p holds Y = X0 (I + R)...(I + R^(2^(p-1))) and Q = R^(2^p) and computes the two
+// independent products  Y <- Y + Y Q,  Q <- Q Q  in one pass (interleaved MFMA chains),
+// one barrier per pass.  Q is the exact residual of the truncation (Y_p S = I - Q), so
+// once rho = 32 max|Q_ij| (>= ||Q||_inf) <= 1e-8 the last factor lands at residual
+// <= 1e-16 -- the same test as Newton-Schulz (whose residual after p steps is this Q),
+// with one barrier per doubling instead of two.
+// Returns false (caller falls back to Gauss-Jordan) if rho(R) > 0.25 or is not finite, or
+// no convergence within 5 doublings.  On success the inverse is in `x` (accumulator layout).
+// Precondition: Sl = S and Xa = X0 (= x) written and a barrier passed.  Sl, Xa, Rl, Xb
+// are four LDS images; the pass images ping-pong between (Xa, Rl) and (Sl, Xb).
+__device__ __forceinline__ float quad_absmax(const dbl4& q) {
+  float m = 0.0f;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) amax = fmax(amax, __shfl_xor(amax, off));
-    if (lane == 0) red[w] = amax;
-    __syncthreads();  // Rr complete, red complete
-    const double rho = 32.0 * fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-    if (!(rho <= 0.25)) return false;  // too far from the warm start (or NaN)
-    dbl4 xr = {0.0, 0.0, 0.0, 0.0};
-    mma32(Xl, Rr, xr);
-    __syncthreads();  // all reads of Xl / Xr / Rr / red done
-#pragma unroll
-    for (int t = 0; t < 4; ++t) x[t] = x[t] + xr[t];
-    if (rho <= 1e-8) return true;
-    if (it == 4) return false;
-    acc_foreach(x, [&](int row, int col, double& v) {
-      Xl[row * SA32 + col] = v;
-      Xr[row * SB32 + col] = v;
-    });
-    __syncthreads();
-  }
-  return false;
+  for (int t = 0; t < 4; ++t) m = fmaxf(m, isfinite(q[t]) ? (float)fabs(q[t]) : INFINITY);
+  return m;
 }
 
-// Invert the 32 x 32 tile `acc` (accumulator layout) into Pn (+ Pstore), Gauss-Jordan when
-// pivots are wanted or no warm start exists, else warm-started Newton-Schulz.
-__device__ void invert_diag_tile(dbl4& acc, double* __restrict__ Pn, double* __restrict__ Pstore,
-                                 double* __restrict__ plog, bool want_gj, double* L0, double* L1, double* R0,
-                                 double* T0, double* scratch) {
-  __syncthreads();  // operand images of the caller are free
-  acc_foreach(acc, [&](int row, int col, double& v) { L0[row * SA32 + col] = v; });
+__device__ __forceinline__ bool ns_invert_tile32(double* Sl, double* Xa, double* Xb, double* Rl, float* red,
+                                                 dbl4& x, int sk = 0) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  STAMP(sk, 5);
+  dbl4 q = {0.0, 0.0, 0.0, 0.0};
+  mma32(Sl, Xa, q);
+  acc_foreach(q, [&](int row, int col, double& v) {
+    v = (row == col ? 1.0 : 0.0) - v;  // R = I - S X0
+    Rl[row * ST + col] = v;
+  });
+  float amax = wave_max(quad_absmax(q));
+  if (lane == 0) red[w] = amax;
+  __syncthreads();  // R and red complete
+  STAMP(sk, 6);
+  double rho = 32.0 * (double)fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (!(rho <= 0.25)) return false;  // too far from the warm start (or not finite)
+  double *Y = Xa, *Q = Rl, *Yn = Sl, *Qn = Xb;
+  int p = 0;
+  for (; rho > 1e-8; ++p) {
+    if (p == 4) return false;
+    q = dbl4{0.0, 0.0, 0.0, 0.0};
+    mma32x2(Y, Q, x, Q, Q, q);  // x = Y + Y Q ; q = Q Q
+    acc_foreach(x, [&](int row, int col, double& v) { Yn[row * ST + col] = v; });
+    acc_foreach(q, [&](int row, int col, double& v) { Qn[row * ST + col] = v; });
+    amax = wave_max(quad_absmax(q));
+    if (lane == 0) red[4 * ((p + 1) & 1) + w] = amax;  // alternate slots: no read/write race
+    __syncthreads();  // Y, Q of the next pass complete; this pass's reads done
+    const float* rr = red + 4 * ((p + 1) & 1);
+    rho = 32.0 * (double)fmaxf(fmaxf(rr[0], rr[1]), fmaxf(rr[2], rr[3]));
+    double* t = Y;
+    Y = Yn;
+    Yn = t;
+    t = Q;
+    Q = Qn;
+    Qn = t;
+  }
+#ifdef MIDAGMA_STAMPS
+  if (threadIdx.x == 0) g_stamps[sk & 255][7] = p + 1;
+#endif
+  mma32(Y, Q, x);  // x = Y (I + Q)
+  return true;
+}
+
+// Invert the 32 x 32 tile `acc` (accumulator layout) into Pn (+ Pstore): warm-started
+// Newton-Schulz from x0 unless pivots are wanted (then, or on NS failure, Gauss-Jordan).
+// Precondition: no wave still reads Simg or Xa (the caller's last MFMA chain used Xb / Rl
+// at most).  Buffers: four 32 x ST images + scratch (4 * NB).
+__device__ __forceinline__ void invert_diag_tile(dbl4 acc, dbl4 x0, double* __restrict__ Pn, double* __restrict__ Pstore,
+                                 double* __restrict__ plog, bool want_gj, double* Simg, double* Xa, double* Xb,
+                                 double* Rl, double* scratch, int sk = 0) {
+  acc_foreach(acc, [&](int row, int col, double& v) { Simg[row * ST + col] = v; });
+  if (!want_gj) acc_foreach(x0, [&](int row, int col, double& v) { Xa[row * ST + col] = v; });
   __syncthreads();
   if (!want_gj) {
-    dbl4 x;
-    if (ns_invert_tile32(L0, Pstore, L1, R0, T0, scratch, x)) {
-      acc_foreach(x, [&](int row, int col, double& v) {
-        Pn[row * NB + col] = v;
-        Pstore[row * NB + col] = v;
+    if (ns_invert_tile32(Simg, Xa, Xb, Rl, reinterpret_cast<float*>(scratch), x0, sk)) {
+      acc_foreach(x0, [&](int row, int col, double& v) {
+        st_wt(Pn + row * NB + col, v);
+        st_wt(Pstore + row * NB + col, v);
       });
       return;
     }
     __syncthreads();
   }
-  invert_tile32(L0, Pn, plog, scratch);
+  invert_tile32(Simg, Pn, plog, scratch);
   if (Pstore) {
     const int tid = threadIdx.x;
 #pragma unroll
@@ -249,6 +334,10 @@ __device__ void invert_diag_tile(dbl4& acc, double* __restrict__ Pn, double* __r
       Pstore[e] = Pn[e];
     }
   }
+}
+
+__device__ __forceinline__ bool want_gauss_jordan(const double* Pstore, const State* st) {
+  return st == nullptr || Pstore == nullptr || st->ckpt_pending || !st->warm_valid;
 }
 
 // Prologue: publish step 0's panels and invert A_00.
@@ -260,25 +349,25 @@ __global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __r
                                                                double* __restrict__ Pstore,
                                                                const State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
-  __shared__ __attribute__((aligned(16))) double L0[NB * SA32];
-  __shared__ __attribute__((aligned(16))) double L1[NB * SA32];
-  __shared__ __attribute__((aligned(16))) double R0[NB * SB32];
-  __shared__ __attribute__((aligned(16))) double T0[NB * SB32];
+  __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
   __shared__ double scratch[4 * NB];
   const int t = blockIdx.x;
   tile32_copy(Cside + (int64_t)t * NB * NB, NB, A + (int64_t)t * NB * D, D);  // column 0
   tile32_copy(Rside + (int64_t)t * NB, D, A + (int64_t)t * NB, D);            // row 0
   if (t != 0) return;
-  dbl4 acc;
+  const bool want_gj = want_gauss_jordan(Pstore, st);
+  dbl4 acc, x0 = {0.0, 0.0, 0.0, 0.0};
   acc_foreach(acc, [&](int row, int col, double& v) { v = A[(int64_t)row * D + col]; });
-  const bool want_gj = st == nullptr || Pstore == nullptr || st->ckpt_pending || !st->warm_valid;
-  invert_diag_tile(acc, Pside, Pstore, pivlog, want_gj, L0, L1, R0, T0, scratch);
+  if (!want_gj) acc_foreach(x0, [&](int row, int col, double& v) { v = Pstore[row * NB + col]; });
+  invert_diag_tile(acc, x0, Pside, Pstore, pivlog, want_gj, img[0], img[1], img[2], img[3], scratch);
 }
 
 // One block step of the elimination (see file header).
 //   side buffers: Cside[2] (D x NB), Rside[2] (NB x D), Pside[2] (NB x NB), parity k & 1 read.
 //   Every operand is requested from memory at kernel entry, so each step pays one
-//   global-load latency before its MFMA chain.
+//   global-load latency before its MFMA chain.  The workgroup owning tile (k+1, k+1)
+//   carries the step's serial chain: it takes linear block id 0 (dispatched first),
+//   prefetches its warm start with the operands, inverts before any global store.
 __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ A, int64_t D, int k,
                                                            double* __restrict__ Cside0, double* __restrict__ Cside1,
                                                            double* __restrict__ Rside0, double* __restrict__ Rside1,
@@ -286,13 +375,17 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
                                                            double* __restrict__ pivlog, double* __restrict__ Pstore,
                                                            const State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
-  __shared__ __attribute__((aligned(16))) double L0[NB * SA32];   // P   ([m][k])
-  __shared__ __attribute__((aligned(16))) double L1[NB * SA32];   // -C_i ([m][k])
-  __shared__ __attribute__((aligned(16))) double R0[NB * SB32];   // R_j or P ([k][n])
-  __shared__ __attribute__((aligned(16))) double T0[NB * SB32];   // P R_j ([k][n])
+  __shared__ __attribute__((aligned(16))) double L0[NB * ST];  // P            ([m][k])
+  __shared__ __attribute__((aligned(16))) double L1[NB * ST];  // -C_i         ([m][k])
+  __shared__ __attribute__((aligned(16))) double R0[NB * ST];  // R_j or P     ([k][n])
+  __shared__ __attribute__((aligned(16))) double T0[NB * ST];  // P R_j        ([k][n])
   __shared__ double scratch[4 * NB];
-  const int bi = blockIdx.y, bj = blockIdx.x;
   const int K = (int)(D / NB);
+  const int k1 = k + 1;
+  const int own = k1 < K ? k1 * K + k1 : 0;  // linear id of the diagonal owner
+  int lin = blockIdx.y * K + blockIdx.x;
+  lin = lin == 0 ? own : (lin == own ? 0 : lin);
+  const int bi = lin / K, bj = lin - bi * K;
   const bool odd = k & 1;
   const double* Cs = odd ? Cside1 : Cside0;
   const double* Rs = odd ? Rside1 : Rside0;
@@ -301,48 +394,74 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
   double* Rn = odd ? Rside0 : Rside1;
   double* Pn = odd ? Pside0 : Pside1;
   double* Aij = A + (int64_t)bi * NB * D + (int64_t)bj * NB;
+  const bool owner = k1 < K && bi == k1 && bj == k1;
+  if (owner) {
+    __builtin_amdgcn_s_setprio(3);  // its waves win issue arbitration against co-resident tiles
+    STAMP(k, 0);
+  }
 
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   if (bi == k && bj == k) {
     acc_foreach(acc, [&](int row, int col, double& v) { v = P[row * NB + col]; });  // A_kk = P
   } else if (bi == k) {
-    tile32_to_lds<SA32>(L0, P, NB, 1.0);  // A_kj = P R_j
-    tile32_to_lds<SB32>(R0, Rs + (int64_t)bj * NB, D, 1.0);
+    tile32_to_lds(L0, P, NB, 1.0);  // A_kj = P R_j
+    tile32_to_lds(R0, Rs + (int64_t)bj * NB, D, 1.0);
     __syncthreads();
     mma32(L0, R0, acc);
   } else if (bj == k) {
-    tile32_to_lds<SA32>(L1, Cs + (int64_t)bi * NB * NB, NB, -1.0);  // A_ik = -C_i P
-    tile32_to_lds<SB32>(R0, P, NB, 1.0);
+    tile32_to_lds(L1, Cs + (int64_t)bi * NB * NB, NB, -1.0);  // A_ik = -C_i P
+    tile32_to_lds(R0, P, NB, 1.0);
     __syncthreads();
     mma32(L1, R0, acc);
   } else {
-    // T = P R_j ; A_ij += (-C_i) T        (all four operands requested up front)
-    tile32_to_lds<SA32>(L0, P, NB, 1.0);
-    tile32_to_lds<SB32>(R0, Rs + (int64_t)bj * NB, D, 1.0);
-    tile32_to_lds<SA32>(L1, Cs + (int64_t)bi * NB * NB, NB, -1.0);
+    // T = P R_j ; A_ij += (-C_i) T        (all operands requested up front)
+    bool want_gj = true;
+    dbl4 x0 = {0.0, 0.0, 0.0, 0.0};
+    if (owner) {
+      want_gj = want_gauss_jordan(Pstore, st);
+      if (!want_gj) {
+        const double* X0 = Pstore + (int64_t)k1 * NB * NB;
+        acc_foreach(x0, [&](int row, int col, double& v) { v = X0[row * NB + col]; });
+      }
+    }
+    tile32_to_lds(L0, P, NB, 1.0);
+    tile32_to_lds(R0, Rs + (int64_t)bj * NB, D, 1.0);
+    tile32_to_lds(L1, Cs + (int64_t)bi * NB * NB, NB, -1.0);
     dbl4 a_old;
     acc_foreach(a_old, [&](int row, int col, double& v) { v = Aij[(int64_t)row * D + col]; });
     __syncthreads();
+    if (owner) STAMP(k, 1);
     dbl4 tq = {0.0, 0.0, 0.0, 0.0};
     mma32(L0, R0, tq);
-    acc_foreach(tq, [&](int row, int col, double& v) { T0[row * SB32 + col] = v; });
+    acc_foreach(tq, [&](int row, int col, double& v) { T0[row * ST + col] = v; });
     __syncthreads();
+    if (owner) STAMP(k, 2);
     acc = a_old;
     mma32(L1, T0, acc);
+    if (owner) {
+      // the only serial chain of the elimination: invert first, store afterwards.
+      // L0 / R0 are free (last read before the barrier above); L1 / T0 after the next one.
+      STAMP(k, 3);
+#ifndef MIDAGMA_GJ_TIMING_NO_INV  // timing experiment only: results are wrong without it
+      invert_diag_tile(acc, x0, Pn, Pstore ? Pstore + (int64_t)k1 * NB * NB : nullptr, pivlog ? pivlog + (int64_t)k1 * NB : nullptr, want_gj, L0, R0, L1,
+                       T0, scratch, k);
+#endif
+      STAMP(k, 4);
+    }
   }
-  acc_foreach(acc, [&](int row, int col, double& v) { Aij[(int64_t)row * D + col] = v; });
-  if (k + 1 >= K) return;
-  const int k1 = k + 1;
-  if (bj == k1) acc_foreach(acc, [&](int row, int col, double& v) { Cn[((int64_t)bi * NB + row) * NB + col] = v; });
-  if (bi == k1) acc_foreach(acc, [&](int row, int col, double& v) { Rn[(int64_t)row * D + (int64_t)bj * NB + col] = v; });
-  if (bi == k1 && bj == k1) {
-    const bool want_gj = st == nullptr || Pstore == nullptr || st->ckpt_pending || !st->warm_valid;
-    invert_diag_tile(acc, Pn, Pstore ? Pstore + (int64_t)k1 * NB * NB : nullptr,
-                     pivlog ? pivlog + (int64_t)k1 * NB : nullptr, want_gj, L0, L1, R0, T0, scratch);
-  }
+  acc_foreach(acc, [&](int row, int col, double& v) { st_wt(Aij + (int64_t)row * D + col, v); });
+  if (k1 >= K) return;
+  if (bj == k1) acc_foreach(acc, [&](int row, int col, double& v) { st_wt(Cn + ((int64_t)bi * NB + row) * NB + col, v); });
+  if (bi == k1) acc_foreach(acc, [&](int row, int col, double& v) { st_wt(Rn + (int64_t)row * D + (int64_t)bj * NB + col, v); });
 }
 
 void gj_setup_attributes() {}
+
+#ifdef MIDAGMA_STAMPS
+extern "C" int midagma_debug_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
+}
+#endif
 
 void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int64_t D, int64_t d, double s,
                      const Params* pr, const State* st, hipStream_t stream) {

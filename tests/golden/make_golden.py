@@ -224,6 +224,37 @@ def gen_fit(X):
     np.savez_compressed(os.path.join(HERE, "fit_d20.npz"), **out)
 
 
+def gen_fit_envelope(X, seeds=(7, 11, 13, 17, 19, 23, 29, 31)):
+    """Several 1e-16-noise replicas of the default d=20 fit: the spread of the chaotic
+    last stage (iteration count, h_final, score_final, W) over noise seeds."""
+    rows = {"W_unthresholded": [], "h_final": [], "score_final": [], "last_iters": []}
+
+    class Spy(DagmaLinear):
+        def minimize(self, W, mu, max_iter, s, lr, tol=1e-6, beta_1=0.99, beta_2=0.999, pbar=None):
+            rec = Recorder()
+            Wr, ok = super().minimize(W, mu, max_iter, s, lr, tol, beta_1, beta_2, pbar=rec)
+            self.last_iters = rec.iters
+            return Wr, ok
+
+        def _h(self, W, s=1.0):
+            self.last_h_W = W.copy()
+            return super()._h(W, s)
+
+    def one_fit():
+        m = Spy(loss_type="l2", verbose=False)
+        m.fit(X.copy(), lambda1=0.03, s=[1.0, .9, .8, .7, .6])
+        return m
+
+    for sd in seeds:
+        m = with_noisy_inv(one_fit, seed=sd)
+        rows["W_unthresholded"].append(m.last_h_W)
+        rows["h_final"].append(m.h_final)
+        rows["score_final"].append(m.score_final)
+        rows["last_iters"].append(m.last_iters)
+    np.savez_compressed(os.path.join(HERE, "fit_d20_envelope.npz"), seeds=np.array(seeds),
+                        **{k: np.array(v, dtype=np.float64) for k, v in rows.items()})
+
+
 def gen_mlp():
     """DagmaMLP.h_func value and autograd gradient (nonlinear.py:68-86).
 
@@ -260,6 +291,7 @@ def main():
         gen_traj(Xl, "logistic_d20", [1, 10, 100, 1000], loss="logistic", lambda1=0.05)
         gen_branches(X20)
         gen_fit(X20)
+        gen_fit_envelope(X20)
         gen_mlp()
     print("golden fixtures written to", HERE)
 

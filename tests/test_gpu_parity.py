@@ -158,12 +158,17 @@ def test_full_fit_d20(hip, golden):
     ref_iters = [int(c[5]) for c in f["calls"]]
     assert iters[:4] == ref_iters[:4]
     assert abs(iters[4] - ref_iters[4]) <= 1000
-    env = float(np.abs(f["W_unthresholded"] - f["W_unthresholded_noisy"]).max())
+    # noise envelopes: the reference itself, refit with 1e-16 relative noise in every inverse
+    # under 9 seeds (fit_d20.npz + fit_d20_envelope.npz); tolerance = 2x the widest spread
+    e = golden("fit_d20_envelope.npz")
+    Wn = np.concatenate([f["W_unthresholded_noisy"][None], e["W_unthresholded"]])
+    hn = np.append(e["h_final"], float(f["h_final_noisy"]))
+    sn = np.append(e["score_final"], float(f["score_final_noisy"]))
+    env = float(np.abs(Wn - f["W_unthresholded"][None]).max())
+    env_h = float(np.abs(hn - float(f["h_final"])).max())
+    env_s = float(np.abs(sn - float(f["score_final"])).max())
     assert np.array_equal(W != 0, f["W"] != 0)
     assert np.abs(W - f["W"]).max() <= max(2 * env, 1e-5)
-    # h_final / score_final: within 2x the reference's own noise envelope (1e-16 in the inverse)
-    env_h = abs(float(f["h_final"]) - float(f["h_final_noisy"]))
-    env_s = abs(float(f["score_final"]) - float(f["score_final_noisy"]))
     assert abs(m.h_final - f["h_final"]) <= max(2 * env_h, 1e-12)
     assert abs(m.score_final - f["score_final"]) <= max(2 * env_s, 1e-9 * abs(float(f["score_final"])))
 
