@@ -104,12 +104,16 @@ int midagma_minimize(midagma_solver* s, double* W, double mu, int64_t max_iter, 
 int midagma_begin(midagma_solver* s, const double* W, double mu, int64_t max_iter, double s_dom, double lr,
                   double tol, double beta1, double beta2, double lambda1, int64_t checkpoint);
 int midagma_step_partial(midagma_solver* s);
-/* enqueue n whole slots (part 1 + part 2) without host polling; midagma_sync waits. */
+/* enqueue n whole slots (part 1 + part 2); midagma_sync waits.  Without host polling,
+ * except in cov mode with the blocked inverse (d > 192), where the host picks the fast or
+ * the GJ path per batch (one sync per batch of <= 64 slots). */
 int midagma_run_slots(midagma_solver* s, int64_t n);
 int midagma_sync(midagma_solver* s);
 /* Diagnostics: average device time (hipEvents on the solver stream, `reps` launches each)
  * of the slot's parts: [0] build (sI-WoW)^T, [1] GJ inverse, [2] score GEMM(s), [3] whole
- * slot, [4] data-mode X(I-W) GEMM, [5] data-mode X^T Y GEMM.  Advances the state by reps slots. */
+ * slot (GJ path), [4] data-mode X(I-W) GEMM, [5] data-mode X^T Y GEMM, [6] cov-mode fast
+ * blocked inverse, [7] whole fast slot ([6], [7]: 0 if not available, -1 if the fast path
+ * handed back).  ms_out holds 8 doubles.  Advances the state by up to 3 reps + 1 slots. */
 int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out);
 int midagma_step_finish(midagma_solver* s);
 int midagma_poll(midagma_solver* s, midagma_result* res); /* synchronizes */

@@ -1,0 +1,370 @@
+// Two-level blocked Gauss-Jordan inverse of sI - W∘W (transposed), the cov-mode slot's
+// replacement for `sla.inv(s*I - W*W)` (linear.py:226, 240) when d > 192.
+//
+// Outer block Gauss-Jordan over B2-wide pivot blocks (B2 = 256, or 128 when 256 does not
+// divide D).  Outer step g sweeps pivot block G = [g B2, (g+1) B2):
+//     P = S^-1 with S = A_GG (the Schur complement left by the steps before g)
+//     A_Gj <- P A_Gj     A_iG <- -A_iG P     A_ij <- A_ij - A_iG (P A_Gj)     A_GG <- P
+// -- the sweep gj.hip applies at 32 granularity; after every block is swept A holds A^-1.
+// Each outer step reads one D x D buffer and writes the other (ping-pong), so the panel and
+// trailing kernels never read what a workgroup of the same launch writes.
+//
+// S^-1 has two sources:
+//   fast (this file)  S^-1 = X0 (I + R)(I + R^2)(I + R^4)...,  X0 = this block's P one slot
+//         earlier (W moves by ~lr per Adam step), R = I - S X0.  One residual launch and up
+//         to NM_PASSES pass launches of B2^3 products spread over (B2/16)^2 workgroups
+//         with K split over the 4 waves -- no serial chain of 32 x 32 inversions.  Pass p
+//         holds Y = X0 (I + R)...(I + R^(2^(p-1))) and Q = R^(2^p), the exact residual of
+//         Y (Y S = I - Q); once rho = ||Q||_inf (max row sum of |Q|) is <= 1e-8 the last
+//         factor Y (I + Q) lands at residual <= 1e-16 and the pass writes P instead.
+//   slow  (gj.hip)    the 32-block Gauss-Jordan run in place on the B2 x B2 block: pivots
+//         for the log-det on checkpoint slots, and every slot the fast path cannot take
+//         (first slot of a minimize call, rho > 0.25, no convergence): the fast kernels
+//         then set ST_NEED_GJ and the host re-runs the slot on the slow path.
+#include "launch.h"
+#include "tile32.h"
+
+namespace midagma {
+
+namespace {
+
+
+__device__ __forceinline__ int xcd_spread(int w, int nwg) {
+  // consecutive jobs (which share operand panels) onto one XCD: blocks b, b+8 share an XCD
+  const int q = nwg / 8, r = nwg % 8, x = w % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
+}
+
+// This wave's quarter of K for a 16 x 16 output tile (m0, n0) of op = A B:
+//   lane (r, kq) runs k = kb + kq L + q, q < L, kb = w * 4L  (L = K / 16)
+// so each lane streams L contiguous values of its A row.  Two chains (q even / odd).
+template <int L>
+__device__ __forceinline__ void splitk_partial(const double* __restrict__ A, int64_t lda,
+                                               const double* __restrict__ B, int64_t ldb, int m0, int n0,
+                                               dbl4& acc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, kq = lane >> 4;
+  const int kb = w * 4 * L + kq * L;
+  const double* a = A + (int64_t)(m0 + r) * lda + kb;
+  const double* b = B + (int64_t)kb * ldb + n0 + r;
+  dbl4 c1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < L; q += 2) {
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[(int64_t)q * ldb], acc, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q + 1], b[(int64_t)(q + 1) * ldb], c1, 0, 0, 0);
+  }
+  acc = acc + c1;
+}
+
+// Sum the 4 waves' partials of one 16 x 16 tile in a fixed order: thread e of the workgroup
+// returns element e (t = e >> 6 register, lane e & 63 of the accumulator layout).
+__device__ __forceinline__ double splitk_sum(const dbl4& part, double* red) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) red[w * 256 + t * 64 + lane] = part[t];
+  __syncthreads();
+  return ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
+}
+
+__device__ __forceinline__ void tile_elem(int e, int& row, int& col) {
+  const int t = e >> 6, lane = e & 63;
+  row = acc_row(lane, t);
+  col = acc_col(lane);
+}
+
+// max over the workgroup of one non-negative float per thread -> red4 (4 floats), all threads
+__device__ __forceinline__ float block_max(float v, float* red4) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
+}
+
+__device__ __forceinline__ double abs_or_inf(double v) { return isfinite(v) ? fabs(v) : INFINITY; }
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_add(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return v + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Row sums of |Q| for the ||.||_inf bound: thread e holds tile element (row, col); the 16
+// threads of a row are one DPP row of a wave.  The row's partial over this tile's 16
+// columns goes to rowpart[(m0 + row) * NT + tile column].
+__device__ __forceinline__ void store_row_partial(double a, double* __restrict__ rowpart, int m0, int n0, int NT) {
+  a = dpp_add<0xB1>(a);   // quad_perm [1,0,3,2]
+  a = dpp_add<0x4E>(a);   // quad_perm [2,3,0,1]
+  a = dpp_add<0x141>(a);  // row_half_mirror
+  a = dpp_add<0x140>(a);  // row_mirror
+  int row, col;
+  tile_elem(threadIdx.x, row, col);
+  if (col == 0) rowpart[(int64_t)(m0 + row) * NT + n0 / 16] = a;
+}
+
+// ||Q||_inf = max over rows of the summed row partials (B2 <= NTHREADS rows, one per thread)
+template <int B2>
+__device__ __forceinline__ double inf_norm(const double* __restrict__ rowpart, float* red4) {
+  constexpr int NT = B2 / 16;
+  double r = 0.0;
+  if ((int)threadIdx.x < B2) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) r += rowpart[(int64_t)threadIdx.x * NT + t];
+  }
+  // non-finite propagates as inf/nan; widen by 1e-6 against the float max below
+  const float f = isfinite(r) ? (float)(r * (1.0 + 1e-6)) : INFINITY;
+  return (double)block_max(f, red4);
+}
+
+// R = I - S X0 (tile (m0, n0) of the B2 x B2 block), row partials of |R| -> part0
+template <int L>
+__global__ __launch_bounds__(NTHREADS) void nm_resid_kernel(const double* __restrict__ S, int64_t lds,
+                                                            const double* __restrict__ X0, double* __restrict__ Q0,
+                                                            double* __restrict__ part0, int* __restrict__ done,
+                                                            State* __restrict__ st) {
+  if (st->status != ST_RUNNING) return;
+  if (st->ckpt_pending) {  // a log-det is due: pivots come from the slow path only
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
+    return;
+  }
+  constexpr int B2 = 16 * L;
+  __shared__ double red[4 * 256];
+  const int nt = B2 / 16, wg = blockIdx.x;
+  const int m0 = (wg / nt) * 16, n0 = (wg % nt) * 16;
+  if (wg == 0 && threadIdx.x == 0) *done = 0;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  splitk_partial<L>(S, lds, X0, B2, m0, n0, acc);
+  const double sum = splitk_sum(acc, red);
+  int row, col;
+  tile_elem(threadIdx.x, row, col);
+  const int gi = m0 + row, gj = n0 + col;
+  const double r = (gi == gj ? 1.0 : 0.0) - sum;
+  st_wt(Q0 + (int64_t)gi * B2 + gj, r);
+  store_row_partial(abs_or_inf(r), part0, m0, n0, nt);
+}
+
+// Pass p: rho = ||Q||_inf from the previous launch's row partials; converged -> P = Y + Y Q
+// (done = 1), else Y' = Y + Y Q, Q' = Q Q and the row partials of |Q'|.  Far or diverging
+// -> ST_NEED_GJ.
+template <int L>
+__global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restrict__ Y,
+                                                           const double* __restrict__ Q, double* __restrict__ Yn,
+                                                           double* __restrict__ Qn, double* __restrict__ P,
+                                                           const double* __restrict__ part_prev,
+                                                           double* __restrict__ part_next, int* __restrict__ done,
+                                                           State* __restrict__ st) {
+  if (st->status != ST_RUNNING) return;
+  if (*done) return;
+  constexpr int B2 = 16 * L;
+  __shared__ double red[4 * 256];
+  __shared__ float red4[4];
+  const int nt = B2 / 16, wg = blockIdx.x, tid = threadIdx.x;
+  const int m0 = (wg / nt) * 16, n0 = (wg % nt) * 16;
+  const double rho = inf_norm<B2>(part_prev, red4);
+  if (!(rho <= 0.25)) {  // warm start too far, diverging, or not finite
+    if (wg == 0 && tid == 0) st->status = ST_NEED_GJ;
+    return;
+  }
+  int row, col;
+  tile_elem(tid, row, col);
+  const int gi = m0 + row, gj = n0 + col;
+  const double yold = Y[(int64_t)gi * B2 + gj];
+  dbl4 ay = {0.0, 0.0, 0.0, 0.0};
+  if (rho <= 1e-8) {  // last factor: P = Y (I + Q)
+    splitk_partial<L>(Y, B2, Q, B2, m0, n0, ay);
+    const double yq = splitk_sum(ay, red);
+    st_wt(P + (int64_t)gi * B2 + gj, yold + yq);
+    if (wg == 0 && tid == 0) __hip_atomic_store(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  dbl4 aq = {0.0, 0.0, 0.0, 0.0};
+  splitk_partial<L>(Y, B2, Q, B2, m0, n0, ay);
+  splitk_partial<L>(Q, B2, Q, B2, m0, n0, aq);
+  const double yq = splitk_sum(ay, red);
+  __syncthreads();  // red reused
+  const double qq = splitk_sum(aq, red);
+  st_wt(Yn + (int64_t)gi * B2 + gj, yold + yq);
+  st_wt(Qn + (int64_t)gi * B2 + gj, qq);
+  store_row_partial(abs_or_inf(qq), part_next, m0, n0, nt);
+}
+
+// acc += A[0:32, 0:K] B[0:K, 0:32] (global operands), 32-deep chunks through double-
+// buffered LDS images with a register prefetch of the next chunk; one barrier per chunk.
+__device__ __forceinline__ void tile32_gemm(const double* __restrict__ A, int64_t lda,
+                                            const double* __restrict__ B, int64_t ldb, int K, dbl4& acc,
+                                            double* As0, double* As1, double* Bs0, double* Bs1) {
+  const int tid = threadIdx.x;
+  const int r0 = tid >> 4, c0 = (tid & 15) * 2;  // items tid and tid + 256: rows r0, r0 + 16
+  double2 a0, a1, b0, b1;
+#define T32_LOAD(kc)                                                                       \
+  do {                                                                                     \
+    const double* ap = A + (int64_t)r0 * lda + (kc) * 32 + c0;                             \
+    const double* bp = B + ((int64_t)(kc) * 32 + r0) * ldb + c0;                           \
+    a0 = *reinterpret_cast<const double2*>(ap);                                            \
+    a1 = *reinterpret_cast<const double2*>(ap + 16 * lda);                                 \
+    b0 = *reinterpret_cast<const double2*>(bp);                                            \
+    b1 = *reinterpret_cast<const double2*>(bp + 16 * ldb);                                 \
+  } while (0)
+  T32_LOAD(0);
+  const int nk = K / 32;
+  for (int kc = 0; kc < nk; ++kc) {
+    double* As = (kc & 1) ? As1 : As0;
+    double* Bs = (kc & 1) ? Bs1 : Bs0;
+    *reinterpret_cast<double2*>(As + r0 * ST + c0) = a0;
+    *reinterpret_cast<double2*>(As + (r0 + 16) * ST + c0) = a1;
+    *reinterpret_cast<double2*>(Bs + r0 * ST + c0) = b0;
+    *reinterpret_cast<double2*>(Bs + (r0 + 16) * ST + c0) = b1;
+    __syncthreads();
+    if (kc + 1 < nk) T32_LOAD(kc + 1);
+    mma32(As, Bs, acc);
+  }
+#undef T32_LOAD
+}
+
+// Panels of outer step g (one 32 x 32 tile per workgroup):
+//   U  Aout[G, j] = P Ain[G, j]         (j outside G)
+//   V  Aout[i, G] = -Ain[i, G] P        (i outside G)
+//   P  Aout[G, G] = P, Pst = P          (next slot's warm start)
+// With `done` (fast path) an unconverged block hands the slot to the host (ST_NEED_GJ).
+__global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __restrict__ Ain,
+                                                              double* __restrict__ Aout, int64_t D, int B2, int g,
+                                                              const double* __restrict__ P, int64_t ldp,
+                                                              double* __restrict__ Pst,
+                                                              const int* __restrict__ done,
+                                                              State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  if (done && *done == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
+  const int nb = (int)(D / NB), gb = B2 / NB, g0 = g * gb, mb = nb - gb;
+  const int nu = gb * mb;
+  const int job = xcd_spread(blockIdx.x, gridDim.x);
+  const int64_t G0 = (int64_t)g0 * NB;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  if (job < nu) {
+    const int a = job / mb, cq = job % mb, c = cq < g0 ? cq : cq + gb;
+    tile32_gemm(P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, img[0], img[1],
+                img[2], img[3]);
+    double* out = Aout + (G0 + (int64_t)a * NB) * D + (int64_t)c * NB;
+    acc_foreach(acc, [&](int row, int col, double& v) { st_wt(out + (int64_t)row * D + col, v); });
+  } else if (job < 2 * nu) {
+    const int j2 = job - nu, iq = j2 / gb, c = j2 % gb, i = iq < g0 ? iq : iq + gb;
+    tile32_gemm(Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, img[0], img[1], img[2],
+                img[3]);
+    double* out = Aout + (int64_t)i * NB * D + G0 + (int64_t)c * NB;
+    acc_foreach(acc, [&](int row, int col, double& v) { st_wt(out + (int64_t)row * D + col, -v); });
+  } else {
+    const int j3 = job - 2 * nu, a = j3 / gb, c = j3 % gb;
+    const double* src = P + (int64_t)a * NB * ldp + (int64_t)c * NB;
+    double* out = Aout + (G0 + (int64_t)a * NB) * D + G0 + (int64_t)c * NB;
+    double* ps = Pst + (int64_t)a * NB * B2 + (int64_t)c * NB;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int e = it * NTHREADS + threadIdx.x, row = e >> 5, col = e & 31;
+      const double v = src[(int64_t)row * ldp + col];
+      st_wt(out + (int64_t)row * D + col, v);
+      st_wt(ps + (int64_t)row * B2 + col, v);
+    }
+  }
+}
+
+// Trailing update of outer step g: Aout[i, j] = Ain[i, j] - Ain[i, G] Aout[G, j] for i, j
+// outside G (Aout[G, j] = P Ain[G, j] from the panel launch).
+__global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __restrict__ Ain,
+                                                              double* __restrict__ Aout, int64_t D, int B2, int g,
+                                                              const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
+  const int nb = (int)(D / NB), gb = B2 / NB, g0 = g * gb, mb = nb - gb;
+  const int job = xcd_spread(blockIdx.x, gridDim.x);
+  const int iq = job / mb, jq = job % mb;
+  const int i = iq < g0 ? iq : iq + gb, j = jq < g0 ? jq : jq + gb;
+  const int64_t G0 = (int64_t)g0 * NB;
+  const double* Ci = Ain + (int64_t)i * NB * D + (int64_t)j * NB;
+  dbl4 c_old;
+  acc_foreach(c_old, [&](int row, int col, double& v) { v = Ci[(int64_t)row * D + col]; });
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  tile32_gemm(Ain + (int64_t)i * NB * D + G0, D, Aout + G0 * D + (int64_t)j * NB, D, B2, acc, img[0], img[1],
+              img[2], img[3]);
+  double* out = Aout + (int64_t)i * NB * D + (int64_t)j * NB;
+  const int lane = threadIdx.x & 63, m0 = q_m0(), n0 = q_n0();
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int row = m0 + acc_row(lane, t), col = n0 + acc_col(lane);
+    st_wt(out + (int64_t)row * D + col, c_old[t] - acc[t]);
+  }
+}
+
+}  // namespace
+
+int binv_block(int64_t D) {
+  if (D < 256 || D % 128 != 0) return 0;  // fast path not available: plain GJ
+  return D % 256 == 0 ? 256 : 128;
+}
+
+double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw) {
+  const int B2 = binv_block(D);
+  if (B2 == 0) return Mt;
+  return ((D / B2) & 1) ? bw.Aalt : Mt;  // K2 ping-pong flips land the inverse in Mt
+}
+
+template <int L>
+static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& bw, int g, State* st,
+                           hipStream_t stream) {
+  constexpr int B2 = 16 * L;
+  const int nwg = (B2 / 16) * (B2 / 16);
+  double* Pst = bw.Pst + (int64_t)g * B2 * B2;
+  int* done = bw.done + g;
+  double* part = bw.part + (int64_t)g * (NM_PASSES + 1) * PART_STRIDE;  // per block: kept for diagnostics
+  hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Ain + G0 * D + G0, D, Pst,
+                     bw.Q[0], part, done, st);
+  for (int p = 1; p <= NM_PASSES; ++p) {
+    const double* Y = p == 1 ? Pst : bw.Y[(p - 1) & 1];
+    hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Y, bw.Q[(p - 1) & 1],
+                       bw.Y[p & 1], bw.Q[p & 1], bw.P, part + (p - 1) * PART_STRIDE, part + p * PART_STRIDE,
+                       done, st);
+  }
+}
+
+void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
+                            hipStream_t stream) {
+  const int B2 = binv_block(D);
+  if (B2 == 0) throw std::invalid_argument("blocked inverse needs D >= 256, D % 128 == 0");
+  const int K2 = (int)(D / B2), gb = B2 / NB, mb = (int)(D / NB) - gb;
+  double* bufs[2] = {binv_build_target(Mt, D, bw), nullptr};
+  bufs[1] = bufs[0] == Mt ? bw.Aalt : Mt;
+  for (int g = 0; g < K2; ++g) {
+    double* Ain = bufs[g & 1];
+    double* Aout = bufs[(g + 1) & 1];
+    const int64_t G0 = (int64_t)g * B2;
+    double* Pst = bw.Pst + (int64_t)g * B2 * B2;
+    const double* P;
+    int64_t ldp;
+    const int* done = nullptr;
+    if (fast) {
+      if (B2 == 256)
+        launch_neumann<16>(Ain, D, G0, bw, g, st, stream);
+      else
+        launch_neumann<8>(Ain, D, G0, bw, g, st, stream);
+      P = bw.P;
+      ldp = B2;
+      done = bw.done + g;
+    } else {
+      GJWork w = gw;
+      w.pivlog = gw.pivlog ? gw.pivlog + G0 : nullptr;
+      w.Pstore = gw.Pstore ? gw.Pstore + G0 * NB : nullptr;
+      launch_gj_inverse(Ain + G0 * D + G0, D, B2, w, st, stream);
+      P = Ain + G0 * D + G0;
+      ldp = D;
+    }
+    hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2,
+                       g, P, ldp, Pst, done, st);
+    if (mb > 0)
+      hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2, g, st);
+  }
+  HIP_TRY(hipGetLastError());
+}
+
+}  // namespace midagma

@@ -30,6 +30,8 @@ enum Status : int32_t {
   ST_FAILED = 2,        // left the M-matrix domain at iter 1 or s <= 0.9 -> (W, False)
   ST_LR_UNDERFLOW = 3,  // lr halved below 1e-16                         -> (W, True)
   ST_SINGULAR = 4,      // non-finite inverse                            -> LinAlgError
+  ST_NEED_GJ = 5,       // internal: the fast inverse could not run this slot (no usable warm
+                        // start, or a log-det is due); the host re-runs it on the GJ path
 };
 
 enum Action : int32_t { ACT_NOOP = 0, ACT_STEP = 1, ACT_HALVE = 2, ACT_REVERT = 3 };

@@ -18,11 +18,10 @@
 // (unpivoted GJ in registers + LDS, pivots -> log|p|), so the only serial
 // chain per step is one 32x32 inversion plus one kernel boundary.
 #include "launch.h"
-#include "mfma64.h"
+#include "tile32.h"
 
 namespace midagma {
 
-constexpr int NB = 32;        // block size of the elimination
 
 #ifdef MIDAGMA_STAMPS
 // Diagnostic build only: s_memtime stamps of the diagonal-owner workgroup per block step.
@@ -40,11 +39,6 @@ __device__ unsigned long long g_stamps[256][16];
   do {                 \
   } while (0)
 #endif
-// Every 32 x 32 LDS image has row stride ST = 34 (= 2 mod 32 doubles): conflict-free as
-// an MFMA A operand ([m][k], lanes walk rows) and 2-way on one ds_read_b64 lane group as
-// a B operand ([k][n], lanes walk columns) -- one image then serves both roles, which the
-// Newton-Schulz iteration needs (X is the B operand of S X and the A operand of X R).
-constexpr int ST = 34;
 constexpr int EPT = NB * NB / NTHREADS;   // elements per thread in the tile inversion (4)
 constexpr int TPR = NB / EPT;             // threads per tile row (8)
 
@@ -82,108 +76,6 @@ __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __rest
     const int e = it * NTHREADS + tid;
     const int r = e >> 6, c = e & 63;  // r: row of At tile (= source col)
     At[((int64_t)bj * 64 + r) * D + (int64_t)bi * 64 + c] = tile[r][c];
-  }
-}
-
-// ---- 32 x 32 tile helpers --------------------------------------------------------
-// Wave w owns the 16 x 16 quadrant (wm, wn) = (w >> 1, w & 1) of a 32 x 32 output.
-__device__ __forceinline__ int q_m0() { return (threadIdx.x >> 7) * 16; }
-__device__ __forceinline__ int q_n0() { return ((threadIdx.x >> 6) & 1) * 16; }
-
-// acc += Ls * Rs, both 32 x 32 LDS images (row stride ST).  Four independent MFMA
-// chains (k mod 16) summed at the end: a dependent chain leaves the SIMD's matrix pipe
-// idle between its MFMAs, and co-resident workgroups' MFMAs take those slots -- with
-// independent chains a high-priority wave (the diagonal owner) keeps the pipe.
-__device__ __forceinline__ void mma32(const double* __restrict__ Ls, const double* __restrict__ Rs, dbl4& acc) {
-  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
-  const double* La = Ls + (q_m0() + r) * ST + kq;
-  const double* Rb = Rs + kq * ST + q_n0() + r;
-  const dbl4 z = {0.0, 0.0, 0.0, 0.0};
-  dbl4 c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[0], Rb[0], acc, 0, 0, 0);
-  dbl4 c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[4], Rb[4 * ST], z, 0, 0, 0);
-  dbl4 c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[8], Rb[8 * ST], z, 0, 0, 0);
-  dbl4 c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[12], Rb[12 * ST], z, 0, 0, 0);
-  c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[16], Rb[16 * ST], c0, 0, 0, 0);
-  c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[20], Rb[20 * ST], c1, 0, 0, 0);
-  c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[24], Rb[24 * ST], c2, 0, 0, 0);
-  c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[28], Rb[28 * ST], c3, 0, 0, 0);
-  acc = (c0 + c1) + (c2 + c3);
-}
-
-template <class F>
-__device__ __forceinline__ void acc_foreach(dbl4& acc, F&& f) {
-  const int lane = threadIdx.x & 63;
-  const int m0 = q_m0(), n0 = q_n0();
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    double v = acc[t];
-    f(m0 + acc_row(lane, t), n0 + acc_col(lane), v);
-    acc[t] = v;
-  }
-}
-
-// 32 x 32 global tile (leading dim ld) -> LDS image (stride ST), scaled by `sc`
-__device__ __forceinline__ void tile32_to_lds(double* __restrict__ dst, const double* __restrict__ src, int64_t ld,
-                                              double sc) {
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int item = it * NTHREADS + threadIdx.x;  // 512 double2 items
-    const int row = item >> 4, c = (item & 15) * 2;
-    double2 v = *reinterpret_cast<const double2*>(src + row * ld + c);
-    v.x *= sc;
-    v.y *= sc;
-    *reinterpret_cast<double2*>(dst + row * ST + c) = v;
-  }
-}
-
-__device__ __forceinline__ void tile32_copy(double* __restrict__ dst, int64_t ldd, const double* __restrict__ src,
-                                            int64_t lds) {
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int item = it * NTHREADS + threadIdx.x;
-    const int row = item >> 4, c = (item & 15) * 2;
-    *reinterpret_cast<double2*>(dst + row * ldd + c) = *reinterpret_cast<const double2*>(src + row * lds + c);
-  }
-}
-
-// Store for data the NEXT launch reads: write-through (sc1), so the tile does not sit
-// dirty in this XCD's L2 and the kernel boundary has nothing of it to write back
-// (MI355X_MICROARCH.md price list: a boundary pays dirty bytes / ~6 TB/s).
-__device__ __forceinline__ void st_wt(double* p, double v) {
-#ifdef MIDAGMA_GJ_PLAIN_STORES
-  *p = v;
-#else
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
-
-// max over the 64 lanes of a wave of a non-negative float: DPP within each row of 16
-// (quad swaps, half-row and row mirrors: single v_max_f32_dpp ops), then the four row
-// results by readlane.  No LDS round trip.
-template <int CTRL>
-__device__ __forceinline__ float dpp_max(float v) {
-  return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false)));
-}
-__device__ __forceinline__ float wave_max(float v) {
-  v = dpp_max<0xB1>(v);   // quad_perm [1,0,3,2]
-  v = dpp_max<0x4E>(v);   // quad_perm [2,3,0,1]
-  v = dpp_max<0x141>(v);  // row_half_mirror
-  v = dpp_max<0x140>(v);  // row_mirror
-  const int b = __float_as_int(v);
-  return fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(b, 0)), __int_as_float(__builtin_amdgcn_readlane(b, 16))),
-               fmaxf(__int_as_float(__builtin_amdgcn_readlane(b, 32)), __int_as_float(__builtin_amdgcn_readlane(b, 48))));
-}
-
-// Two independent 32 x 32 products in one pass (their MFMA chains interleave):
-//   c1 += A1 * B1,  c2 += A2 * B2   (LDS images, stride ST)
-__device__ __forceinline__ void mma32x2(const double* __restrict__ A1, const double* __restrict__ B1, dbl4& c1,
-                                        const double* __restrict__ A2, const double* __restrict__ B2, dbl4& c2) {
-  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
-  const int ao = (q_m0() + r) * ST + kq, bo = kq * ST + q_n0() + r;
-#pragma unroll
-  for (int k0 = 0; k0 < NB; k0 += 4) {
-    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(A1[ao + k0], B1[bo + k0 * ST], c1, 0, 0, 0);
-    c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(A2[ao + k0], B2[bo + k0 * ST], c2, 0, 0, 0);
   }
 }
 
@@ -341,7 +233,7 @@ __device__ __forceinline__ bool want_gauss_jordan(const double* Pstore, const St
 }
 
 // Prologue: publish step 0's panels and invert A_00.
-__global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __restrict__ A, int64_t D,
+__global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __restrict__ A, int64_t lda, int64_t D,
                                                                double* __restrict__ Cside,
                                                                double* __restrict__ Rside,
                                                                double* __restrict__ Pside,
@@ -352,12 +244,12 @@ __global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __r
   __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
   __shared__ double scratch[4 * NB];
   const int t = blockIdx.x;
-  tile32_copy(Cside + (int64_t)t * NB * NB, NB, A + (int64_t)t * NB * D, D);  // column 0
-  tile32_copy(Rside + (int64_t)t * NB, D, A + (int64_t)t * NB, D);            // row 0
+  tile32_copy(Cside + (int64_t)t * NB * NB, NB, A + (int64_t)t * NB * lda, lda);  // column 0
+  tile32_copy(Rside + (int64_t)t * NB, D, A + (int64_t)t * NB, lda);              // row 0
   if (t != 0) return;
   const bool want_gj = want_gauss_jordan(Pstore, st);
   dbl4 acc, x0 = {0.0, 0.0, 0.0, 0.0};
-  acc_foreach(acc, [&](int row, int col, double& v) { v = A[(int64_t)row * D + col]; });
+  acc_foreach(acc, [&](int row, int col, double& v) { v = A[(int64_t)row * lda + col]; });
   if (!want_gj) acc_foreach(x0, [&](int row, int col, double& v) { v = Pstore[row * NB + col]; });
   invert_diag_tile(acc, x0, Pside, Pstore, pivlog, want_gj, img[0], img[1], img[2], img[3], scratch);
 }
@@ -368,7 +260,7 @@ __global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __r
 //   global-load latency before its MFMA chain.  The workgroup owning tile (k+1, k+1)
 //   carries the step's serial chain: it takes linear block id 0 (dispatched first),
 //   prefetches its warm start with the operands, inverts before any global store.
-__global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ A, int64_t D, int k,
+__global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ A, int64_t lda, int64_t D, int k,
                                                            double* __restrict__ Cside0, double* __restrict__ Cside1,
                                                            double* __restrict__ Rside0, double* __restrict__ Rside1,
                                                            double* __restrict__ Pside0, double* __restrict__ Pside1,
@@ -393,7 +285,7 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
   double* Cn = odd ? Cside0 : Cside1;
   double* Rn = odd ? Rside0 : Rside1;
   double* Pn = odd ? Pside0 : Pside1;
-  double* Aij = A + (int64_t)bi * NB * D + (int64_t)bj * NB;
+  double* Aij = A + (int64_t)bi * NB * lda + (int64_t)bj * NB;
   const bool owner = k1 < K && bi == k1 && bj == k1;
   if (owner) {
     __builtin_amdgcn_s_setprio(3);  // its waves win issue arbitration against co-resident tiles
@@ -428,7 +320,7 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
     tile32_to_lds(R0, Rs + (int64_t)bj * NB, D, 1.0);
     tile32_to_lds(L1, Cs + (int64_t)bi * NB * NB, NB, -1.0);
     dbl4 a_old;
-    acc_foreach(a_old, [&](int row, int col, double& v) { v = Aij[(int64_t)row * D + col]; });
+    acc_foreach(a_old, [&](int row, int col, double& v) { v = Aij[(int64_t)row * lda + col]; });
     __syncthreads();
     if (owner) STAMP(k, 1);
     dbl4 tq = {0.0, 0.0, 0.0, 0.0};
@@ -449,7 +341,7 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
       STAMP(k, 4);
     }
   }
-  acc_foreach(acc, [&](int row, int col, double& v) { st_wt(Aij + (int64_t)row * D + col, v); });
+  acc_foreach(acc, [&](int row, int col, double& v) { st_wt(Aij + (int64_t)row * lda + col, v); });
   if (k1 >= K) return;
   if (bj == k1) acc_foreach(acc, [&](int row, int col, double& v) { st_wt(Cn + ((int64_t)bi * NB + row) * NB + col, v); });
   if (bi == k1) acc_foreach(acc, [&](int row, int col, double& v) { st_wt(Rn + (int64_t)row * D + (int64_t)bj * NB + col, v); });
@@ -474,7 +366,7 @@ void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int6
   HIP_TRY(hipGetLastError());
 }
 
-void launch_gj_inverse(double* A, int64_t D, const GJWork& w, const State* st, hipStream_t stream) {
+void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream) {
   const int K = (int)(D / NB);
   double* C0 = w.C;
   double* C1 = w.C + D * NB;
@@ -482,10 +374,10 @@ void launch_gj_inverse(double* A, int64_t D, const GJWork& w, const State* st, h
   double* R1 = w.R + NB * D;
   double* P0 = w.P;
   double* P1 = w.P + NB * NB;
-  hipLaunchKernelGGL(gj_prologue_kernel, dim3(K), dim3(NTHREADS), 0, stream, A, D, C0, R0, P0, w.pivlog, w.Pstore,
+  hipLaunchKernelGGL(gj_prologue_kernel, dim3(K), dim3(NTHREADS), 0, stream, A, lda, D, C0, R0, P0, w.pivlog, w.Pstore,
                      st);
   for (int k = 0; k < K; ++k)
-    hipLaunchKernelGGL(gj_step_kernel, dim3(K, K), dim3(NTHREADS), 0, stream, A, D, k, C0, C1, R0, R1, P0, P1,
+    hipLaunchKernelGGL(gj_step_kernel, dim3(K, K), dim3(NTHREADS), 0, stream, A, lda, D, k, C0, C1, R0, R1, P0, P1,
                        w.pivlog, w.Pstore, st);
   HIP_TRY(hipGetLastError());
 }

@@ -31,8 +31,31 @@ void gj_setup_attributes();
 // s is read from pr->s when pr != nullptr (graph-replayed slots), else the argument.
 void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int64_t D, int64_t d, double s,
                      const Params* pr, const State* st, hipStream_t stream);
-// In place: A <- inv(A) (unpivoted blocked Gauss-Jordan), pivot logs into w.pivlog.
-void launch_gj_inverse(double* A, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
+// In place: A <- inv(A) (unpivoted blocked Gauss-Jordan) on the D x D matrix at A with
+// leading dimension lda (D multiple of 32), pivot logs into w.pivlog.
+void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
+
+// --- blockinv.hip -----------------------------------------------------------
+constexpr int NM_PASSES = 4;        // product-form passes per outer block in the fast graph
+constexpr int PART_STRIDE = 4096;   // doubles per pass: row partials of |Q| (B2 x B2/16)
+struct BInvWork {
+  double* Aalt;    // second D x D buffer (outer steps ping-pong)
+  double* Pst;     // D x B2: warm start (last inverse) of every outer diagonal block
+  double* Y[2];    // B2 x B2 product-form iterates
+  double* Q[2];
+  double* P;       // B2 x B2 converged inverse of the current block
+  double* part;    // (D / B2) x (NM_PASSES + 1) x PART_STRIDE row partials
+  int* done;       // D / B2 convergence words
+};
+// Outer block width of the two-level inverse (0: not available, use launch_gj_inverse).
+int binv_block(int64_t D);
+// The buffer launch_build_at must fill so that the inverse ends in Mt.
+double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
+// Mt <- inv(A) for A in binv_build_target(Mt): two-level blocked Gauss-Jordan, diagonal
+// blocks by the warm-started product form (fast; sets ST_NEED_GJ when it cannot) or by the
+// 32-block Gauss-Jordan with pivots (slow).
+void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
+                            hipStream_t stream);
 
 // --- gemm.hip ---------------------------------------------------------------
 enum GemmB : int { B_PLAIN = 0, B_IMINUS = 1 };

@@ -49,6 +49,10 @@ struct midagma_solver {
   std::string err;
 
   DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
+  // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
+  int B2 = 0;
+  DevBuf Malt, Pst2, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone;
+  bool fast_ready = false;  // Pst2 holds the previous slot's outer-block inverses
   double* zbuf = nullptr;  // d x d (+64 tail) score partial; internal or bound
   int64_t zbuf_cap = 0;
   // data mode
@@ -74,13 +78,14 @@ struct midagma_solver {
   double mu = 1.0;
   Params hp{};
 
-  hipGraphExec_t g_part1 = nullptr, g_part2 = nullptr, g_full = nullptr;
+  hipGraphExec_t g_part1 = nullptr, g_part2 = nullptr, g_full = nullptr, g_fast = nullptr;
   bool graphs_valid = false;
 
   ~midagma_solver() {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
-                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore})
+                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2,
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone})
       b->release();
     if (d_params) (void)hipFree(d_params);
     if (d_state) (void)hipFree(d_state);
@@ -92,7 +97,7 @@ struct midagma_solver {
   }
 
   void destroy_graphs() {
-    for (hipGraphExec_t* ge : {&g_part1, &g_part2, &g_full})
+    for (hipGraphExec_t* ge : {&g_part1, &g_part2, &g_full, &g_fast})
       if (*ge) {
         (void)hipGraphExecDestroy(*ge);
         *ge = nullptr;
@@ -101,11 +106,30 @@ struct midagma_solver {
   }
 
   GJWork gj() { return GJWork{P.p, R.p, C.p, pivlog.p, Pstore.p}; }
+  BInvWork binv() {
+    return BInvWork{Malt.p,
+                    Pst2.p,
+                    {nmY0.p, nmY1.p},
+                    {nmQ0.p, nmQ1.p},
+                    nmP.p,
+                    nmPart.p,
+                    reinterpret_cast<int*>(nmDone.p)};
+  }
+  bool blocked() const { return B2 > 0; }
 
   // ---- the slot -----------------------------------------------------------
-  void enqueue_part1() {
-    launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, 0.0, d_params, d_state, stream);
-    launch_gj_inverse(Mt.p, D, gj(), d_state, stream);
+  // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
+  void enqueue_part1(bool fast = false) {
+    if (blocked()) {
+      launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
+                      stream);
+      launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream);
+    } else {
+      launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, 0.0, d_params, d_state, stream);
+      launch_gj_inverse(Mt.p, D, D, gj(), d_state, stream);
+    }
+    // (a fork/join of the score GEMMs onto a second stream inside the graph measured slower:
+    // the cross-queue dependencies cost more than the overlap gains)
     if (mode == MIDAGMA_MODE_COV) {
       // rhs = ((-mu) cov) @ (I - W)    (linear.py:244)
       enqueue_cov_gemm(covs.p, W.p, zbuf, d_state);
@@ -155,7 +179,7 @@ struct midagma_solver {
     hipGraph_t graph = nullptr;
     HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
-      if (which & 1) enqueue_part1();
+      if (which & 1) enqueue_part1((which & 4) != 0);
       if (which & 2) enqueue_part2();
     } catch (...) {
       (void)hipStreamEndCapture(stream, &graph);
@@ -175,6 +199,7 @@ struct midagma_solver {
     g_full = capture(3);
     g_part1 = capture(1);
     g_part2 = capture(2);
+    if (blocked()) g_fast = capture(3 | 4);
     graphs_valid = true;
   }
 
@@ -194,6 +219,14 @@ struct midagma_solver {
     if (D % 128 == 0 && (D / 128) * (D / 128) < 256) {
       cov_split = (int)std::min<int64_t>(4, D / 128);
       if (cov_split > 1) cov_parts.alloc((size_t)cov_split * DD);
+    }
+    if (mode == MIDAGMA_MODE_COV) B2 = binv_block(D);
+    if (blocked()) {
+      Malt.alloc(DD);
+      Pst2.alloc((size_t)D * B2);
+      for (DevBuf* b : {&nmY0, &nmY1, &nmQ0, &nmQ1, &nmP}) b->alloc((size_t)B2 * B2);
+      nmPart.alloc((size_t)(D / B2) * (NM_PASSES + 1) * PART_STRIDE);
+      nmDone.alloc(D / B2);
     }
     zown.alloc(DD + 64);
     HIP_TRY(hipMemsetAsync(zown.p, 0, (DD + 64) * sizeof(double), stream));
@@ -296,6 +329,7 @@ struct midagma_solver {
     const size_t DD = (size_t)D * D;
     for (DevBuf* b : {&m, &v, &g}) HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
     HIP_TRY(hipStreamSynchronize(stream));  // h_state[0] reused as a snapshot slot below
+    fast_ready = false;  // the first slot of a call runs the GJ path (warm starts are stale)
     begun = true;
   }
 
@@ -306,7 +340,59 @@ struct midagma_solver {
 
   static bool terminal(const State& s) { return s.status != ST_RUNNING; }
 
+  // Cov mode with the blocked inverse: fast slots in batches, a GJ (slow) slot wherever a
+  // log-det is due (checkpoint), there is no warm start (first slot) or a fast slot handed
+  // back (ST_NEED_GJ).  Batches stop at the next checkpoint iteration, so the host knows
+  // when the slow slot is due; one host sync per batch.  n_slots < 0: until terminal.
+  void drive_blocked(int64_t n_slots) {
+    ensure_graphs();
+    const int64_t max_iter = hp.max_iter, checkpoint = std::max<int64_t>(hp.checkpoint, 1);
+    const int64_t cap = max_iter + max_iter / checkpoint + 512;
+    int64_t launched = 0, handbacks = 0;
+    int64_t bmax = fast_batch;  // fast batch cap: 1 after a hand-back, doubling up to 64
+    State cur = h_state[0];
+    HIP_TRY(hipMemcpyAsync(&cur, d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (;;) {
+      if (cur.status != ST_RUNNING && cur.status != ST_NEED_GJ) break;
+      if (n_slots >= 0 && launched >= n_slots) break;
+      if (n_slots < 0 && (cur.slots > cap || launched > 4 * cap))
+        throw std::runtime_error("minimize: slot budget exceeded (controller stuck)");
+      int64_t it_hi = cur.iter;
+      if (cur.status == ST_NEED_GJ || cur.ckpt_pending || !fast_ready) {
+        if (cur.status == ST_NEED_GJ) {
+          ++handbacks;
+          bmax = 1;
+          static const int32_t running = ST_RUNNING;
+          HIP_TRY(hipMemcpyAsync(&d_state->status, &running, sizeof(int32_t), hipMemcpyHostToDevice, stream));
+        }
+        HIP_TRY(hipGraphLaunch(g_full, stream));  // slow slot: pivots + fresh warm starts
+        ++launched;
+        ++it_hi;
+        fast_ready = true;
+      }
+      // fast slots up to the next checkpoint iteration (the slot after it must be slow)
+      const int64_t next_ck = std::min(max_iter, (it_hi / checkpoint + 1) * checkpoint);
+      int64_t B = std::min<int64_t>(bmax, next_ck - it_hi);
+      if (n_slots >= 0) B = std::min<int64_t>(B, n_slots - launched);
+      for (int64_t b = 0; b < B; ++b) HIP_TRY(hipGraphLaunch(g_fast, stream));
+      launched += std::max<int64_t>(B, 0);
+      HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      cur = h_state[1];
+      if (cur.status != ST_NEED_GJ) bmax = std::min<int64_t>(64, 2 * bmax);
+    }
+    handback_count += handbacks;
+    fast_batch = bmax;
+  }
+  int64_t handback_count = 0;
+  int64_t fast_batch = 64;
+
   void run_loop(int64_t max_iter, int64_t checkpoint) {
+    if (blocked()) {
+      drive_blocked(-1);
+      return;
+    }
     ensure_graphs();
     const int64_t cap = max_iter + max_iter / std::max<int64_t>(checkpoint, 1) + 512;
     int64_t launched = 0, known_iter = 0;
@@ -343,7 +429,7 @@ struct midagma_solver {
     res->halvings = s.halvings;
     res->slots = s.slots;
     res->n_checkpoints = s.n_ckpt;
-    res->status = s.status;
+    res->status = s.status == ST_NEED_GJ ? ST_RUNNING : s.status;  // internal hand-back, not an outcome
     res->early_stop = s.early_stop;
     res->lr_final = s.lr;
     res->obj_last = s.obj_last;
@@ -583,6 +669,10 @@ int midagma_begin(midagma_solver* s, const double* W, double mu, int64_t max_ite
 int midagma_run_slots(midagma_solver* s, int64_t n) {
   if (!s || !s->begun || n < 0) return fail(s, MIDAGMA_E_STATE, "run_slots: call begin first");
   return guarded(s, [&] {
+    if (s->blocked()) {
+      s->drive_blocked(n);
+      return MIDAGMA_OK;
+    }
     for (int64_t i = 0; i < n; ++i) HIP_TRY(hipGraphLaunch(s->g_full, s->stream));
     return MIDAGMA_OK;
   });
@@ -616,7 +706,7 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
     // data mode: [4] Y = X (I - W) GEMM   [5] Z = X^T Y GEMM (+ slice sum)
     ms_out[0] = timed([&] { launch_build_at(s->W.p, D, true, s->Mt.p, D, s->d, 0.0, s->d_params, s->d_state,
                                             s->stream); });
-    ms_out[1] = timed([&] { launch_gj_inverse(s->Mt.p, D, s->gj(), s->d_state, s->stream); });
+    ms_out[1] = timed([&] { launch_gj_inverse(s->Mt.p, D, D, s->gj(), s->d_state, s->stream); });
     if (s->mode == MIDAGMA_MODE_COV) {
       ms_out[2] = timed([&] { s->enqueue_cov_gemm(s->covs.p, s->W.p, s->zbuf, s->d_state); });
       ms_out[4] = ms_out[5] = 0.0;
@@ -642,6 +732,26 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
       });
     }
     ms_out[3] = timed([&] { HIP_TRY(hipGraphLaunch(s->g_full, s->stream)); });
+    ms_out[6] = ms_out[7] = 0.0;
+    if (s->blocked()) {
+      // [6] build + fast blocked inverse, less [0]   [7] whole fast slot (graph).  Both need a
+      // warm start and no pending checkpoint: one slow slot first.
+      HIP_TRY(hipGraphLaunch(s->g_full, s->stream));
+      ms_out[6] = timed([&] {
+        launch_build_at(s->W.p, D, true, binv_build_target(s->Mt.p, D, s->binv()), D, s->d, 0.0, s->d_params,
+                        s->d_state, s->stream);
+        launch_blocked_inverse(s->Mt.p, D, s->binv(), true, s->gj(), s->d_state, s->stream);
+      }) - ms_out[0];
+      ms_out[7] = timed([&] { HIP_TRY(hipGraphLaunch(s->g_fast, s->stream)); });
+      State st{};
+      HIP_TRY(hipMemcpy(&st, s->d_state, sizeof(State), hipMemcpyDeviceToHost));
+      if (st.status == ST_NEED_GJ) {  // the fast path did not run: report it, leave a clean state
+        ms_out[6] = ms_out[7] = -1.0;
+        static const int32_t running = ST_RUNNING;
+        HIP_TRY(hipMemcpy(&s->d_state->status, &running, sizeof(int32_t), hipMemcpyHostToDevice));
+        s->fast_ready = false;
+      }
+    }
     HIP_TRY(hipEventDestroy(a));
     HIP_TRY(hipEventDestroy(b));
     return MIDAGMA_OK;
@@ -685,6 +795,34 @@ int midagma_end(midagma_solver* s, double* W, midagma_result* res) {
   return rc;
 }
 
+// Diagnostics of the fast blocked inverse (not in the public header): per outer block g,
+// out[g*(NM_PASSES+2) + 0] = done word, out[... + 1 + p] = ||Q_p||_inf of pass p (stale for
+// passes that did not run in the last slot).
+extern "C" int midagma_debug_blocked(midagma_solver* s, double* out, int64_t cap) {
+  if (!s || !s->blocked()) return 0;
+  const int64_t K2 = s->D / s->B2, per = NM_PASSES + 2;
+  if (cap < K2 * per) return -1;
+  std::vector<double> part((size_t)K2 * (NM_PASSES + 1) * PART_STRIDE);
+  std::vector<int> done(K2);
+  if (hipMemcpy(part.data(), s->nmPart.p, part.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(done.data(), s->nmDone.p, K2 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  const int B2 = s->B2, NT = B2 / 16;
+  for (int64_t g = 0; g < K2; ++g) {
+    out[g * per] = done[g];
+    for (int p = 0; p <= NM_PASSES; ++p) {
+      const double* rp = part.data() + ((size_t)g * (NM_PASSES + 1) + p) * PART_STRIDE;
+      double m = 0.0;
+      for (int r = 0; r < B2; ++r) {
+        double acc = 0.0;
+        for (int t = 0; t < NT; ++t) acc += rp[r * NT + t];
+        m = std::max(m, acc);
+      }
+      out[g * per + 1 + p] = m;
+    }
+  }
+  return (int)K2;
+}
+
 int64_t midagma_checkpoints(midagma_solver* s, midagma_ckpt* out, int64_t cap) {
   if (!s || !s->d_ckpt) return 0;
   int64_t n = 0;
@@ -711,7 +849,7 @@ int midagma_h(midagma_solver* s, const double* W, double s_dom, double* h, doubl
     launch_build_at(s->scratch.p, D, true, work.p, D, d, s_dom, nullptr, nullptr, s->stream);
     GJWork gw = s->gj();
     gw.Pstore = nullptr;
-    launch_gj_inverse(work.p, D, gw, nullptr, s->stream);
+    launch_gj_inverse(work.p, D, D, gw, nullptr, s->stream);
     std::vector<double> pl(D);
     HIP_TRY(hipMemcpyAsync(pl.data(), s->pivlog.p, D * sizeof(double), hipMemcpyDeviceToHost, s->stream));
     if (G) {
@@ -856,7 +994,7 @@ extern "C" int midagma_logdet_inv_dev(const double* A, int64_t d, int64_t lda, d
     }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     launch_build_at(A, lda, false, ws->A.p, D, d, s_dom, nullptr, nullptr, st);
-    launch_gj_inverse(ws->A.p, D, GJWork{ws->P.p, ws->R.p, ws->C.p, ws->piv.p}, nullptr, st);
+    launch_gj_inverse(ws->A.p, D, D, GJWork{ws->P.p, ws->R.p, ws->C.p, ws->piv.p}, nullptr, st);
     if (logdet_dev) launch_sum_vector(ws->piv.p, d, logdet_dev, nullptr, st);
     if (Mt_dev)
       HIP_TRY(hipMemcpy2DAsync(Mt_dev, ldm * sizeof(double), ws->A.p, D * sizeof(double), d * sizeof(double), d,

@@ -146,7 +146,7 @@ class HipSolver:
         """Average device ms per launch group, measured with hipEvents on the solver stream."""
         out = np.zeros(8)
         check(self.L.midagma_profile_parts(self.h, int(reps), dptr(out)), self.h, "profile_parts")
-        keys = ["build_at", "gj_inverse", "score", "slot", "gemm_xw", "gemm_xty"]
+        keys = ["build_at", "gj_inverse", "score", "slot", "gemm_xw", "gemm_xty", "inverse_fast", "slot_fast"]
         return {k: float(out[i]) for i, k in enumerate(keys)}
 
     def step_partial(self):

@@ -17,7 +17,7 @@ def cov_case(d, n, warm, K):
     cov = X.T @ X / n
     s = HipSolver(d, "l2", "cov")
     s.set_cov(cov)
-    s.begin(np.zeros((d, d)), 1.0, warm + K + 10, 1.0, 3e-4, tol=-1.0)
+    s.begin(np.zeros((d, d)), 1.0, warm + K + 1000, 1.0, 3e-4, tol=-1.0)
     s.run_slots(warm)
     s.sync()
     t0 = time.perf_counter()
@@ -37,7 +37,7 @@ def data_case(d, n, warm, K, loss="l2"):
     s.set_data(X, n_global=n)
     if loss == "logistic":
         s.set_cov(X.T @ X / n)
-    s.begin(np.zeros((d, d)), 1.0, warm + K + 10, 1.0, 3e-4, tol=-1.0)
+    s.begin(np.zeros((d, d)), 1.0, warm + K + 1000, 1.0, 3e-4, tol=-1.0)
     s.run_slots(warm)
     s.sync()
     t0 = time.perf_counter()
