@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 1
+#define MIDAGMA_ABI_VERSION 2
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -61,9 +61,15 @@ typedef struct {
   double obj_last, score_last, h_last, l1_last;
 } midagma_result;
 
+/* The numeric fields of the reference's `minimize.checkpoint` event (linear.py:290-326):
+ * obj_total, score_datafit, reg_dag_value (h), lr, w_abs_sum (l1), W statistics after the
+ * step, and the norms of the checkpoint step's gradients (linear.py:262-273). */
 typedef struct {
   int64_t iter;
-  double obj, score, h, lr, l1; /* subset of the minimize.checkpoint record (linear.py:290-326) */
+  double obj, score, h, lr, l1;
+  double w_norm, max_abs_w, min_abs_w_nonzero;
+  double grad_raw_norm, grad_step_norm, grad_score_norm, grad_dag_norm, grad_l1_norm, grad_inc_norm;
+  double elapsed; /* seconds since the call's first device slot */
 } midagma_ckpt;
 
 int midagma_abi_version(void);

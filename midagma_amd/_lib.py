@@ -35,7 +35,11 @@ class MidagmaResult(C.Structure):
 
 class MidagmaCkpt(C.Structure):
     _fields_ = [("iter", C.c_int64), ("obj", C.c_double), ("score", C.c_double), ("h", C.c_double),
-                ("lr", C.c_double), ("l1", C.c_double)]
+                ("lr", C.c_double), ("l1", C.c_double),
+                ("w_norm", C.c_double), ("max_abs_w", C.c_double), ("min_abs_w_nonzero", C.c_double),
+                ("grad_raw_norm", C.c_double), ("grad_step_norm", C.c_double), ("grad_score_norm", C.c_double),
+                ("grad_dag_norm", C.c_double), ("grad_l1_norm", C.c_double), ("grad_inc_norm", C.c_double),
+                ("elapsed", C.c_double)]
 
 
 class HipSolverError(RuntimeError):

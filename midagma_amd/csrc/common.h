@@ -67,13 +67,24 @@ struct State {
   double obj_last, score_last, h_last, l1_last;
   int32_t flags;         // bit0: inverse has an entry < 0 after +1e-16; bit1: non-finite
   int32_t warm_valid;    // Pstore holds the diagonal-block inverses of the previous slot
+  uint64_t t0;           // device real-time clock (100 MHz) at the call's first slot
 };
 
-// One checkpoint record (linear.py:280-326 subset; norms are a later row).
+// One checkpoint record: the numeric fields of the reference's `minimize.checkpoint` event
+// (linear.py:290-326).  W statistics are of W after the checkpoint step; the gradient norms
+// are of that step (linear.py:262-273), as the reference computes them.
 struct CkptRec {
   int64_t iter;
   double obj, score, h, lr, l1;
+  double w_norm, max_abs_w, min_abs_w_nonzero;
+  double grad_raw_norm, grad_step_norm, grad_score_norm, grad_dag_norm, grad_l1_norm, grad_inc_norm;
+  double elapsed;  // seconds from the call's first slot to this record (device real-time clock)
 };
+
+// Per-workgroup partials the fused update leaves on a checkpoint step (sums of squares, then
+// max |W| and min nonzero |W|), reduced by the next slot's controller.
+constexpr int NORM_FIELDS = 9;
+enum NormField : int { NF_GOBJ = 0, NF_GSCORE, NF_GDAG, NF_GL1, NF_GINC, NF_GSTEP, NF_W2, NF_WMAX, NF_WMIN };
 
 __host__ __device__ inline int64_t round_up64(int64_t x) { return (x + 63) / 64 * 64; }
 

@@ -79,12 +79,14 @@ void launch_sum_vector(const double* v, int64_t n, double* out, const State* st,
 // --- step.hip ---------------------------------------------------------------
 void launch_reduce_check(const double* Mt, const double* W, const double* Z, const Params* pr, State* st,
                          double* partials, int64_t d, int64_t D, hipStream_t stream);
+// npart: the checkpoint-step norm partials of fused_update (NORM_FIELDS per workgroup of its
+// ceil(d/256) x d grid), reduced into the checkpoint record.
 void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
                     const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
-                    hipStream_t stream);
+                    const double* npart, int64_t d, hipStream_t stream);
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
                          const double* Mt, const double* Z, const double* cov, const double* minc,
-                         const double* mexc, int64_t d, int64_t D, hipStream_t stream);
+                         const double* mexc, int64_t d, int64_t D, double* npart, hipStream_t stream);
 // y = a * x elementwise over n doubles
 void launch_scale(const double* x, double a, double* y, int64_t n, hipStream_t stream);
 // G = 2 * W * Mt on the logical block (linear.py:115)

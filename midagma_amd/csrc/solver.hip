@@ -49,6 +49,7 @@ struct midagma_solver {
   std::string err;
 
   DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
+  DevBuf npart;  // checkpoint-step norm partials (fused_update -> control)
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
   DevBuf Malt, Pst2, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone;
@@ -85,7 +86,7 @@ struct midagma_solver {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2,
-                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone})
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart})
       b->release();
     if (d_params) (void)hipFree(d_params);
     if (d_state) (void)hipFree(d_state);
@@ -170,9 +171,10 @@ struct midagma_solver {
 
   void enqueue_part2() {
     launch_reduce_check(Mt.p, W.p, zbuf, d_params, d_state, partials.p, d, D, stream);
-    launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, stream);
+    launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
+                   stream);
     launch_fused_update(d_params, d_state, W.p, m.p, v.p, g.p, Mt.p, zbuf, cov.p, has_inc ? minc.p : nullptr,
-                        has_exc ? mexc.p : nullptr, d, D, stream);
+                        has_exc ? mexc.p : nullptr, d, D, npart.p, stream);
   }
 
   hipGraphExec_t capture(int which) {
@@ -216,6 +218,8 @@ struct midagma_solver {
     pivlog.alloc(D);
     Pstore.alloc((size_t)D * 32);
     partials.alloc(2 * NRED);
+    npart.alloc((size_t)((d + NTHREADS - 1) / NTHREADS) * d * NORM_FIELDS);
+    HIP_TRY(hipMemsetAsync(npart.p, 0, npart.n * sizeof(double), stream));
     if (D % 128 == 0 && (D / 128) * (D / 128) < 256) {
       cov_split = (int)std::min<int64_t>(4, D / 128);
       if (cov_split > 1) cov_parts.alloc((size_t)cov_split * DD);

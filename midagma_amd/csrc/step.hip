@@ -13,6 +13,18 @@
 
 namespace midagma {
 
+__device__ __forceinline__ double block_sum_min(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = NTHREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmin(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
 __device__ __forceinline__ double block_sum(double v, double* red) {
   red[threadIdx.x] = v;
   __syncthreads();
@@ -67,7 +79,8 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
                                                            const double* __restrict__ pivlog,
                                                            const double* __restrict__ loss_total,
                                                            const double* __restrict__ bc_table,
-                                                           CkptRec* __restrict__ ckpt, int64_t ckpt_cap) {
+                                                           CkptRec* __restrict__ ckpt, int64_t ckpt_cap,
+                                                           const double* __restrict__ npart, int64_t nnpart) {
   if (st->status != ST_RUNNING) {
     if (threadIdx.x == 0) st->action = ACT_NOOP;
     return;
@@ -75,6 +88,7 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
   __shared__ double red[NTHREADS];
   const bool ck = st->ckpt_pending != 0;
   double sd = 0.0, l1 = 0.0, ld = 0.0;
+  double nf[NORM_FIELDS];
   if (ck) {
     for (int i = threadIdx.x; i < NRED; i += NTHREADS) {
       sd += partials[2 * i];
@@ -84,8 +98,20 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
     sd = block_sum(sd, red);
     l1 = block_sum(l1, red);
     ld = block_sum(ld, red);
+    // the checkpoint step's norms (fused_update partials of the previous slot)
+    for (int f = 0; f < NORM_FIELDS; ++f) nf[f] = f == NF_WMIN ? INFINITY : 0.0;
+    for (int64_t b = threadIdx.x; b < nnpart; b += NTHREADS) {
+      const double* q = npart + b * NORM_FIELDS;
+      for (int f = 0; f < NF_WMAX; ++f) nf[f] += q[f];
+      nf[NF_WMAX] = fmax(nf[NF_WMAX], q[NF_WMAX]);
+      nf[NF_WMIN] = fmin(nf[NF_WMIN], q[NF_WMIN]);
+    }
+    for (int f = 0; f < NF_WMAX; ++f) nf[f] = block_sum(nf[f], red);
+    nf[NF_WMAX] = -block_sum_min(-nf[NF_WMAX], red);
+    nf[NF_WMIN] = block_sum_min(nf[NF_WMIN], red);
   }
   if (threadIdx.x != 0) return;
+  if (st->slots == 0) st->t0 = __builtin_amdgcn_s_memrealtime();
   st->slots += 1;
   st->warm_valid = 1;  // this slot's GJ pass stored every diagonal-block inverse
   const int flags = st->flags;
@@ -103,6 +129,16 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
       r.h = h;
       r.lr = st->lr;
       r.l1 = l1;
+      r.w_norm = sqrt(nf[NF_W2]);
+      r.max_abs_w = nf[NF_WMAX];
+      r.min_abs_w_nonzero = isfinite(nf[NF_WMIN]) ? nf[NF_WMIN] : 0.0;  // linear.py:311: 0 if W == 0
+      r.grad_raw_norm = sqrt(nf[NF_GOBJ]);
+      r.grad_step_norm = sqrt(nf[NF_GSTEP]);
+      r.grad_score_norm = sqrt(nf[NF_GSCORE]);
+      r.grad_dag_norm = sqrt(nf[NF_GDAG]);
+      r.grad_l1_norm = sqrt(nf[NF_GL1]);
+      r.grad_inc_norm = sqrt(nf[NF_GINC]);
+      r.elapsed = (double)(__builtin_amdgcn_s_memrealtime() - st->t0) * 1e-8;
     }
     st->n_ckpt += 1;
     st->obj_last = obj;
@@ -157,15 +193,90 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
 
 __device__ __forceinline__ double sign_of(double w) { return w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : w); }
 
+// The STEP of a checkpoint iteration: the same update as fused_update_kernel plus the
+// partials of the record's norms (linear.py:262-273, 307-311), one row of NORM_FIELDS per
+// workgroup.  Only every `checkpoint`-th slot takes this path.
+__device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr, const State* __restrict__ st,
+                                                   double* __restrict__ W, double* __restrict__ m,
+                                                   double* __restrict__ v, double* __restrict__ g,
+                                                   const double* __restrict__ Mt, const double* __restrict__ Z,
+                                                   const double* __restrict__ cov, const double* __restrict__ minc,
+                                                   const double* __restrict__ mexc, int64_t d, int64_t D,
+                                                   double* __restrict__ npart) {
+  __shared__ double red[NORM_FIELDS][4];
+  const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  double q[NORM_FIELDS];
+  for (int f = 0; f < NORM_FIELDS; ++f) q[f] = f == NF_WMIN ? INFINITY : 0.0;
+  if (j < d) {
+    const int64_t idx = i * D + j;
+    const double w = W[idx];
+    const double mt = Mt[idx] + 1e-16;
+    double gs = pr->zscale * Z[idx];
+    if (pr->logistic) gs = gs + pr->cscale * cov[idx];
+    const double sg = sign_of(w);
+    const double gl1 = pr->mu_l1 * sg;
+    const double gh = (2.0 * w) * mt;
+    double gobj = gs + gl1;
+    gobj = gobj + gh;
+    double ginc = 0.0;
+    if (pr->has_inc) {
+      ginc = minc[idx] * sg;
+      gobj = gobj + ginc;
+    }
+    const double mm = m[idx] * pr->beta1 + pr->c1 * gobj;
+    const double vv = v[idx] * pr->beta2 + pr->c2 * (gobj * gobj);
+    const double mh = mm / st->bc1;
+    const double vh = vv / st->bc2;
+    const double gd = mh / (sqrt(vh) + 1e-8);
+    double wn = w - st->lr_a * gd;
+    if (pr->has_exc) wn = wn * mexc[idx];
+    m[idx] = mm;
+    v[idx] = vv;
+    g[idx] = gd;
+    W[idx] = wn;
+    q[NF_GOBJ] = gobj * gobj;
+    q[NF_GSCORE] = gs * gs;
+    q[NF_GDAG] = gh * gh;
+    q[NF_GL1] = gl1 * gl1;
+    q[NF_GINC] = ginc * ginc;
+    q[NF_GSTEP] = gd * gd;
+    q[NF_W2] = wn * wn;
+    q[NF_WMAX] = fabs(wn);
+    if (wn != 0.0) q[NF_WMIN] = fabs(wn);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int f = 0; f < NORM_FIELDS; ++f) {
+    double x = q[f];
+    for (int off = 32; off > 0; off >>= 1) {
+      const double y = __shfl_xor(x, off);
+      x = f == NF_WMAX ? fmax(x, y) : (f == NF_WMIN ? fmin(x, y) : x + y);
+    }
+    if (lane == 0) red[f][wv] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < NORM_FIELDS) {
+    const int f = threadIdx.x;
+    const double a = red[f][0], b = red[f][1], c = red[f][2], e = red[f][3];
+    const double r = f == NF_WMAX ? fmax(fmax(a, b), fmax(c, e))
+                                  : (f == NF_WMIN ? fmin(fmin(a, b), fmin(c, e)) : (a + b) + (c + e));
+    npart[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * NORM_FIELDS + f] = r;
+  }
+}
+
 __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
     double* __restrict__ v, double* __restrict__ g, const double* __restrict__ Mt, const double* __restrict__ Z,
     const double* __restrict__ cov, const double* __restrict__ minc, const double* __restrict__ mexc, int64_t d,
-    int64_t D) {
+    int64_t D, double* __restrict__ npart) {
   const int act = st->action;
   if (act == ACT_NOOP) return;
   const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   const int64_t i = blockIdx.y;
+  if (act == ACT_STEP && st->ckpt_pending) {  // checkpoint step: also the record's norms
+    fused_step_with_norms(pr, st, W, m, v, g, Mt, Z, cov, minc, mexc, d, D, npart);
+    return;
+  }
   if (j >= d) return;
   const int64_t idx = i * D + j;
   if (act == ACT_STEP) {
@@ -239,18 +350,19 @@ void launch_reduce_check(const double* Mt, const double* W, const double* Z, con
 
 void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
                     const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
-                    hipStream_t stream) {
+                    const double* npart, int64_t d, hipStream_t stream) {
+  const int64_t nnpart = ((d + NTHREADS - 1) / NTHREADS) * d;  // fused_update workgroups
   hipLaunchKernelGGL(control_kernel, dim3(1), dim3(NTHREADS), 0, stream, pr, st, partials, pivlog, loss_total,
-                     bc_table, ckpt, ckpt_cap);
+                     bc_table, ckpt, ckpt_cap, npart, nnpart);
   HIP_TRY(hipGetLastError());
 }
 
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
                          const double* Mt, const double* Z, const double* cov, const double* minc,
-                         const double* mexc, int64_t d, int64_t D, hipStream_t stream) {
+                         const double* mexc, int64_t d, int64_t D, double* npart, hipStream_t stream) {
   dim3 grid((unsigned)((d + NTHREADS - 1) / NTHREADS), (unsigned)d);
   hipLaunchKernelGGL(fused_update_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, g, Mt, Z, cov, minc,
-                     mexc, d, D);
+                     mexc, d, D, npart);
   HIP_TRY(hipGetLastError());
 }
 

@@ -25,11 +25,10 @@ import typing
 
 import numpy as np
 
+from .slog import LogConfig, StructuredLogger, build_default_logger, checkpoint_row
 from .solver import HipSolver, run_allreduce_minimize
 
 __all__ = ["DagmaLinear"]
-
-_log = logging.getLogger("midagma_amd")
 
 
 class _NullBar:
@@ -67,8 +66,11 @@ class DagmaLinear:
         self.dtype = dtype
         self.vprint = print if verbose else (lambda *a, **k: None)
         self.trek_reg = trek_reg
-        self._logger = logger or _log
-        self._log_cfg = log_cfg
+        # structured logging as the reference (linear.py:64-67): one `minimize.checkpoint` row
+        # per checkpoint, assembled from the device records after each minimize call
+        self._logger = logger or build_default_logger(level=logging.INFO if verbose else logging.WARNING)
+        self._log_cfg = log_cfg or LogConfig(enabled=verbose)
+        self._slog = StructuredLogger(self._logger, self._log_cfg)
         self.score_mode = score_mode or ("cov" if loss_type == "l2" else "data")
         if self.loss_type == "logistic" and self.score_mode != "data":
             raise ValueError("logistic loss needs score_mode='data' (the gradient depends on X every step)")
@@ -165,12 +167,20 @@ class DagmaLinear:
         W = np.ascontiguousarray(W, dtype=np.float64)
         mask_inc, mask_exc = self._masks(mu)
         self._solver.set_masks(mask_inc, mask_exc)
+        logging_on = bool(self._log_cfg.enabled)
         if self.score_mode == "data" and getattr(self, "_allreduce", None) is not None:
             res = run_allreduce_minimize(self._solver, W, mu, max_iter, s, lr, tol, beta_1, beta_2,
                                          self.lambda1, self.checkpoint, allreduce=self._allreduce)
+            ckpts = self._solver.checkpoints() if logging_on else ()
         else:
             res = self._solver.minimize(W, mu, max_iter, s, lr, tol, beta_1, beta_2, self.lambda1,
-                                        self.checkpoint)
+                                        self.checkpoint, want_checkpoints=logging_on)
+            ckpts = res.checkpoints
+        if logging_on:  # linear.py:282-326 (elapsed: device clock from the first slot)
+            stage = getattr(self, "_stage", 0)
+            for rec in ckpts:
+                self._slog.emit("minimize.checkpoint", checkpoint_row(rec, stage=stage, mu=mu, s=s,
+                                                                      trek_reg=self.trek_reg))
         if res.halvings:
             self.vprint(f'Learning rate decreased {res.halvings} time(s) to lr: {res.lr_final}')
         if not res.success:
@@ -238,6 +248,7 @@ class DagmaLinear:
         self.h_final, _ = self._h(self.W_est)
         self.score_final, _ = self._score(self.W_est)
         self.W_est[np.abs(self.W_est) < w_threshold] = 0
+        self._slog.close()
         return self.W_est
 
 

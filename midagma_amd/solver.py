@@ -9,6 +9,7 @@ partial Z_k = X_k^T(...), the caller's all-reduce sums it over ranks
 from __future__ import annotations
 
 import ctypes as C
+from collections import namedtuple
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -16,7 +17,10 @@ import numpy as np
 from . import _lib
 from ._lib import check, dptr
 
-__all__ = ["HipSolver", "MinimizeResult", "run_allreduce_minimize", "device_count"]
+__all__ = ["HipSolver", "MinimizeResult", "CheckpointRecord", "run_allreduce_minimize", "device_count"]
+
+
+CheckpointRecord = namedtuple("CheckpointRecord", [f for f, _ in _lib.MidagmaCkpt._fields_])
 
 
 @dataclass
@@ -166,11 +170,14 @@ class HipSolver:
         return MinimizeResult.from_c(r)
 
     def checkpoints(self):
+        """Checkpoint records of the last minimize call (`CheckpointRecord`: tuple-indexable
+        (iter, obj, score, h, lr, l1, ...) and attribute access)."""
         cap = 1 << 16
         buf = (_lib.MidagmaCkpt * cap)()
         n = self.L.midagma_checkpoints(self.h, buf, cap)
         check(n, self.h, "checkpoints")
-        return [(int(c.iter), c.obj, c.score, c.h, c.lr, c.l1) for c in buf[:n]]
+        return [CheckpointRecord(*(int(c.iter) if f == "iter" else float(getattr(c, f))
+                                   for f in CheckpointRecord._fields)) for c in buf[:n]]
 
     # -- helpers of the reference API ----------------------------------------------
     def h_value(self, W: np.ndarray, s: float = 1.0, grad: bool = True):

@@ -329,6 +329,55 @@ def test_blocked_fast_path_trajectory(hip, d):
         assert abs(obj - obj_r) <= 1e-10 * abs(obj_r) and abs(h - h_r) <= 1e-9 * max(1.0, abs(h_r))
 
 
+CKPT_FIELDS = {"obj_total": "obj", "score_datafit": "score", "reg_dag_value": "h", "lr": "lr", "w_abs_sum": "l1",
+               "w_norm": "w_norm", "max_abs_w": "max_abs_w", "min_abs_w_nonzero": "min_abs_w_nonzero",
+               "grad_raw_norm": "grad_raw_norm", "grad_step_norm": "grad_step_norm",
+               "grad_score_norm": "grad_score_norm", "grad_dag_norm": "grad_dag_norm",
+               "grad_l1_norm": "grad_l1_norm", "grad_inc_norm": "grad_inc_norm"}
+
+
+@pytest.mark.parametrize("d", [20, 300])
+def test_checkpoint_records_match_oracle(hip, golden, d):
+    """minimize.checkpoint numeric fields (linear.py:262-326) from the device records equal the
+    oracle's, with include/exclude masks so every norm is non-trivial.  d=300 runs the
+    blocked-inverse path (fast slots between the GJ checkpoint slots)."""
+    if d == 20:
+        X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    else:
+        X, _, _ = make_dataset(d, 2 * d, seed=3)
+    exc, inc = ((0, 1), (2, 3), (5, 4)), ((4, 5), (7, 8))
+    o = _oracle(X, exc=exc, inc=inc)
+    o.checkpoint = 50
+    mi, me = o.masks(1.0)
+    sol = _solver(d, o.cov)
+    sol.set_masks(mi, me)
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, 130, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=50, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, 130, 1.0, 3e-4, tol=-1.0)
+    assert np.abs(W - Wr).max() <= 1e-9
+    got = res.checkpoints
+    assert [c.iter for c in got] == [r["iter"] for r in tr.records] == [50, 100, 130]
+    for c, r in zip(got, tr.records):
+        for key, attr in CKPT_FIELDS.items():
+            a, b = getattr(c, attr), r[key]
+            assert abs(a - b) <= 1e-9 * max(1e-12, abs(b)), (c.iter, key, a, b)
+        assert 0.0 <= c.elapsed < 60.0
+
+
+def test_dagma_linear_emits_checkpoint_rows(hip, golden):
+    """fit() with logging on: one reference-schema row per checkpoint of every stage."""
+    from midagma_amd import DagmaLinear
+    from midagma_amd.slog import LogConfig
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    m = DagmaLinear("l2", log_cfg=LogConfig(enabled=True, store_jsonl=False))
+    m.fit(X, lambda1=0.03, T=2, warm_iter=300, max_iter=500, checkpoint=100)
+    rows = m._slog.load(event="minimize.checkpoint")
+    calls = m.minimize_log
+    assert len(rows["iter"]) == sum(-(-c["iters"] // 100) for c in calls)
+    assert set(rows["reg_dag_name"]) == {"dagma_logdet"} and set(rows["mu"]) == {1.0, 0.1}
+    assert all(float(v) >= 0.0 for v in rows["grad_dag_norm"])
+
+
 # --------------------------------------------------------------------------- DagmaMLP h_func
 @pytest.mark.parametrize("d", [20, 200])
 @pytest.mark.parametrize("s", [1.0, 0.8])
