@@ -81,6 +81,10 @@ __device__ __forceinline__ float block_max(float v, float* red4) {
 
 __device__ __forceinline__ double abs_or_inf(double v) { return isfinite(v) ? fabs(v) : INFINITY; }
 
+// The domain flags of reduce_check (linear.py:226-230: any(inv + 1e-16 < 0); non-finite),
+// taken on the last outer step's outputs so the fast slot needs no extra pass over Mt.
+__device__ __forceinline__ int domain_flag(double v) { return (v + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v) ? 0 : 2); }
+
 template <int CTRL>
 __device__ __forceinline__ double dpp_add(double v) {
   const long long b = __double_as_longlong(v);
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
                                                               double* __restrict__ Aout, int64_t D, int B2, int g,
                                                               const double* __restrict__ P, int64_t ldp,
                                                               double* __restrict__ Pst,
-                                                              const int* __restrict__ done,
+                                                              const int* __restrict__ done, int check,
                                                               State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
   if (done && *done == 0) {
@@ -248,25 +252,38 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
     tile32_gemm(P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, img[0], img[1],
                 img[2], img[3]);
     double* out = Aout + (G0 + (int64_t)a * NB) * D + (int64_t)c * NB;
-    acc_foreach(acc, [&](int row, int col, double& v) { st_wt(out + (int64_t)row * D + col, v); });
+    int flag = 0;
+    acc_foreach(acc, [&](int row, int col, double& v) {
+      st_wt(out + (int64_t)row * D + col, v);
+      flag |= domain_flag(v);
+    });
+    if (check && flag) atomicOr(&st->flags, flag);
   } else if (job < 2 * nu) {
     const int j2 = job - nu, iq = j2 / gb, c = j2 % gb, i = iq < g0 ? iq : iq + gb;
     tile32_gemm(Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, img[0], img[1], img[2],
                 img[3]);
     double* out = Aout + (int64_t)i * NB * D + G0 + (int64_t)c * NB;
-    acc_foreach(acc, [&](int row, int col, double& v) { st_wt(out + (int64_t)row * D + col, -v); });
+    int flag = 0;
+    acc_foreach(acc, [&](int row, int col, double& v) {
+      st_wt(out + (int64_t)row * D + col, -v);
+      flag |= domain_flag(-v);
+    });
+    if (check && flag) atomicOr(&st->flags, flag);
   } else {
     const int j3 = job - 2 * nu, a = j3 / gb, c = j3 % gb;
     const double* src = P + (int64_t)a * NB * ldp + (int64_t)c * NB;
     double* out = Aout + (G0 + (int64_t)a * NB) * D + G0 + (int64_t)c * NB;
     double* ps = Pst + (int64_t)a * NB * B2 + (int64_t)c * NB;
+    int flag = 0;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int e = it * NTHREADS + threadIdx.x, row = e >> 5, col = e & 31;
       const double v = src[(int64_t)row * ldp + col];
       st_wt(out + (int64_t)row * D + col, v);
       st_wt(ps + (int64_t)row * B2 + col, v);
+      flag |= domain_flag(v);
     }
+    if (check && flag) atomicOr(&st->flags, flag);
   }
 }
 
@@ -274,7 +291,7 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
 // outside G (Aout[G, j] = P Ain[G, j] from the panel launch).
 __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __restrict__ Ain,
                                                               double* __restrict__ Aout, int64_t D, int B2, int g,
-                                                              const State* __restrict__ st) {
+                                                              int check, State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
   __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
   const int nb = (int)(D / NB), gb = B2 / NB, g0 = g * gb, mb = nb - gb;
@@ -290,11 +307,15 @@ __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __re
               img[2], img[3]);
   double* out = Aout + (int64_t)i * NB * D + (int64_t)j * NB;
   const int lane = threadIdx.x & 63, m0 = q_m0(), n0 = q_n0();
+  int flag = 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int row = m0 + acc_row(lane, t), col = n0 + acc_col(lane);
-    st_wt(out + (int64_t)row * D + col, c_old[t] - acc[t]);
+    const double v = c_old[t] - acc[t];
+    st_wt(out + (int64_t)row * D + col, v);
+    flag |= domain_flag(v);
   }
+  if (check && flag) atomicOr(&st->flags, flag);
 }
 
 }  // namespace
@@ -359,10 +380,13 @@ void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
       P = Ain + G0 * D + G0;
       ldp = D;
     }
+    // the fast slot takes the domain flags from the last outer step's outputs (no reduce_check)
+    const int check = fast && g == K2 - 1;
     hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2,
-                       g, P, ldp, Pst, done, st);
+                       g, P, ldp, Pst, done, check, st);
     if (mb > 0)
-      hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2, g, st);
+      hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2, g, check,
+                         st);
   }
   HIP_TRY(hipGetLastError());
 }

@@ -8,6 +8,8 @@
 // LDS in conflict-free images (mfma64.h); I - W is formed while staging B, the
 // sigmoid and the logistic loss are fused into the epilogue.  Long K (= rows of
 // the shard) is split over blockIdx.z into fixed slices summed in fixed order.
+#include <cstdlib>
+
 #include "launch.h"
 #include "mfma64.h"
 
@@ -88,13 +90,15 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(int64_t K, int64_t kslic
 // accumulator values per lane).  BK = 16, LDS double-buffered with register prefetch of the
 // next k-tile (one barrier per k-tile).  LDS images (strides in doubles, conflict-free for
 // the MFMA fragment reads of a 32-lane group):
-//   op(A) from A[m][k] : [m][k] image, stride 18  (36 r mod 64 distinct for r < 16)
+//   op(A) from A[m][k] : [m][k] image, stride 17  (34 r dwords: distinct banks mod 64 for
+//                        ds_read_b64 AND mod 32 for the ds_read2_b64 hipcc forms from two
+//                        k-steps; stride 18 gave a 2-way conflict there: SQ_LDS_BANK_CONFLICT)
 //   op(A) from A[k][m] : [k][m] image, stride 144 (= 16 mod 32)
 //   op(B)              : [k][n] image, stride 144
 // Workgroups are remapped so consecutive tiles (which share an A panel) run on one XCD.
 constexpr int G_BM = 128, G_BN = 128, G_BK = 16;
-constexpr int G_SMK = 18, G_SKM = 144;
-constexpr int G_IMG = 128 * 18;  // doubles per operand image (== 16 * 144)
+constexpr int G_SMK = 17, G_SKM = 144;
+constexpr int G_IMG = 16 * 144;  // doubles per operand image (>= 128 * 17)
 
 __device__ __forceinline__ int xcd_remap(int w, int nwg) {
   const int q = nwg / 8, r = nwg % 8, x = w % 8;
@@ -155,8 +159,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
     const int i_ = (IT) * NTHREADS + tid;                                                       \
     if (ATRANS)                                                                                 \
       *reinterpret_cast<double2*>((AS) + (i_ >> 6) * G_SKM + 2 * (i_ & 63)) = RA;               \
-    else                                                                                        \
-      *reinterpret_cast<double2*>((AS) + (i_ >> 3) * G_SMK + 2 * (i_ & 7)) = RA;                \
+    else {                                                                                      \
+      double* a_ = (AS) + (i_ >> 3) * G_SMK + 2 * (i_ & 7); /* odd stride: 8-byte aligned */    \
+      a_[0] = RA.x;                                                                             \
+      a_[1] = RA.y;                                                                             \
+    }                                                                                           \
     *reinterpret_cast<double2*>((BS) + (i_ >> 6) * G_SKM + 2 * (i_ & 63)) = RB;                 \
   }
 #define G128_LOAD(KT)                 \
@@ -289,7 +296,8 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
                  int64_t ldb, GemmB bmode, double* C, int64_t ldc, GemmEpi epi, int split, int64_t slice_stride,
                  double* loss_part, int64_t m_valid, int64_t n_valid, const State* st, hipStream_t stream) {
   if (M % 64 || N % 64 || K % 64 || split < 1) throw std::invalid_argument("launch_gemm: bad shape");
-  if (M % 128 == 0 && N % 128 == 0 && K % 128 == 0) {
+  static const bool force64 = getenv("MIDAGMA_EXP_GEMM64") != nullptr;  // experiment knob
+  if (M % 128 == 0 && N % 128 == 0 && K % 128 == 0 && !force64) {
     const int64_t ktiles16 = K / G_BK;
     const int64_t per16 = (ktiles16 + split - 1) / split;
     const int nsplit = (int)((ktiles16 + per16 - 1) / per16);

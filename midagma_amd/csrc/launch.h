@@ -53,7 +53,8 @@ int binv_block(int64_t D);
 double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
 // Mt <- inv(A) for A in binv_build_target(Mt): two-level blocked Gauss-Jordan, diagonal
 // blocks by the warm-started product form (fast; sets ST_NEED_GJ when it cannot) or by the
-// 32-block Gauss-Jordan with pivots (slow).
+// 32-block Gauss-Jordan with pivots (slow).  The fast path also ORs reduce_check's domain
+// flags into st->flags from the last outer step's outputs.
 void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream);
 
@@ -84,9 +85,12 @@ void launch_reduce_check(const double* Mt, const double* W, const double* Z, con
 void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
                     const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
                     const double* npart, int64_t d, hipStream_t stream);
+// Z: the score partial, or (zsplit > 1) split-K slices Z + z*zstride summed here in the order
+// of launch_sum_slices.
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
-                         const double* Mt, const double* Z, const double* cov, const double* minc,
-                         const double* mexc, int64_t d, int64_t D, double* npart, hipStream_t stream);
+                         const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
+                         const double* minc, const double* mexc, int64_t d, int64_t D, double* npart,
+                         hipStream_t stream);
 // y = a * x elementwise over n doubles
 void launch_scale(const double* x, double a, double* y, int64_t n, hipStream_t stream);
 // G = 2 * W * Mt on the logical block (linear.py:115)

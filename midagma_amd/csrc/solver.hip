@@ -132,8 +132,9 @@ struct midagma_solver {
     // (a fork/join of the score GEMMs onto a second stream inside the graph measured slower:
     // the cross-queue dependencies cost more than the overlap gains)
     if (mode == MIDAGMA_MODE_COV) {
-      // rhs = ((-mu) cov) @ (I - W)    (linear.py:244)
-      enqueue_cov_gemm(covs.p, W.p, zbuf, d_state);
+      // rhs = ((-mu) cov) @ (I - W)    (linear.py:244); a fast slot leaves the split-K slices
+      // for fused_update to sum (its only reader there)
+      enqueue_cov_gemm(covs.p, W.p, zbuf, d_state, /*sum=*/!(fast && blocked()));
     } else {
       enqueue_data_partial(W.p, d_state);
     }
@@ -141,11 +142,11 @@ struct midagma_solver {
 
   // out = Cm @ (I - Wp) on the d x d problem; split-K over fixed slices when the tile grid
   // alone cannot fill the chip (summed in fixed order: deterministic)
-  void enqueue_cov_gemm(const double* Cm, const double* Wp, double* out, const State* st) {
+  void enqueue_cov_gemm(const double* Cm, const double* Wp, double* out, const State* st, bool sum = true) {
     if (cov_split > 1) {
       launch_gemm(D, D, D, Cm, D, false, Wp, D, B_IMINUS, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
                   0, st, stream);
-      launch_sum_slices(cov_parts.p, cov_split, D * D, D * D, out, st, stream);
+      if (sum) launch_sum_slices(cov_parts.p, cov_split, D * D, D * D, out, st, stream);
     } else {
       launch_gemm(D, D, D, Cm, D, false, Wp, D, B_IMINUS, out, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
     }
@@ -169,12 +170,17 @@ struct midagma_solver {
     }
   }
 
-  void enqueue_part2() {
-    launch_reduce_check(Mt.p, W.p, zbuf, d_params, d_state, partials.p, d, D, stream);
+  // fast (blocked cov slots): the domain flags come from the inverse's last outer step and the
+  // score slices are summed inside fused_update; fast slots never carry a checkpoint
+  void enqueue_part2(bool fast = false) {
+    const bool lean = fast && blocked();
+    if (!lean) launch_reduce_check(Mt.p, W.p, zbuf, d_params, d_state, partials.p, d, D, stream);
     launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
                    stream);
-    launch_fused_update(d_params, d_state, W.p, m.p, v.p, g.p, Mt.p, zbuf, cov.p, has_inc ? minc.p : nullptr,
-                        has_exc ? mexc.p : nullptr, d, D, npart.p, stream);
+    const bool slices = lean && cov_split > 1;
+    launch_fused_update(d_params, d_state, W.p, m.p, v.p, g.p, Mt.p, slices ? cov_parts.p : zbuf,
+                        slices ? cov_split : 1, D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr,
+                        d, D, npart.p, stream);
   }
 
   hipGraphExec_t capture(int which) {
@@ -182,7 +188,7 @@ struct midagma_solver {
     HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
       if (which & 1) enqueue_part1((which & 4) != 0);
-      if (which & 2) enqueue_part2();
+      if (which & 2) enqueue_part2((which & 4) != 0);
     } catch (...) {
       (void)hipStreamEndCapture(stream, &graph);
       if (graph) (void)hipGraphDestroy(graph);
@@ -222,6 +228,7 @@ struct midagma_solver {
     HIP_TRY(hipMemsetAsync(npart.p, 0, npart.n * sizeof(double), stream));
     if (D % 128 == 0 && (D / 128) * (D / 128) < 256) {
       cov_split = (int)std::min<int64_t>(4, D / 128);
+      if (const char* e = getenv("MIDAGMA_EXP_COV_SPLIT")) cov_split = atoi(e);  // experiment knob
       if (cov_split > 1) cov_parts.alloc((size_t)cov_split * DD);
     }
     if (mode == MIDAGMA_MODE_COV) B2 = binv_block(D);

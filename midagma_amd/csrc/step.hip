@@ -193,6 +193,13 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
 
 __device__ __forceinline__ double sign_of(double w) { return w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : w); }
 
+// the score partial at idx: one buffer, or split-K slices summed as sum_slices_kernel does
+__device__ __forceinline__ double z_at(const double* __restrict__ Z, int zsplit, int64_t zstride, int64_t idx) {
+  double acc = Z[idx];
+  for (int z = 1; z < zsplit; ++z) acc += Z[z * zstride + idx];
+  return acc;
+}
+
 // The STEP of a checkpoint iteration: the same update as fused_update_kernel plus the
 // partials of the record's norms (linear.py:262-273, 307-311), one row of NORM_FIELDS per
 // workgroup.  Only every `checkpoint`-th slot takes this path.
@@ -200,6 +207,7 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
                                                    double* __restrict__ W, double* __restrict__ m,
                                                    double* __restrict__ v, double* __restrict__ g,
                                                    const double* __restrict__ Mt, const double* __restrict__ Z,
+                                                   int zsplit, int64_t zstride,
                                                    const double* __restrict__ cov, const double* __restrict__ minc,
                                                    const double* __restrict__ mexc, int64_t d, int64_t D,
                                                    double* __restrict__ npart) {
@@ -212,7 +220,7 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
     const int64_t idx = i * D + j;
     const double w = W[idx];
     const double mt = Mt[idx] + 1e-16;
-    double gs = pr->zscale * Z[idx];
+    double gs = pr->zscale * z_at(Z, zsplit, zstride, idx);
     if (pr->logistic) gs = gs + pr->cscale * cov[idx];
     const double sg = sign_of(w);
     const double gl1 = pr->mu_l1 * sg;
@@ -267,14 +275,14 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
 __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
     double* __restrict__ v, double* __restrict__ g, const double* __restrict__ Mt, const double* __restrict__ Z,
-    const double* __restrict__ cov, const double* __restrict__ minc, const double* __restrict__ mexc, int64_t d,
-    int64_t D, double* __restrict__ npart) {
+    int zsplit, int64_t zstride, const double* __restrict__ cov, const double* __restrict__ minc,
+    const double* __restrict__ mexc, int64_t d, int64_t D, double* __restrict__ npart) {
   const int act = st->action;
   if (act == ACT_NOOP) return;
   const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   const int64_t i = blockIdx.y;
   if (act == ACT_STEP && st->ckpt_pending) {  // checkpoint step: also the record's norms
-    fused_step_with_norms(pr, st, W, m, v, g, Mt, Z, cov, minc, mexc, d, D, npart);
+    fused_step_with_norms(pr, st, W, m, v, g, Mt, Z, zsplit, zstride, cov, minc, mexc, d, D, npart);
     return;
   }
   if (j >= d) return;
@@ -282,7 +290,7 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
   if (act == ACT_STEP) {
     const double w = W[idx];
     const double mt = Mt[idx] + 1e-16;
-    double gs = pr->zscale * Z[idx];
+    double gs = pr->zscale * z_at(Z, zsplit, zstride, idx);
     if (pr->logistic) gs = gs + pr->cscale * cov[idx];
     const double sg = sign_of(w);
     double gobj = gs + pr->mu_l1 * sg;
@@ -358,11 +366,12 @@ void launch_control(const Params* pr, State* st, const double* partials, const d
 }
 
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
-                         const double* Mt, const double* Z, const double* cov, const double* minc,
-                         const double* mexc, int64_t d, int64_t D, double* npart, hipStream_t stream) {
+                         const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
+                         const double* minc, const double* mexc, int64_t d, int64_t D, double* npart,
+                         hipStream_t stream) {
   dim3 grid((unsigned)((d + NTHREADS - 1) / NTHREADS), (unsigned)d);
-  hipLaunchKernelGGL(fused_update_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, g, Mt, Z, cov, minc,
-                     mexc, d, D, npart);
+  hipLaunchKernelGGL(fused_update_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, g, Mt, Z, zsplit,
+                     zstride, cov, minc, mexc, d, D, npart);
   HIP_TRY(hipGetLastError());
 }
 
