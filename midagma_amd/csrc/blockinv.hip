@@ -21,6 +21,8 @@
 //         for the log-det on checkpoint slots, and every slot the fast path cannot take
 //         (first slot of a minimize call, rho > 0.25, no convergence): the fast kernels
 //         then set ST_NEED_GJ and the host re-runs the slot on the slow path.
+#include <cstdlib>
+
 #include "launch.h"
 #include "tile32.h"
 
@@ -320,6 +322,10 @@ __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __re
 
 }  // namespace
 
+// (D - B2) from which the trailing update runs on the 128-tile GEMM: (D - B2)/128 >= 14
+// gives >= 196 workgroups
+static const int64_t TRAIL128_MIN = getenv("MIDAGMA_EXP_TRAIL128") ? atoll(getenv("MIDAGMA_EXP_TRAIL128")) : 1792;
+
 int binv_block(int64_t D) {
   if (D < 256 || D % 128 != 0) return 0;  // fast path not available: plain GJ
   return D % 256 == 0 ? 256 : 128;
@@ -384,9 +390,14 @@ void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     const int check = fast && g == K2 - 1;
     hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2,
                        g, P, ldp, Pst, done, check, st);
-    if (mb > 0)
-      hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2, g, check,
-                         st);
+    if (mb > 0) {
+      // large D: 128 x 128 tiles (operand reuse; enough tiles to fill the chip), else 32 x 32
+      if (D - B2 >= TRAIL128_MIN)
+        launch_trail128(Ain, Aout, D, B2, g, check, st, stream);
+      else
+        hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2, g, check,
+                           st);
+    }
   }
   HIP_TRY(hipGetLastError());
 }

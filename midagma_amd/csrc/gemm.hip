@@ -119,7 +119,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
   const int t = xcd_remap(blockIdx.x, nwg);
   const int per_slice = tiles_m * tiles_n;
   const int z = t / per_slice, rem = t % per_slice;
-  const int bm = rem / tiles_n, bn = rem % tiles_n;
+  int bm = rem / tiles_n, bn = rem % tiles_n;
+  if (EPI == EPI_SUB_BAND) {
+    // trailing update of the blocked inverse: the tile grid skips the pivot band
+    // [m_valid, m_valid + n_valid) (in 128-tiles) in both rows and columns
+    bm += bm >= (int)m_valid ? (int)n_valid : 0;
+    bn += bn >= (int)m_valid ? (int)n_valid : 0;
+  }
   const int64_t m0 = (int64_t)bm * G_BM, n0 = (int64_t)bn * G_BN;
   const int64_t k_begin = (int64_t)z * kslice;
   const int64_t k_end = (k_begin + kslice < K) ? k_begin + kslice : K;
@@ -224,6 +230,24 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
 #undef G128_STORE1
 
   double* Ct = C + (int64_t)z * slice_stride;
+  if (EPI == EPI_SUB_BAND) {  // C = C0 - acc, C0 passed as loss_part; slice_stride = check flags
+    const double* C0 = loss_part;
+    int flag = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const int64_t row = m0 + mb + i * 16 + acc_row(lane, tt);
+          const int64_t col = n0 + nbs + j * 16 + acc_col(lane);
+          const double v = C0[row * ldc + col] - acc[i][j][tt];
+          C[row * ldc + col] = v;
+          flag |= (v + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v) ? 0 : 2);
+        }
+    if (slice_stride && flag) atomicOr(const_cast<int32_t*>(&st->flags), flag);
+    return;
+  }
   if (EPI == EPI_STORE) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -285,6 +309,7 @@ void gemm_setup_attributes() {
   set_attr128<true, B_PLAIN, EPI_STORE>();
   set_attr128<true, B_IMINUS, EPI_STORE>();
   set_attr128<false, B_PLAIN, EPI_SIGMOID>();
+  set_attr128<false, B_PLAIN, EPI_SUB_BAND>();
   set_attr<false, B_PLAIN, EPI_STORE>();
   set_attr<false, B_IMINUS, EPI_STORE>();
   set_attr<true, B_PLAIN, EPI_STORE>();
@@ -310,6 +335,8 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
     if (epi == EPI_SIGMOID) {
       if (a_trans || bmode != B_PLAIN || nsplit != 1) throw std::invalid_argument("launch_gemm: sigmoid form");
       MIDAGMA_GEMM128(false, B_PLAIN, EPI_SIGMOID);
+    } else if (epi == EPI_SUB_BAND) {
+      throw std::invalid_argument("launch_gemm: use launch_trail128");
     } else if (!a_trans && bmode == B_PLAIN) {
       MIDAGMA_GEMM128(false, B_PLAIN, EPI_STORE);
     } else if (!a_trans) {
@@ -344,6 +371,19 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
     MIDAGMA_GEMM(true, B_IMINUS, EPI_STORE);
   }
 #undef MIDAGMA_GEMM
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
+                     hipStream_t stream) {
+  if (D % 128 || B2 % 128) throw std::invalid_argument("launch_trail128: D, B2 must be multiples of 128");
+  const int tm = (int)((D - B2) / 128);
+  if (tm <= 0) return;
+  const int64_t G0 = g * B2;
+  // A = Ain[:, G] (lda D), B = Aout[G, :] (the row panel), C = Aout, C0 = Ain; K = B2
+  hipLaunchKernelGGL((gemm128_kernel<false, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
+                     kGemm128Lds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
+                     (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
   HIP_TRY(hipGetLastError());
 }
 

@@ -60,7 +60,7 @@ void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
 
 // --- gemm.hip ---------------------------------------------------------------
 enum GemmB : int { B_PLAIN = 0, B_IMINUS = 1 };
-enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1 };
+enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1, EPI_SUB_BAND = 2 /* launch_trail128 only */ };
 void gemm_setup_attributes();
 // C[M x N] = op(A) * op(B); op(A) = A ([m][k], lda) or, if a_trans, A stored [k][m] (lda);
 // op(B) = B or (I - B) ([k][n], ldb).  M, N, K multiples of 64.  With split > 1
@@ -71,6 +71,11 @@ void gemm_setup_attributes();
 void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, bool a_trans, const double* B,
                  int64_t ldb, GemmB bmode, double* C, int64_t ldc, GemmEpi epi, int split, int64_t slice_stride,
                  double* loss_part, int64_t m_valid, int64_t n_valid, const State* st, hipStream_t stream);
+// Trailing update of the blocked inverse's outer step g on 128 x 128 tiles:
+// Aout[i, j] = Ain[i, j] - Ain[i, G] Aout[G, j] for i, j outside G = [g B2, (g+1) B2);
+// with `check`, ORs the domain flags of the outputs into st->flags.
+void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
+                     hipStream_t stream);
 // out[i] = sum_z parts[z*stride + i] (fixed order) for i < count.
 void launch_sum_slices(const double* parts, int split, int64_t stride, int64_t count, double* out,
                        const State* st, hipStream_t stream);

@@ -307,16 +307,17 @@ def test_minimize_d1000_short(hip):
     assert np.abs(W - Wr).max() <= 1e-10
 
 
-@pytest.mark.parametrize("d", [300, 600, 1000])
+@pytest.mark.parametrize("d", [300, 600, 1000, 2000])
 def test_blocked_fast_path_trajectory(hip, d):
     """Cov mode at d > 192 runs the two-level blocked inverse: warm-started fast slots between
     Gauss-Jordan slots (first slot, every checkpoint).  d=300 -> D=384 (B2=128, 3 outer
-    blocks), 600 -> 640 (B2=128, 5), 1000 -> 1024 (B2=256, 4).  Same iterations, W and
-    checkpoint objectives as the oracle (LAPACK inverse)."""
+    blocks), 600 -> 640 (B2=128, 5), 1000 -> 1024 (B2=256, 4), 2000 -> 2048 (B2=256, 8;
+    trailing update on the 128-tile GEMM).  Same iterations, W and checkpoint objectives as
+    the oracle (LAPACK inverse)."""
     X, _, _ = make_dataset(d, 2 * d, seed=d)
     o = _oracle(X)
     o.checkpoint = 40
-    K = 130
+    K = 130 if d < 2000 else 90
     sol = _solver(d, o.cov)
     W = np.zeros((d, d))
     res = sol.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=40, want_checkpoints=True)
@@ -324,7 +325,7 @@ def test_blocked_fast_path_trajectory(hip, d):
     assert res.iters == tr.iters == K and res.success
     assert np.abs(W - Wr).max() <= 1e-9
     got = [(c[0], c[1], c[3]) for c in res.checkpoints]
-    assert [g[0] for g in got] == [c[0] for c in tr.checkpoints] == [40, 80, 120, 130]
+    assert [g[0] for g in got] == [c[0] for c in tr.checkpoints] == list(range(40, K, 40)) + [K]
     for (it, obj, h), (_, obj_r, _, h_r) in zip(got, tr.checkpoints):
         assert abs(obj - obj_r) <= 1e-10 * abs(obj_r) and abs(h - h_r) <= 1e-9 * max(1.0, abs(h_r))
 
