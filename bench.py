@@ -51,6 +51,10 @@ def parse():
     p.add_argument("--no-cov", action="store_true")
     p.add_argument("--profile-reps", type=int, default=3)
     p.add_argument("--no-fit", action="store_true", help="skip the full-fit wall-clock leg (config 2)")
+    p.add_argument("--no-large", action="store_true", help="skip the config 3 leg (d=5000, n=5e4, cov mode)")
+    p.add_argument("--large-d", type=int, default=5000)
+    p.add_argument("--large-n", type=int, default=50_000)
+    p.add_argument("--large-steps", type=int, default=100)
     return p.parse_args()
 
 
@@ -176,6 +180,41 @@ def bench_cov(args, device):
                 r.iters == K + 20), prof=prof, cov=cov)
 
 
+def bench_cov_large(args, device):
+    """Config 3: d=5000, n=5e4, l2, cov mode on one GPU -- the inverse-dominated
+    size.  X is generated and reduced to cov = X^T X / n on the GPU (torch plumbing: a CPU
+    generator would take minutes); the solver gets cov as the reference's fit() would."""
+    import torch
+    from midagma_amd.solver import HipSolver
+    d, n = args.large_d, args.large_n
+    dev = torch.device("cuda", device)
+    X, _ = make_shard(d, n, 1, 0, args.seed, dev)
+    X -= X.mean(dim=0, keepdim=True)
+    cov = (X.T @ X / float(n)).cpu().numpy()
+    del X
+    torch.cuda.empty_cache()
+    s = HipSolver(d, "l2", "cov", device=device)
+    s.set_cov(cov)
+    K = args.large_steps
+    s.begin(np.zeros((d, d)), 1.0, K + 1000, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
+    s.run_slots(3)
+    s.sync()
+    t0 = time.perf_counter()
+    s.run_slots(K)
+    s.sync()
+    t1 = time.perf_counter()
+    r = s.poll()
+    prof = s.profile_parts(3)
+    s.close()
+    F = 4.0 * d ** 3
+    return dict(value=K / (t1 - t0), unit="steps/s", ms_per_step=(t1 - t0) / K * 1e3, steps=K,
+                verified=(r.status == 0 and r.iters == K + 3),
+                workload=f"config3: d={d}, n={n}, l2, cov mode (reference algorithm), 1 GPU",
+                kernel_ms={k: round(v, 4) for k, v in prof.items()},
+                slot_tflops=F / ((t1 - t0) / K) / 1e12, slot_frac_fp64_peak=F / ((t1 - t0) / K) / 1e12 / 78.6,
+                cov=cov)
+
+
 _CPU_CHILD = r"""
 import json, os, sys, time
 import numpy as np
@@ -203,7 +242,10 @@ with threadpool_limits(limits=th):
         o.cov, o.d, o.n, o.eye, o.lambda1, o.checkpoint = cov, d, 10000, np.eye(d), 0.03, 10 ** 9
         o.inc = o.exc = None
         o.X = None
-        print(json.dumps({"t": per_step(o, 1, 3) if th == 1 else per_step(o, 2, 5)}))
+        if d >= 3000:  # config 3: a few seconds per step -- 1 and 2 steps (3 CPU steps)
+            print(json.dumps({"t": per_step(o, 1, 2)}))
+        else:
+            print(json.dumps({"t": per_step(o, 1, 3) if th == 1 else per_step(o, 2, 5)}))
     else:
         ts = []
         for n in (int(sys.argv[5]), 2 * int(sys.argv[5])):
@@ -325,6 +367,9 @@ def main():
     fit_res = None
     if rank == 0 and world == 1 and not args.no_fit:
         fit_res = bench_fit(args, local)
+    large_res = None
+    if rank == 0 and world == 1 and not args.no_large and args.workload == "data":
+        large_res = bench_cov_large(args, local)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and cov_res is not None:
         cpu = cpu_baseline(args, cov_res["cov"])
@@ -387,6 +432,23 @@ def main():
             if "reference_algorithm" in cpu and cov_res is not None:
                 line["cpu_reference_algorithm"] = cpu["reference_algorithm"]
                 line["cov_mode_vs_cpu_reference_algorithm"] = cov_res["value"] / cpu["reference_algorithm"]["value"]
+        if large_res is not None:
+            lr_ = {k: v for k, v in large_res.items() if k != "cov"}
+            if cpu is not None and not args.no_cpu:
+                import tempfile
+                share = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+                with tempfile.TemporaryDirectory() as td:
+                    path = os.path.join(td, "cov.npy")
+                    np.save(path, large_res["cov"])
+                    t = _cpu_runs("cov", args.large_d, path, [share], dict(os.environ))
+                if t:
+                    th, tt = next(iter(t.items()))
+                    lr_["cpu_reference_algorithm"] = dict(
+                        value=1.0 / tt, unit="steps/s", cores=th, kind="port",
+                        sample=f"oracle cov-mode Adam steps at d={args.large_d}: 1 and 2 steps, difference "
+                               f"(checkpoint cost cancelled), {th} threads")
+                    lr_["vs_cpu"] = lr_["value"] * tt
+            line["config3"] = lr_
         if fit_res is not None:
             fr = dict(fit_res)
             fr["workload"] = f"config2: DagmaLinear('l2').fit(X) defaults, d={d}, n={args.cov_n}, 1 GPU (cov mode)"
