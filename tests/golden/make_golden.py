@@ -255,6 +255,28 @@ def gen_fit_envelope(X, seeds=(7, 11, 13, 17, 19, 23, 29, 31)):
                         **{k: np.array(v, dtype=np.float64) for k, v in rows.items()})
 
 
+def gen_trek():
+    """PST trek regularizer value and gradient from the reference (notreks.trek_value_grad)
+    for every seq and agg it offers, on a small in-domain W."""
+    from notreks.notreks import PSTRegularizer, trek_value_grad
+    rng = np.random.default_rng(17)
+    out = {}
+    for d in (8, 20):
+        W = in_domain_W(d, rng, 0.35)
+        pairs = np.array([(i, j) for i in range(d) for j in range(i + 1, d) if rng.uniform() < 0.3], dtype=np.int64)
+        out[f"W_d{d}"], out[f"pairs_d{d}"] = W, pairs
+        for seq in ("exp", "inv", "log", "binom"):
+            for agg in ("mean", "sum", "max", "lse"):
+                kw = {"agg": agg}
+                if seq == "log":
+                    kw["K_log"] = 12
+                tr = PSTRegularizer(I=pairs, seq=seq, weight=0.5, kwargs=kw, mode="opt")
+                v, g = trek_value_grad(W.copy(), tr)
+                out[f"val_{seq}_{agg}_d{d}"] = np.array(v)
+                out[f"grad_{seq}_{agg}_d{d}"] = g
+    np.savez_compressed(os.path.join(HERE, "trek_pst.npz"), **out)
+
+
 def gen_mlp():
     """DagmaMLP.h_func value and autograd gradient (nonlinear.py:68-86).
 
@@ -292,6 +314,7 @@ def main():
         gen_branches(X20)
         gen_fit(X20)
         gen_fit_envelope(X20)
+        gen_trek()
         gen_mlp()
     print("golden fixtures written to", HERE)
 
