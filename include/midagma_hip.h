@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 2
+#define MIDAGMA_ABI_VERSION 3
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -70,6 +70,7 @@ typedef struct {
   double w_norm, max_abs_w, min_abs_w_nonzero;
   double grad_raw_norm, grad_step_norm, grad_score_norm, grad_dag_norm, grad_l1_norm, grad_inc_norm;
   double elapsed; /* seconds since the call's first device slot */
+  double reg_trek_value, grad_trek_norm; /* PST trek regularizer (0 when none) */
 } midagma_ckpt;
 
 int midagma_abi_version(void);
@@ -125,6 +126,17 @@ int midagma_step_finish(midagma_solver* s);
 int midagma_poll(midagma_solver* s, midagma_result* res); /* synchronizes */
 int midagma_end(midagma_solver* s, double* W, midagma_result* res);
 int64_t midagma_checkpoints(midagma_solver* s, midagma_ckpt* out, int64_t cap);
+
+/* The PST trek regularizer of notreks.py (pst / trek_value_grad) inside the loop
+ * (linear.py:251-258, 131-133).  seq: 0 exp, 1 inv, 2 log, 3 binom; agg: 0 mean, 1 sum,
+ * 2 max, 3 lse; mode: 0 off, 1 'log' (value at checkpoints only), 2 'opt' (value and
+ * weight * gradient every step, weight * value in the checkpoint objective); K: log series
+ * terms (binom: ignored, the exponent is d as in the reference); pairs: m (i, j) int64. */
+int midagma_set_trek(midagma_solver* s, int seq, int agg, int mode, double weight, double eps_inv, int64_t K,
+                     const int64_t* pairs, int64_t m);
+/* trek_value_grad(W, tr) (notreks.py): value and, in 'opt' mode, the gradient (G nullable, d x d;
+ * zeros in 'log' mode, as the reference returns). */
+int midagma_trek(midagma_solver* s, const double* W, double* value, double* G);
 
 /* Replaces DagmaLinear._h (linear.py:97-116): h and G_h = 2 W o inv(sI - W o W)^T (G nullable). */
 int midagma_h(midagma_solver* s, const double* W, double s_dom, double* h, double* G);

@@ -39,7 +39,7 @@ class MidagmaCkpt(C.Structure):
                 ("w_norm", C.c_double), ("max_abs_w", C.c_double), ("min_abs_w_nonzero", C.c_double),
                 ("grad_raw_norm", C.c_double), ("grad_step_norm", C.c_double), ("grad_score_norm", C.c_double),
                 ("grad_dag_norm", C.c_double), ("grad_l1_norm", C.c_double), ("grad_inc_norm", C.c_double),
-                ("elapsed", C.c_double)]
+                ("elapsed", C.c_double), ("reg_trek_value", C.c_double), ("grad_trek_norm", C.c_double)]
 
 
 class HipSolverError(RuntimeError):
@@ -78,6 +78,8 @@ EXPORTED = {
     "midagma_poll": (_int, [_vp, C.POINTER(MidagmaResult)]),
     "midagma_end": (_int, [_vp, _dp, C.POINTER(MidagmaResult)]),
     "midagma_checkpoints": (_i64, [_vp, C.POINTER(MidagmaCkpt), _i64]),
+    "midagma_set_trek": (_int, [_vp, _int, _int, _int, _d, _d, _i64, C.POINTER(_i64), _i64]),
+    "midagma_trek": (_int, [_vp, _dp, _dp, _dp]),
     "midagma_h": (_int, [_vp, _dp, _d, _dp, _dp]),
     "midagma_score": (_int, [_vp, _dp, _dp, _dp]),
     "midagma_score_partial": (_int, [_vp, _dp]),

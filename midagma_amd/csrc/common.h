@@ -47,6 +47,9 @@ struct Params {
   double d_log_s;     // d * log(s), host-rounded (linear.py:114)
   int64_t max_iter, checkpoint, d, D, ld_table;
   int32_t has_inc, has_exc, logistic, pad_;
+  double trek_weight;  // PST trek regularizer (linear.py:257-258, 131-133): weight,
+  int32_t trek_mode;   //   0 off, 1 'log' (value at checkpoints), 2 'opt' (+ gradient every step)
+  int32_t pad2_;
 };
 
 // Device-resident solver state: written only by the 1-workgroup controller
@@ -79,12 +82,13 @@ struct CkptRec {
   double w_norm, max_abs_w, min_abs_w_nonzero;
   double grad_raw_norm, grad_step_norm, grad_score_norm, grad_dag_norm, grad_l1_norm, grad_inc_norm;
   double elapsed;  // seconds from the call's first slot to this record (device real-time clock)
+  double reg_trek_value, grad_trek_norm;  // trek regularizer value at W, ||weight * trek grad||
 };
 
 // Per-workgroup partials the fused update leaves on a checkpoint step (sums of squares, then
 // max |W| and min nonzero |W|), reduced by the next slot's controller.
-constexpr int NORM_FIELDS = 9;
-enum NormField : int { NF_GOBJ = 0, NF_GSCORE, NF_GDAG, NF_GL1, NF_GINC, NF_GSTEP, NF_W2, NF_WMAX, NF_WMIN };
+constexpr int NORM_FIELDS = 10;  // sums of squares first, then the two extrema
+enum NormField : int { NF_GOBJ = 0, NF_GSCORE, NF_GDAG, NF_GL1, NF_GINC, NF_GTREK, NF_GSTEP, NF_W2, NF_WMAX, NF_WMIN };
 
 __host__ __device__ inline int64_t round_up64(int64_t x) { return (x + 63) / 64 * 64; }
 

@@ -58,6 +58,37 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
 void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream);
 
+// --- trek.hip ---------------------------------------------------------------
+enum TrekSeq : int { TREK_EXP = 0, TREK_INV = 1, TREK_LOG = 2, TREK_BINOM = 3 };
+enum TrekAgg : int { TREK_MEAN = 0, TREK_SUM = 1, TREK_MAX = 2, TREK_LSE = 3 };
+constexpr int TREK_TAYLOR_M = 12;   // exp: Taylor degree after scaling to ||X||_1 <= 1/4
+constexpr int TREK_SMAX = 12;       // exp: squaring slots (||W o W||_1 up to 2^10)
+struct TrekCfg {
+  int seq, agg;
+  int mode;              // 1 'log' (value on checkpoint slots), 2 'opt' (value + gradient every slot)
+  double weight, eps_inv;
+  int K;                 // log: series terms; binom: the exponent (= d, notreks pst_mat)
+  int smax;              // exp: squaring slots
+  int64_t m;             // pairs
+  const int32_t* pairs;  // device, (i, j) x m
+};
+struct TrekWork {
+  GJWork gj;             // inv: the Gauss-Jordan side panels (borrowed from the solver)
+  double *X, *F, *H, *S, *GT, *L, *tmp, *tmp2, *tmp3, *tmp4, *slices;  // D x D (slices: 4 D x D or null)
+  double* Q[TREK_TAYLOR_M + 1 > 64 ? TREK_TAYLOR_M + 1 : 64];  // Horner / powering iterates (sized at setup)
+  double* E[TREK_SMAX + 1];
+  double* dQ[2];
+  double* colpart;       // (D / 64) x D
+  double* part;          // 4 x 256
+  double* scal;          // [0] value [1] 2^-s [2] s [3] max [4] coefficient [5] ||W o W||_1
+  State* gates;          // 1 + 2 smax gate words
+};
+// The PST penalty of W (value in w.scal[0]) and, in 'opt' mode, weight * d value / d W into
+// Gtrek (D x D), gated by st (a terminated slot or, in 'log' mode, a non-checkpoint slot
+// runs nothing).
+void launch_trek_pst(const double* W, int64_t d, int64_t D, const TrekCfg& cfg, const TrekWork& w, const State* st,
+                     double* Gtrek, hipStream_t stream);
+
 // --- gemm.hip ---------------------------------------------------------------
 enum GemmB : int { B_PLAIN = 0, B_IMINUS = 1 };
 enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1, EPI_SUB_BAND = 2 /* launch_trail128 only */ };
@@ -87,15 +118,16 @@ void launch_reduce_check(const double* Mt, const double* W, const double* Z, con
                          double* partials, int64_t d, int64_t D, hipStream_t stream);
 // npart: the checkpoint-step norm partials of fused_update (NORM_FIELDS per workgroup of its
 // ceil(d/256) x d grid), reduced into the checkpoint record.
+// trek_val (nullable): the trek regularizer value of this slot's W (PST, trek.hip)
 void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
                     const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
-                    const double* npart, int64_t d, hipStream_t stream);
+                    const double* npart, int64_t d, const double* trek_val, hipStream_t stream);
 // Z: the score partial, or (zsplit > 1) split-K slices Z + z*zstride summed here in the order
-// of launch_sum_slices.
+// of launch_sum_slices.  trek (nullable): weight * trek gradient, added last (linear.py:258).
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
                          const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
-                         const double* minc, const double* mexc, int64_t d, int64_t D, double* npart,
-                         hipStream_t stream);
+                         const double* minc, const double* mexc, const double* trek, int64_t d, int64_t D,
+                         double* npart, hipStream_t stream);
 // y = a * x elementwise over n doubles
 void launch_scale(const double* x, double a, double* y, int64_t n, hipStream_t stream);
 // G = 2 * W * Mt on the logical block (linear.py:115)

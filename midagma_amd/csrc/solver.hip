@@ -50,6 +50,14 @@ struct midagma_solver {
 
   DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
   DevBuf npart;  // checkpoint-step norm partials (fused_update -> control)
+  // PST trek regularizer (trek.hip)
+  TrekCfg tcfg{};
+  bool trek_on = false;
+  std::vector<DevBuf> tbufs;  // every D x D work buffer of the regularizer
+  DevBuf tpairs, tsmall, Gtrek, tslices;
+  State* tgates = nullptr;
+  State* d_state_probe = nullptr;  // RUNNING + checkpoint: gates the API-call (midagma_trek) path
+  TrekWork tw{};
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
   DevBuf Malt, Pst2, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone;
@@ -88,6 +96,10 @@ struct midagma_solver {
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart})
       b->release();
+    for (DevBuf& b : tbufs) b.release();
+    for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices}) b->release();
+    if (tgates) (void)hipFree(tgates);
+    if (d_state_probe) (void)hipFree(d_state_probe);
     if (d_params) (void)hipFree(d_params);
     if (d_state) (void)hipFree(d_state);
     if (d_ckpt) (void)hipFree(d_ckpt);
@@ -138,6 +150,10 @@ struct midagma_solver {
     } else {
       enqueue_data_partial(W.p, d_state);
     }
+    // trek regularizer of this slot's W (linear.py:251-258): every slot in 'opt' mode; in 'log'
+    // mode only checkpoint slots, which are never fast slots
+    if (trek_on && (tcfg.mode == 2 || !(fast && blocked())))
+      launch_trek_pst(W.p, d, D, tcfg, tw, d_state, Gtrek.p, stream);
   }
 
   // out = Cm @ (I - Wp) on the d x d problem; split-K over fixed slices when the tile grid
@@ -176,11 +192,11 @@ struct midagma_solver {
     const bool lean = fast && blocked();
     if (!lean) launch_reduce_check(Mt.p, W.p, zbuf, d_params, d_state, partials.p, d, D, stream);
     launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
-                   stream);
+                   trek_on ? tw.scal : nullptr, stream);
     const bool slices = lean && cov_split > 1;
     launch_fused_update(d_params, d_state, W.p, m.p, v.p, g.p, Mt.p, slices ? cov_parts.p : zbuf,
                         slices ? cov_split : 1, D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr,
-                        d, D, npart.p, stream);
+                        trek_on && tcfg.mode == 2 ? Gtrek.p : nullptr, d, D, npart.p, stream);
   }
 
   hipGraphExec_t capture(int which) {
@@ -209,6 +225,77 @@ struct midagma_solver {
     g_part2 = capture(2);
     if (blocked()) g_fast = capture(3 | 4);
     graphs_valid = true;
+  }
+
+  // ---- trek regularizer ---------------------------------------------------------
+  void set_trek(int seq, int agg, int tmode, double weight, double eps_inv, int64_t K, const int64_t* pairs,
+                int64_t mpairs) {
+    if (tmode == 0 || mpairs <= 0 || weight == 0.0) {  // TrekRegularizer.enabled() false, or no pairs
+      trek_on = false;
+      graphs_valid = false;
+      return;
+    }
+    if (seq < 0 || seq > 3 || agg < 0 || agg > 3 || tmode < 1 || tmode > 2)
+      throw std::invalid_argument("set_trek: bad seq / agg / mode");
+    if (seq == TREK_LOG && K < 1) throw std::invalid_argument("set_trek: K_log must be >= 1");
+    const size_t DD = (size_t)D * D;
+    int nq = 2;
+    if (seq == TREK_EXP) nq = TREK_TAYLOR_M + 1;
+    if (seq == TREK_BINOM) nq = 64 - __builtin_clzll((unsigned long long)d) + 2;
+    const int nbuf = 11 + nq + TREK_SMAX + 1 + 2;
+    if ((int)tbufs.size() < nbuf) tbufs.resize(nbuf);
+    for (int i = 0; i < nbuf; ++i) tbufs[i].alloc(DD);
+    int b = 0;
+    TrekWork w{};
+    w.gj = gj();
+    for (double** slot : {&w.X, &w.F, &w.H, &w.S, &w.GT, &w.L, &w.tmp, &w.tmp2, &w.tmp3, &w.tmp4}) *slot = tbufs[b++].p;
+    ++b;  // spare
+    for (int i = 0; i < nq; ++i) w.Q[i] = tbufs[b++].p;
+    for (int i = 0; i <= TREK_SMAX; ++i) w.E[i] = tbufs[b++].p;
+    w.dQ[0] = tbufs[b++].p;
+    w.dQ[1] = tbufs[b++].p;
+    if (D % 128 == 0 && (D / 128) * (D / 128) < 256) {
+      tslices.alloc(4 * DD);
+      w.slices = tslices.p;
+    }
+    tsmall.alloc((size_t)(D / 64) * D + 4 * 256 + 16);
+    w.colpart = tsmall.p;
+    w.part = tsmall.p + (D / 64) * D;
+    w.scal = w.part + 4 * 256;
+    HIP_TRY(hipMemsetAsync(tsmall.p, 0, tsmall.n * sizeof(double), stream));
+    if (!tgates) HIP_TRY(hipMalloc(&tgates, (1 + 2 * TREK_SMAX) * sizeof(State)));
+    HIP_TRY(hipMemsetAsync(tgates, 0, (1 + 2 * TREK_SMAX) * sizeof(State), stream));
+    w.gates = tgates;
+    Gtrek.alloc(DD);
+    HIP_TRY(hipMemsetAsync(Gtrek.p, 0, DD * sizeof(double), stream));
+    std::vector<int32_t> pr(2 * mpairs);
+    for (int64_t i = 0; i < 2 * mpairs; ++i) {
+      if (pairs[i] < 0 || pairs[i] >= d) throw std::invalid_argument("set_trek: pair index out of range");
+      pr[i] = (int32_t)pairs[i];
+    }
+    tpairs.alloc((size_t)(mpairs + 1));  // 2 int32 per double slot
+    HIP_TRY(hipMemcpy(tpairs.p, pr.data(), pr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    TrekCfg c{};
+    c.seq = seq;
+    c.agg = agg;
+    c.mode = tmode;
+    c.weight = weight;
+    c.eps_inv = eps_inv;
+    c.K = seq == TREK_BINOM ? (int)d : (int)K;
+    c.smax = TREK_SMAX;
+    c.m = mpairs;
+    c.pairs = reinterpret_cast<const int32_t*>(tpairs.p);
+    tcfg = c;
+    tw = w;
+    trek_on = true;
+    if (!d_state_probe) {
+      HIP_TRY(hipMalloc(&d_state_probe, sizeof(State)));
+      State probe{};
+      probe.status = ST_RUNNING;
+      probe.ckpt_pending = 1;
+      HIP_TRY(hipMemcpy(d_state_probe, &probe, sizeof(State), hipMemcpyHostToDevice));
+    }
+    graphs_valid = false;
   }
 
   // ---- buffers -------------------------------------------------------------
@@ -312,6 +399,8 @@ struct midagma_solver {
     p.has_inc = has_inc;
     p.has_exc = has_exc;
     p.logistic = loss == MIDAGMA_LOSS_LOGISTIC;
+    p.trek_weight = trek_on ? tcfg.weight : 0.0;
+    p.trek_mode = trek_on ? tcfg.mode : 0;
     const double n = (double)n_global;
     if (mode == MIDAGMA_MODE_COV) {
       p.zscale = 1.0;  // Z already is ((-mu) cov) @ (I - W)
@@ -846,6 +935,45 @@ int64_t midagma_checkpoints(midagma_solver* s, midagma_ckpt* out, int64_t cap) {
     return MIDAGMA_OK;
   });
   return rc == MIDAGMA_OK ? n : rc;
+}
+
+int midagma_set_trek(midagma_solver* s, int seq, int agg, int mode, double weight, double eps_inv, int64_t K,
+                     const int64_t* pairs, int64_t m) {
+  if (!s || (m > 0 && !pairs) || m < 0) return fail(s, MIDAGMA_E_ARG, "set_trek: bad arguments");
+  return guarded(s, [&] {
+    s->set_trek(seq, agg, mode, weight, eps_inv, K, pairs, m);
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_trek(midagma_solver* s, const double* W, double* value, double* G) {
+  if (!s || !W || !value) return fail(s, MIDAGMA_E_ARG, "trek: null argument");
+  return guarded(s, [&] {
+    const int64_t D = s->D, d = s->d, DD = D * D;
+    if (!s->trek_on) {  // trek_value_grad: (0, zeros) when disabled (notreks.py)
+      *value = 0.0;
+      if (G) std::fill(G, G + d * d, 0.0);
+      return MIDAGMA_OK;
+    }
+    s->scratch.alloc(DD);
+    HIP_TRY(hipMemsetAsync(s->scratch.p, 0, DD * sizeof(double), s->stream));
+    s->upload_matrix(s->scratch, W, d);
+    TrekCfg c = s->tcfg;
+    c.weight = 1.0;  // the bare gradient, as trek_value_grad returns it
+    launch_trek_pst(s->scratch.p, d, D, c, s->tw, s->d_state_probe, s->Gtrek.p, s->stream);
+    HIP_TRY(hipMemcpyAsync(value, s->tw.scal, sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    if (G) {
+      if (c.mode == 2) {
+        HIP_TRY(hipMemcpy2DAsync(G, d * sizeof(double), s->Gtrek.p, D * sizeof(double), d * sizeof(double), d,
+                                 hipMemcpyDeviceToHost, s->stream));
+      } else {
+        std::fill(G, G + d * d, 0.0);
+      }
+    }
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
 }
 
 int midagma_h(midagma_solver* s, const double* W, double s_dom, double* h, double* G) {

@@ -80,7 +80,8 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
                                                            const double* __restrict__ loss_total,
                                                            const double* __restrict__ bc_table,
                                                            CkptRec* __restrict__ ckpt, int64_t ckpt_cap,
-                                                           const double* __restrict__ npart, int64_t nnpart) {
+                                                           const double* __restrict__ npart, int64_t nnpart,
+                                                           const double* __restrict__ trek_val) {
   if (st->status != ST_RUNNING) {
     if (threadIdx.x == 0) st->action = ACT_NOOP;
     return;
@@ -120,7 +121,9 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
     st->ckpt_pending = 0;
     const double h = -ld + pr->d_log_s;
     const double score = pr->logistic ? loss_total[0] * pr->logit_scale : pr->score_scale * sd;
-    const double obj = pr->mu * (score + pr->lambda1 * l1) + h;
+    double obj = pr->mu * (score + pr->lambda1 * l1) + h;
+    const double tv = trek_val ? trek_val[0] : 0.0;
+    if (pr->trek_mode == 2) obj = obj + pr->trek_weight * tv;  // linear.py:131-133
     if (st->n_ckpt < ckpt_cap) {
       CkptRec& r = ckpt[st->n_ckpt];
       r.iter = st->iter;
@@ -139,6 +142,8 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
       r.grad_l1_norm = sqrt(nf[NF_GL1]);
       r.grad_inc_norm = sqrt(nf[NF_GINC]);
       r.elapsed = (double)(__builtin_amdgcn_s_memrealtime() - st->t0) * 1e-8;
+      r.reg_trek_value = tv;
+      r.grad_trek_norm = sqrt(nf[NF_GTREK]);
     }
     st->n_ckpt += 1;
     st->obj_last = obj;
@@ -209,8 +214,8 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
                                                    const double* __restrict__ Mt, const double* __restrict__ Z,
                                                    int zsplit, int64_t zstride,
                                                    const double* __restrict__ cov, const double* __restrict__ minc,
-                                                   const double* __restrict__ mexc, int64_t d, int64_t D,
-                                                   double* __restrict__ npart) {
+                                                   const double* __restrict__ mexc, const double* __restrict__ trek,
+                                                   int64_t d, int64_t D, double* __restrict__ npart) {
   __shared__ double red[NORM_FIELDS][4];
   const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   const int64_t i = blockIdx.y;
@@ -232,6 +237,11 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
       ginc = minc[idx] * sg;
       gobj = gobj + ginc;
     }
+    double gtr = 0.0;
+    if (trek) {  // Gobj + weight * trek_grad (linear.py:257-258); trek holds weight * grad
+      gtr = trek[idx];
+      gobj = gobj + gtr;
+    }
     const double mm = m[idx] * pr->beta1 + pr->c1 * gobj;
     const double vv = v[idx] * pr->beta2 + pr->c2 * (gobj * gobj);
     const double mh = mm / st->bc1;
@@ -248,6 +258,7 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
     q[NF_GDAG] = gh * gh;
     q[NF_GL1] = gl1 * gl1;
     q[NF_GINC] = ginc * ginc;
+    q[NF_GTREK] = gtr * gtr;
     q[NF_GSTEP] = gd * gd;
     q[NF_W2] = wn * wn;
     q[NF_WMAX] = fabs(wn);
@@ -276,13 +287,14 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
     double* __restrict__ v, double* __restrict__ g, const double* __restrict__ Mt, const double* __restrict__ Z,
     int zsplit, int64_t zstride, const double* __restrict__ cov, const double* __restrict__ minc,
-    const double* __restrict__ mexc, int64_t d, int64_t D, double* __restrict__ npart) {
+    const double* __restrict__ mexc, const double* __restrict__ trek, int64_t d, int64_t D,
+    double* __restrict__ npart) {
   const int act = st->action;
   if (act == ACT_NOOP) return;
   const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   const int64_t i = blockIdx.y;
   if (act == ACT_STEP && st->ckpt_pending) {  // checkpoint step: also the record's norms
-    fused_step_with_norms(pr, st, W, m, v, g, Mt, Z, zsplit, zstride, cov, minc, mexc, d, D, npart);
+    fused_step_with_norms(pr, st, W, m, v, g, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, d, D, npart);
     return;
   }
   if (j >= d) return;
@@ -296,6 +308,7 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     double gobj = gs + pr->mu_l1 * sg;
     gobj = gobj + (2.0 * w) * mt;
     if (pr->has_inc) gobj = gobj + minc[idx] * sg;
+    if (trek) gobj = gobj + trek[idx];
     const double mm = m[idx] * pr->beta1 + pr->c1 * gobj;
     const double vv = v[idx] * pr->beta2 + pr->c2 * (gobj * gobj);
     const double mh = mm / st->bc1;
@@ -358,20 +371,20 @@ void launch_reduce_check(const double* Mt, const double* W, const double* Z, con
 
 void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
                     const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
-                    const double* npart, int64_t d, hipStream_t stream) {
+                    const double* npart, int64_t d, const double* trek_val, hipStream_t stream) {
   const int64_t nnpart = ((d + NTHREADS - 1) / NTHREADS) * d;  // fused_update workgroups
   hipLaunchKernelGGL(control_kernel, dim3(1), dim3(NTHREADS), 0, stream, pr, st, partials, pivlog, loss_total,
-                     bc_table, ckpt, ckpt_cap, npart, nnpart);
+                     bc_table, ckpt, ckpt_cap, npart, nnpart, trek_val);
   HIP_TRY(hipGetLastError());
 }
 
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
                          const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
-                         const double* minc, const double* mexc, int64_t d, int64_t D, double* npart,
-                         hipStream_t stream) {
+                         const double* minc, const double* mexc, const double* trek, int64_t d, int64_t D,
+                         double* npart, hipStream_t stream) {
   dim3 grid((unsigned)((d + NTHREADS - 1) / NTHREADS), (unsigned)d);
   hipLaunchKernelGGL(fused_update_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, g, Mt, Z, zsplit,
-                     zstride, cov, minc, mexc, d, D, npart);
+                     zstride, cov, minc, mexc, trek, d, D, npart);
   HIP_TRY(hipGetLastError());
 }
 

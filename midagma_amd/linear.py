@@ -13,8 +13,11 @@ the C ABI.  Extra keyword-only constructor arguments:
 * ``process_group``  a torch.distributed group: in data mode each rank keeps
   its row shard of X and the per-step score partial is all-reduced over it.
 
-The trek regularizer (`trek_reg`, linear.py:251-258) is out of scope for the
-GPU path; passing an enabled one raises.
+Trek regularizers (`trek_reg`, linear.py:251-258): the PST family of
+`notreks.PSTRegularizer` (seq exp / inv / log / binom, agg mean / sum / max / lse,
+modes 'opt' and 'log') runs on the GPU inside the loop (csrc/trek.hip).  The TCC
+regularizer (spectral Perron eigenvectors of a 2d x 2d non-symmetric matrix every
+step, numpy `eig` in the reference) has no GPU path yet; passing an enabled one raises.
 """
 from __future__ import annotations
 
@@ -60,8 +63,8 @@ class DagmaLinear:
         assert loss_type in losses, f"loss_type should be one of {losses}"
         if dtype is not np.float64:
             raise ValueError("the HIP inner solver computes in float64 only (as the reference's cov/X)")
-        if trek_reg is not None and getattr(trek_reg, "enabled", lambda: True)():
-            raise NotImplementedError("trek regularizers are not implemented on the GPU path")
+        if trek_reg is not None and trek_reg.enabled() and str(trek_reg.name).lower().strip() != "pst":
+            raise NotImplementedError(f"trek regularizer {trek_reg.name!r}: only 'pst' runs on the GPU path")
         self.loss_type = loss_type
         self.dtype = dtype
         self.vprint = print if verbose else (lambda *a, **k: None)
@@ -115,6 +118,11 @@ class DagmaLinear:
             else:
                 self._allreduce = None
         s.set_cov(self.cov)
+        tr = self.trek_reg
+        if tr is not None and tr.enabled() and tr.cfg.get("I") is not None and len(tr.cfg["I"]) > 0:
+            kw = dict(tr.cfg.get("kwargs") or {})
+            s.set_trek(tr.cfg["I"], tr.cfg.get("seq", "exp"), agg=kw.get("agg", "mean"), mode=tr.mode,
+                       weight=tr.weight, eps_inv=kw.get("eps_inv", 1e-8), K_log=kw.get("K_log"))
         self._solver = s
 
     # ------------------------------------------------------- reference methods
@@ -132,11 +140,15 @@ class DagmaLinear:
         return self._solver.h_value(W, s, grad=True)
 
     def _func(self, W: np.ndarray, mu: float, s: float = 1.0):
-        """objective at W (linear.py:118-135); trek term is 0 (regularizer disabled)."""
+        """objective at W (linear.py:118-135), with the trek term in 'opt' mode."""
         score, _ = self._score(W)
         h, _ = self._h(W, s)
+        trek_val, _ = self._solver.trek_value(W, grad=False)
         obj = mu * (score + self.lambda1 * np.abs(W).sum()) + h
-        return obj, score, h, 0.0
+        tr = self.trek_reg
+        if tr is not None and tr.enabled() and tr.mode == "opt":
+            obj = obj + tr.weight * trek_val
+        return obj, score, h, trek_val
 
     def _adam_update(self, grad: np.ndarray, iter: int, beta_1: float, beta_2: float) -> np.ndarray:
         """API-compatibility helper (linear.py:138-163).  Not used by `minimize`, whose

@@ -238,7 +238,7 @@ def checkpoint_row(rec, *, stage: int, mu: float, s: float, elapsed_offset: floa
         "reg_dag_value": float(rec.h),
         "reg_dag_cfg": {"s": float(s)},
         "reg_trek_name": trek_reg.name if trek_reg is not None else "none",
-        "reg_trek_value": 0.0,
+        "reg_trek_value": float(getattr(rec, "reg_trek_value", 0.0)),
         "reg_trek_cfg": {k: v for k, v in trek_reg.cfg.items() if k != "I"} if trek_reg is not None else {},
         "trek_mode": trek_reg.mode if trek_reg is not None else "off",
         "trek_weight": float(trek_reg.weight) if trek_reg is not None else 0.0,
@@ -255,5 +255,5 @@ def checkpoint_row(rec, *, stage: int, mu: float, s: float, elapsed_offset: floa
         "grad_dag_norm": float(rec.grad_dag_norm),
         "grad_l1_norm": float(rec.grad_l1_norm),
         "grad_inc_norm": float(rec.grad_inc_norm),
-        "grad_trek_norm": 0.0,
+        "grad_trek_norm": float(getattr(rec, "grad_trek_norm", 0.0)),
     }

@@ -96,6 +96,31 @@ class HipSolver:
         me = None if mask_exc is None else _as_f64(mask_exc)
         check(self.L.midagma_set_masks(self.h, dptr(mi), dptr(me)), self.h, "set_masks")
 
+    TREK_SEQ = {"exp": 0, "inv": 1, "log": 2, "binom": 3}
+    TREK_AGG = {"mean": 0, "sum": 1, "max": 2, "lse": 3}
+    TREK_MODE = {"off": 0, "log": 1, "opt": 2}
+
+    def set_trek(self, pairs, seq: str = "exp", *, agg: str = "mean", mode: str = "opt", weight: float = 0.0,
+                 eps_inv: float = 1e-8, K_log: int | None = None):
+        """The PST trek regularizer (notreks.pst) inside the loop; mode 'off' or no pairs disables it."""
+        P = np.ascontiguousarray(np.asarray(pairs, dtype=np.int64).reshape(-1, 2)) if pairs is not None \
+            else np.zeros((0, 2), dtype=np.int64)
+        seq, agg, mode = seq.lower().strip(), agg.lower().strip(), mode.lower().strip()
+        if seq not in self.TREK_SEQ or agg not in self.TREK_AGG or mode not in self.TREK_MODE:
+            raise ValueError(f"unsupported PST configuration seq={seq!r} agg={agg!r} mode={mode!r}")
+        K = 2 * self.d if K_log is None else int(K_log)
+        check(self.L.midagma_set_trek(self.h, self.TREK_SEQ[seq], self.TREK_AGG[agg], self.TREK_MODE[mode],
+                                      float(weight), float(eps_inv), K, P.ctypes.data_as(C.POINTER(C.c_int64)),
+                                      int(P.shape[0])), self.h, "set_trek")
+
+    def trek_value(self, W: np.ndarray, grad: bool = True):
+        """notreks.trek_value_grad(W, tr) for the configured regularizer: (value, grad or None)."""
+        W = _as_f64(W)
+        v = C.c_double()
+        G = np.empty((self.d, self.d)) if grad else None
+        check(self.L.midagma_trek(self.h, dptr(W), C.byref(v), dptr(G)), self.h, "trek")
+        return float(v.value), G
+
     def set_data(self, X, n_global: int | None = None):
         """X: host ndarray (n_local x d) or a torch CUDA tensor (copied)."""
         if hasattr(X, "data_ptr"):

@@ -1,0 +1,114 @@
+"""PST trek regularizer on the GPU (csrc/trek.hip) vs the reference's trek_value_grad
+(fixtures) and the oracle, standalone and inside the minimize loop (linear.py:251-258)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from midagma_amd.simulate import make_dataset  # noqa: E402
+from oracle.dagma_oracle import LinearOracle  # noqa: E402
+from oracle.trek_oracle import pst_value_grad  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from midagma_amd import _lib
+    _lib.load()
+    return _lib
+
+
+def _solver(d, cov=None):
+    from midagma_amd.solver import HipSolver
+    s = HipSolver(d, "l2", "cov", device=0)
+    if cov is not None:
+        s.set_cov(cov)
+    return s
+
+
+@pytest.mark.parametrize("seq", ["exp", "inv", "log", "binom"])
+@pytest.mark.parametrize("agg", ["mean", "sum", "max", "lse"])
+@pytest.mark.parametrize("d", [8, 20])
+def test_trek_value_grad_matches_reference(hip, golden, seq, agg, d):
+    f = golden("trek_pst.npz")
+    W, pairs = f[f"W_d{d}"], f[f"pairs_d{d}"]
+    s = _solver(d, np.eye(d))
+    s.set_trek(pairs, seq, agg=agg, mode="opt", weight=0.5, K_log=12 if seq == "log" else None)
+    v, g = s.trek_value(W)
+    v_ref, g_ref = float(f[f"val_{seq}_{agg}_d{d}"]), f[f"grad_{seq}_{agg}_d{d}"]
+    assert abs(v - v_ref) <= 1e-11 * max(1.0, abs(v_ref))
+    assert np.abs(g - g_ref).max() <= 1e-10 * max(1.0, np.abs(g_ref).max())
+
+
+@pytest.mark.parametrize("seq", ["exp", "inv", "log"])
+def test_trek_large_d_matches_oracle(hip, seq):
+    """d=300 (D=384): split-K GEMMs, several squarings for exp, dense pair list."""
+    d = 300
+    rng = np.random.default_rng(3)
+    W = (rng.uniform(-1, 1, (d, d)) * (rng.uniform(size=(d, d)) < 3.0 / d)) * 0.6
+    np.fill_diagonal(W, 0)
+    iu = np.array(np.triu_indices(d, 1)).T
+    pairs = iu[rng.uniform(size=len(iu)) < 0.2]
+    s = _solver(d, np.eye(d))
+    s.set_trek(pairs, seq, agg="mean", mode="opt", weight=1.0, K_log=20 if seq == "log" else None)
+    v, g = s.trek_value(W)
+    v_ref, g_ref = pst_value_grad(W, pairs, seq, K_log=20 if seq == "log" else None)
+    assert abs(v - v_ref) <= 1e-10 * abs(v_ref)
+    assert np.abs(g - g_ref).max() <= 1e-9 * np.abs(g_ref).max()
+
+
+def _trek_case(d, seed):
+    X, _, _ = make_dataset(d, 2 * d if d > 20 else 1000, seed=seed)
+    rng = np.random.default_rng(seed)
+    iu = np.array(np.triu_indices(d, 1)).T
+    return X, iu[rng.uniform(size=len(iu)) < 0.3]
+
+
+@pytest.mark.parametrize("d,seq,mode", [(20, "exp", "opt"), (20, "inv", "opt"), (20, "log", "log"),
+                                        (300, "exp", "opt")])
+def test_minimize_with_trek_matches_oracle(hip, d, seq, mode):
+    """The loop with the regularizer: W, checkpoint objective (+ weight * value in 'opt'),
+    reg_trek_value and grad_trek_norm of the records.  d=300 runs the blocked fast path."""
+    X, pairs = _trek_case(d, 5)
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 40)
+    o.trek = dict(pairs=pairs, seq=seq, agg="mean", mode=mode, weight=0.2, K_log=10)
+    K = 90 if d == 20 else 50
+    s = _solver(d, o.cov)
+    s.set_trek(pairs, seq, agg="mean", mode=mode, weight=0.2, K_log=10)
+    W = np.zeros((d, d))
+    res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=40, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert res.iters == tr.iters == K
+    assert np.abs(W - Wr).max() <= 1e-9
+    assert [c.iter for c in res.checkpoints] == [r["iter"] for r in tr.records]
+    for c, r in zip(res.checkpoints, tr.records):
+        assert abs(c.obj - r["obj_total"]) <= 1e-10 * abs(r["obj_total"])
+        # small values (H entries of F ~ I + W o W): absolute floor for the summation-order noise
+        assert abs(c.reg_trek_value - r["reg_trek_value"]) <= 1e-9 * abs(r["reg_trek_value"]) + 1e-13
+        assert abs(c.grad_trek_norm - r["grad_trek_norm"]) <= 1e-9 * r["grad_trek_norm"] + 1e-13
+    if mode == "log":
+        assert all(c.grad_trek_norm == 0.0 for c in res.checkpoints)
+
+
+def test_dagma_linear_pst_fit_runs(hip):
+    """DagmaLinear(trek_reg=PSTRegularizer-like) configures the GPU regularizer; TCC raises."""
+    from types import SimpleNamespace
+    from midagma_amd import DagmaLinear
+    X, pairs = _trek_case(20, 7)
+
+    def reg(name, mode="opt"):
+        return SimpleNamespace(name=name, mode=mode, weight=0.1, cfg={"I": pairs, "seq": "exp", "kwargs": {}},
+                               enabled=lambda: True)
+
+    m = DagmaLinear("l2", trek_reg=reg("pst"))
+    W = m.fit(X, lambda1=0.03, T=2, warm_iter=200, max_iter=300)
+    assert W.shape == (20, 20)
+    Wr = np.random.default_rng(0).uniform(-0.3, 0.3, (20, 20))
+    np.fill_diagonal(Wr, 0)
+    obj, sc, h, tv = m._func(Wr, 0.1, 0.9)
+    v_ref, _ = pst_value_grad(Wr, pairs, "exp", grad=False)
+    assert abs(tv - v_ref) <= 1e-11 * v_ref
+    with pytest.raises(NotImplementedError):
+        DagmaLinear("l2", trek_reg=reg("tcc"))
