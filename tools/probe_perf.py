@@ -53,6 +53,25 @@ def data_case(d, n, warm, K, loss="l2"):
     s.close()
 
 
+def trek_case(d, seq, K):
+    X, _, _ = make_dataset(d, 2 * d, seed=0)
+    X -= X.mean(0)
+    s = HipSolver(d, "l2", "cov")
+    s.set_cov(X.T @ X / X.shape[0])
+    rng = np.random.default_rng(0)
+    iu = np.array(np.triu_indices(d, 1)).T
+    s.set_trek(iu[rng.uniform(size=len(iu)) < 0.3], seq, agg="mean", mode="opt", weight=0.1, K_log=20)
+    s.begin(np.zeros((d, d)), 1.0, K + 1000, 1.0, 3e-4, tol=-1.0)
+    s.run_slots(3)
+    s.sync()
+    t0 = time.perf_counter()
+    s.run_slots(K)
+    s.sync()
+    dt = time.perf_counter() - t0
+    print(f"cov+PST-{seq} d={d}: {K / dt:.1f} steps/s ({dt / K * 1e3:.3f} ms/step)", flush=True)
+    s.close()
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "small"):
@@ -62,5 +81,8 @@ if __name__ == "__main__":
         cov_case(1000, 2000, 10, 300)
     if which in ("all", "d5000"):
         cov_case(5000, 6000, 2, 10)
+    if which == "trek":
+        for seq in ("exp", "inv", "log"):
+            trek_case(1000, seq, 50)
     if which in ("all", "data"):
         data_case(1000, 100000, 2, 10)
