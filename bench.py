@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--no-cov", action="store_true")
     p.add_argument("--profile-reps", type=int, default=3)
     p.add_argument("--no-fit", action="store_true", help="skip the full-fit wall-clock leg (config 2)")
+    p.add_argument("--no-data", action="store_true", help="skip the data-mode leg (profiling the other legs)")
     p.add_argument("--no-large", action="store_true", help="skip the config 3 leg (d=5000, n=5e4, cov mode)")
     p.add_argument("--large-d", type=int, default=5000)
     p.add_argument("--large-n", type=int, default=50_000)
@@ -360,7 +361,7 @@ def main():
     args = parse()
     import torch
     world, rank, local = setup_dist(args)
-    res = bench_data(args, world, rank, local) if args.workload == "data" else None
+    res = bench_data(args, world, rank, local) if args.workload == "data" and not args.no_data else None
     cov_res = None
     if rank == 0 and (args.workload == "cov" or (world == 1 and not args.no_cov)):
         cov_res = bench_cov(args, local)
@@ -373,6 +374,10 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and cov_res is not None:
         cpu = cpu_baseline(args, cov_res["cov"])
+    if rank == 0 and res is None and cov_res is None:   # --no-data --no-cov: a profiling run of the other legs
+        out = {k: v for k, v in (large_res or {}).items() if k != "cov"}
+        print(json.dumps({"config3": out, "full_fit": fit_res}), flush=True)
+        return
     if rank == 0:
         d = args.d
         if args.workload == "data":
