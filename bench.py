@@ -74,20 +74,23 @@ def setup_dist(args):
 
 
 def make_shard(d, n, world, rank, seed, device):
-    """Rows of an ER(s0=d) linear-Gaussian SEM, generated on the GPU: X = E (I - W)^-1."""
+    """This rank's rows of an ER(s0=d) linear-Gaussian SEM, generated on the GPU by the
+    library's SEM generator (csrc/sem.hip, counter-based noise: the shard is exactly the
+    rank's rows of the unsharded X).  Returns (X, n_k, generation seconds)."""
     import torch
     from midagma_amd.simulate import simulate_er_dag, simulate_weights
+    from midagma_amd.utils import simulate_linear_sem_gpu
     rng = np.random.default_rng(seed)
     W_true = simulate_weights(simulate_er_dag(d, d, rng), rng)
-    Binv = torch.from_numpy(np.linalg.inv(np.eye(d) - W_true)).to(device)
     base, extra = divmod(n, world)
     n_k = base + (1 if rank < extra else 0)
-    g = torch.Generator(device=device)
-    g.manual_seed(seed * 1000003 + rank)
-    E = torch.randn(n_k, d, dtype=torch.float64, device=device, generator=g)
-    X = E @ Binv
-    del E
-    return X, n_k
+    row0 = rank * base + min(rank, extra)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    X = simulate_linear_sem_gpu(W_true, n, "gauss", seed=seed * 1000003 + 17, device=device.index
+                                if hasattr(device, "index") else device, row0=row0, n_rows=n_k)
+    torch.cuda.synchronize(device)
+    return X, n_k, time.perf_counter() - t0
 
 
 def allreduce_(t, op=None):
@@ -103,7 +106,7 @@ def bench_data(args, world, rank, local):
     from midagma_amd.solver import HipSolver
     dev = torch.device("cuda", local)
     d, n = args.d, args.n
-    X, n_k = make_shard(d, n, world, rank, args.seed, dev)
+    X, n_k, t_gen = make_shard(d, n, world, rank, args.seed, dev)
     colsum = allreduce_(X.sum(0))
     X -= colsum / n                      # l2 centers X with the global mean (linear.py:411)
     torch.cuda.synchronize()
@@ -152,7 +155,7 @@ def bench_data(args, world, rank, local):
     ok = (r.status == 0 and r.iters == Wm + K)
     prof = s.profile_parts(args.profile_reps) if rank == 0 else {}
     out = dict(ms_per_step=elapsed / K * 1e3, value=K / elapsed, verified_iters=int(r.iters), verified=ok,
-               n_local=n_k, prof=prof, D=s.D)
+               n_local=n_k, prof=prof, D=s.D, sem_gen_s=t_gen)
     s.close()
     return out
 
@@ -189,7 +192,7 @@ def bench_cov_large(args, device):
     from midagma_amd.solver import HipSolver
     d, n = args.large_d, args.large_n
     dev = torch.device("cuda", device)
-    X, _ = make_shard(d, n, 1, 0, args.seed, dev)
+    X, _, _ = make_shard(d, n, 1, 0, args.seed, dev)
     X -= X.mean(dim=0, keepdim=True)
     cov = (X.T @ X / float(n)).cpu().numpy()
     del X
@@ -380,6 +383,7 @@ def main():
         return
     if rank == 0:
         d = args.d
+        sem_gen = None
         if args.workload == "data":
             prof = res["prof"]
             n_k = res["n_local"]
@@ -400,6 +404,11 @@ def main():
                     "algorithmic_per_launch": f"2*n_k*d^2 = {gemm_flops:.3e} flop",
                     "kernel_ms": {k: round(v, 4) for k, v in prof.items()}}
             verified = res["verified"]
+            t_gen = res["sem_gen_s"]
+            sem_gen = {"what": "X shard generation on the GPU (csrc/sem.hip: Philox noise, structural equations "
+                               "level by level, slab transpose), one cold call", "rows": n_k, "d": d,
+                       "seconds": t_gen, "output_GB_per_s": 8.0 * n_k * d / t_gen / 1e9,
+                       "frac_hbm_peak_output_bytes": 8.0 * n_k * d / t_gen / 8.0e12}
         else:
             value, ms = cov_res["value"], cov_res["ms_per_step"]
             metric = "Adam steps/s, d=1000 linear DAGMA (l2, cov mode)"
@@ -414,6 +423,8 @@ def main():
                 "verified": verified}
         if roof is not None:
             line["roofline"] = roof
+        if sem_gen is not None:
+            line["sem_generator"] = sem_gen
         if cov_res is not None:
             p = cov_res["prof"]
             F = 4.0 * d ** 3

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 3
+#define MIDAGMA_ABI_VERSION 4
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -151,6 +151,17 @@ int midagma_score_finish(midagma_solver* s, double* loss, double* G);
  * Enqueued on `stream`, no host synchronization. */
 int midagma_logdet_inv_dev(const double* A, int64_t d, int64_t lda, double s_dom, double* logdet_dev,
                            double* Mt_dev, int64_t ldm, void* stream);
+
+/* Linear-SEM samples on the GPU (replaces utils.simulate_linear_sem, utils.py:99-172):
+ * rows [row0, row0 + n_rows) of X (row-major, ld = ldx >= d, device memory) for the weighted
+ * DAG W (host, d x d row-major, W[p, j] = weight of edge p -> j):
+ *   x_j = sum_{p in pa(j)} W[p, j] x_p + z_j   (sem_type 0 gauss, 1 exp, 2 gumbel, 3 uniform)
+ *   x_j ~ Bernoulli(sigmoid(.)) (4 logistic),  x_j ~ Poisson(exp(.)) (5 poisson).
+ * Noise: Philox4x32-10 keyed by `seed`, counter (row / 2, node, draw) -- row r's values are the
+ * same whatever row0 / n_rows split generated it.  noise_scale: d scales or NULL (ones).
+ * MIDAGMA_E_ARG if W has a cycle.  Enqueued on `stream`; returns after the rows are written. */
+int midagma_sem_linear(const double* W, int64_t d, int64_t row0, int64_t n_rows, int sem_type,
+                       const double* noise_scale, uint64_t seed, double* X_dev, int64_t ldx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,7 @@ EXPORTED = {
     "midagma_score_partial": (_int, [_vp, _dp]),
     "midagma_score_finish": (_int, [_vp, _dp, _dp]),
     "midagma_logdet_inv_dev": (_int, [_vp, _i64, _i64, _d, _vp, _vp, _i64, _vp]),
+    "midagma_sem_linear": (_int, [_dp, _i64, _i64, _i64, _int, _dp, C.c_uint64, _vp, _i64, _vp]),
 }
 
 _lock = threading.Lock()

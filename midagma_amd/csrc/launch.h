@@ -4,6 +4,7 @@
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "common.h"
 
@@ -88,6 +89,25 @@ struct TrekWork {
 // runs nothing).
 void launch_trek_pst(const double* W, int64_t d, int64_t D, const TrekCfg& cfg, const TrekWork& w, const State* st,
                      double* Gtrek, hipStream_t stream);
+
+// --- sem.hip ----------------------------------------------------------------
+// Parents (CSR over columns of W, ascending) and topological levels of a weighted DAG.
+struct SemGraph {
+  std::vector<int32_t> pptr, pidx, nodes, level_off;
+  std::vector<double> pw;
+};
+struct SemDev {  // device copies of SemGraph (+ per-node noise scales)
+  const int32_t *nodes, *pptr, *pidx;
+  const double *pw, *scale;
+};
+// false if W (host, d x d row-major, W[p, j] = edge p -> j) has a cycle
+bool sem_levels(const double* W, int64_t d, SemGraph& g);
+// Rows [row0, row0 + rows) of the linear SEM (row0 even) into the node-major slab XT (ldt even),
+// then rows [skip, rows) of it to X (row-major, ldx).  sem: 0 gauss 1 exp 2 gumbel 3 uniform
+// 4 logistic 5 poisson.
+void launch_sem_slab(const SemDev& g, const std::vector<int32_t>& level_off, int64_t d, int sem, uint64_t seed,
+                     int64_t row0, int64_t rows, int64_t skip, double* XT, int64_t ldt, double* X, int64_t ldx,
+                     hipStream_t stream);
 
 // --- gemm.hip ---------------------------------------------------------------
 enum GemmB : int { B_PLAIN = 0, B_IMINUS = 1 };

@@ -1141,3 +1141,61 @@ extern "C" int midagma_logdet_inv_dev(const double* A, int64_t d, int64_t lda, d
     return MIDAGMA_OK;
   });
 }
+
+// ---------------------------------------------------------------------------
+// Linear-SEM generator (sem.hip; utils.py:99-172)
+extern "C" int midagma_sem_linear(const double* W, int64_t d, int64_t row0, int64_t n_rows, int sem_type,
+                                  const double* noise_scale, uint64_t seed, double* X_dev, int64_t ldx,
+                                  void* stream) {
+  if (!W || d < 1 || d > (1 << 30)) return fail(nullptr, MIDAGMA_E_ARG, "sem_linear: bad W / d");
+  SemGraph g;
+  if (!sem_levels(W, d, g)) return fail(nullptr, MIDAGMA_E_ARG, "sem_linear: W must be a DAG");
+  if (row0 < 0 || n_rows < 0 || ldx < d || sem_type < 0 || sem_type > 5 || (n_rows > 0 && !X_dev))
+    return fail(nullptr, MIDAGMA_E_ARG, "sem_linear: bad arguments");
+  if (n_rows == 0) return MIDAGMA_OK;
+  return guarded(nullptr, [&] {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    std::vector<double> scale(d, 1.0);
+    if (noise_scale) std::copy(noise_scale, noise_scale + d, scale.begin());
+    // slab: rows of the node-major scratch, even, ~MIDAGMA_SEM_SLAB_MB (default 2048) MB
+    int64_t budget = 2048;
+    if (const char* e = getenv("MIDAGMA_SEM_SLAB_MB")) budget = std::max<int64_t>(1, atoll(e));
+    const int64_t first = row0 & ~int64_t(1), end = row0 + n_rows;
+    int64_t S = std::max<int64_t>(1024, (budget << 20) / (8 * d));
+    S = std::min<int64_t>(S, (end - first + 1) & ~int64_t(1));
+    S = (S + 1) & ~int64_t(1);
+    const size_t nnz = g.pidx.size();
+    struct Raw {
+      void* p = nullptr;
+      ~Raw() {
+        if (p) (void)hipFree(p);
+      }
+    } ints, dbls, xt;
+    const size_t n_int = g.nodes.size() + g.pptr.size() + std::max<size_t>(nnz, 1);
+    HIP_TRY(hipMalloc(&ints.p, n_int * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&dbls.p, (std::max<size_t>(nnz, 1) + d) * sizeof(double)));
+    HIP_TRY(hipMalloc(&xt.p, static_cast<size_t>(S) * d * sizeof(double)));
+    int32_t* ip = static_cast<int32_t*>(ints.p);
+    double* dp = static_cast<double*>(dbls.p);
+    SemDev dev{ip, ip + g.nodes.size(), ip + g.nodes.size() + g.pptr.size(), dp, dp + std::max<size_t>(nnz, 1)};
+    HIP_TRY(hipMemcpyAsync(ip, g.nodes.data(), g.nodes.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ip + g.nodes.size(), g.pptr.data(), g.pptr.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice, st));
+    if (nnz) {
+      HIP_TRY(hipMemcpyAsync(const_cast<int32_t*>(dev.pidx), g.pidx.data(), nnz * sizeof(int32_t),
+                             hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(dp, g.pw.data(), nnz * sizeof(double), hipMemcpyHostToDevice, st));
+    }
+    HIP_TRY(hipMemcpyAsync(const_cast<double*>(dev.scale), scale.data(), d * sizeof(double), hipMemcpyHostToDevice,
+                           st));
+    for (int64_t a = first; a < end; a += S) {
+      const int64_t rows = std::min<int64_t>(S, end - a);
+      const int64_t skip = a < row0 ? row0 - a : 0;
+      launch_sem_slab(dev, g.level_off, d, sem_type, seed, a, rows, skip, static_cast<double*>(xt.p), S,
+                      X_dev + (a + skip - row0) * ldx, ldx, st);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));  // the scratch is freed on return
+    return MIDAGMA_OK;
+  });
+}
