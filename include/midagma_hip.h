@@ -134,6 +134,11 @@ int64_t midagma_checkpoints(midagma_solver* s, midagma_ckpt* out, int64_t cap);
  * terms (binom: ignored, the exponent is d as in the reference); pairs: m (i, j) int64. */
 int midagma_set_trek(midagma_solver* s, int seq, int agg, int mode, double weight, double eps_inv, int64_t K,
                      const int64_t* pairs, int64_t m);
+/* The TCC trek regularizer (notreks.py:291-395 as trek_value_grad:667-706 calls it in the loop:
+ * spectral penalty, 'approx_trek_graph', Perron pairs) inside the loop; mode as above; w: the
+ * multiplier of the pair indicator S; eps: the reference's stabiliser (1e-12). */
+int midagma_set_trek_tcc(midagma_solver* s, int mode, double weight, double w, double eps, const int64_t* pairs,
+                         int64_t m);
 /* trek_value_grad(W, tr) (notreks.py): value and, in 'opt' mode, the gradient (G nullable, d x d;
  * zeros in 'log' mode, as the reference returns). */
 int midagma_trek(midagma_solver* s, const double* W, double* value, double* G);

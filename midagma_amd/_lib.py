@@ -79,6 +79,7 @@ EXPORTED = {
     "midagma_end": (_int, [_vp, _dp, C.POINTER(MidagmaResult)]),
     "midagma_checkpoints": (_i64, [_vp, C.POINTER(MidagmaCkpt), _i64]),
     "midagma_set_trek": (_int, [_vp, _int, _int, _int, _d, _d, _i64, C.POINTER(_i64), _i64]),
+    "midagma_set_trek_tcc": (_int, [_vp, _int, _d, _d, _d, C.POINTER(_i64), _i64]),
     "midagma_trek": (_int, [_vp, _dp, _dp, _dp]),
     "midagma_h": (_int, [_vp, _dp, _d, _dp, _dp]),
     "midagma_score": (_int, [_vp, _dp, _dp, _dp]),

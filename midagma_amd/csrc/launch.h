@@ -90,6 +90,29 @@ struct TrekWork {
 void launch_trek_pst(const double* W, int64_t d, int64_t D, const TrekCfg& cfg, const TrekWork& w, const State* st,
                      double* Gtrek, hipStream_t stream);
 
+// --- tcc.hip ----------------------------------------------------------------
+constexpr int TCC_NODA_MAX = 24;     // Noda steps per slot (gated off once converged)
+struct TccCfg {
+  int mode;              // 1 'log', 2 'opt' (as TrekCfg)
+  double weight, w, eps; // regularizer weight, multiplier of S, the reference's eps
+  int64_t m;             // pairs
+};
+struct TccWork {
+  GJWork gj;             // sized for D2
+  int64_t D2;            // round_up64(2 d)
+  double *A, *Mi;        // D2 x D2: the block matrix, the shifted inverse
+  double* S;             // D x D pair indicator
+  double *x, *y, *u, *z, *vprev, *uprev;  // D2 vectors
+  double* part;          // ceil(2d / 64) x D2 transposed-GEMV partials
+  double* scal;          // [0] value [1] sigma [2] lower [3] rho [4] u.v+eps [5] u.u+eps [7] breakdown [8] warm
+                         // [9] converged
+  State* gates;          // 1 + TCC_NODA_MAX gate words
+};
+// The TCC penalty of W (value in w.scal[0]) and, in 'opt' mode, weight * d value / d W into
+// Gtrek (D x D), gated like launch_trek_pst.
+void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, const TccWork& w, const State* st,
+                     double* Gtrek, hipStream_t stream);
+
 // --- sem.hip ----------------------------------------------------------------
 // Parents (CSR over columns of W, ascending) and topological levels of a weighted DAG.
 struct SemGraph {

@@ -58,6 +58,12 @@ struct midagma_solver {
   State* tgates = nullptr;
   State* d_state_probe = nullptr;  // RUNNING + checkpoint: gates the API-call (midagma_trek) path
   TrekWork tw{};
+  // TCC trek regularizer (tcc.hip): trek_tcc selects it; mode / weight live in tcfg as for PST
+  bool trek_tcc = false;
+  TccCfg ccfg{};
+  TccWork cw{};
+  DevBuf cA, cMi, cS, cvec, cpart, cP, cR, cC;
+  State* cgates = nullptr;
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
   DevBuf Malt, Pst2, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone;
@@ -97,7 +103,8 @@ struct midagma_solver {
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart})
       b->release();
     for (DevBuf& b : tbufs) b.release();
-    for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices}) b->release();
+    for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices, &cA, &cMi, &cS, &cvec, &cpart, &cP, &cR, &cC}) b->release();
+    if (cgates) (void)hipFree(cgates);
     if (tgates) (void)hipFree(tgates);
     if (d_state_probe) (void)hipFree(d_state_probe);
     if (d_params) (void)hipFree(d_params);
@@ -152,8 +159,12 @@ struct midagma_solver {
     }
     // trek regularizer of this slot's W (linear.py:251-258): every slot in 'opt' mode; in 'log'
     // mode only checkpoint slots, which are never fast slots
-    if (trek_on && (tcfg.mode == 2 || !(fast && blocked())))
-      launch_trek_pst(W.p, d, D, tcfg, tw, d_state, Gtrek.p, stream);
+    if (trek_on && (tcfg.mode == 2 || !(fast && blocked()))) {
+      if (trek_tcc)
+        launch_trek_tcc(W.p, d, D, ccfg, cw, d_state, Gtrek.p, stream);
+      else
+        launch_trek_pst(W.p, d, D, tcfg, tw, d_state, Gtrek.p, stream);
+    }
   }
 
   // out = Cm @ (I - Wp) on the d x d problem; split-K over fixed slices when the tile grid
@@ -192,7 +203,7 @@ struct midagma_solver {
     const bool lean = fast && blocked();
     if (!lean) launch_reduce_check(Mt.p, W.p, zbuf, d_params, d_state, partials.p, d, D, stream);
     launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
-                   trek_on ? tw.scal : nullptr, stream);
+                   trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream);
     const bool slices = lean && cov_split > 1;
     launch_fused_update(d_params, d_state, W.p, m.p, v.p, g.p, Mt.p, slices ? cov_parts.p : zbuf,
                         slices ? cov_split : 1, D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr,
@@ -288,6 +299,12 @@ struct midagma_solver {
     tcfg = c;
     tw = w;
     trek_on = true;
+    trek_tcc = false;
+    ensure_probe();
+    graphs_valid = false;
+  }
+
+  void ensure_probe() {
     if (!d_state_probe) {
       HIP_TRY(hipMalloc(&d_state_probe, sizeof(State)));
       State probe{};
@@ -295,6 +312,61 @@ struct midagma_solver {
       probe.ckpt_pending = 1;
       HIP_TRY(hipMemcpy(d_state_probe, &probe, sizeof(State), hipMemcpyHostToDevice));
     }
+  }
+
+  // TCC (notreks TCCRegularizer as trek_value_grad runs it): w multiplies S, eps as the reference
+  void set_trek_tcc(int tmode, double weight, double wS, double eps, const int64_t* pairs, int64_t mpairs) {
+    if (tmode == 0 || mpairs <= 0 || weight == 0.0) {
+      trek_on = false;
+      graphs_valid = false;
+      return;
+    }
+    if (tmode < 1 || tmode > 2) throw std::invalid_argument("set_trek_tcc: bad mode");
+    std::vector<double> S((size_t)D * D, 0.0);
+    for (int64_t k = 0; k < mpairs; ++k) {
+      const int64_t i = pairs[2 * k], j = pairs[2 * k + 1];
+      if (i < 0 || i >= d || j < 0 || j >= d) throw std::invalid_argument("set_trek_tcc: pair index out of range");
+      S[(size_t)i * D + j] = 1.0;  // S[rows, cols] = 1 (notreks _indicator_from_pairs)
+    }
+    const int64_t D2 = round_up64(2 * d);
+    const int64_t nch = (2 * d + 63) / 64;
+    cA.alloc((size_t)D2 * D2);
+    cMi.alloc((size_t)D2 * D2);
+    cS.alloc((size_t)D * D);
+    cvec.alloc((size_t)6 * D2 + 16);
+    cpart.alloc((size_t)nch * D2);
+    cP.alloc(2 * 32 * 32);
+    cR.alloc((size_t)2 * 32 * D2);
+    cC.alloc((size_t)2 * D2 * 32);
+    HIP_TRY(hipMemcpy(cS.p, S.data(), S.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(cvec.p, 0, cvec.n * sizeof(double)));  // warm flag off, vectors 0
+    if (!cgates) HIP_TRY(hipMalloc(&cgates, (1 + TCC_NODA_MAX) * sizeof(State)));
+    HIP_TRY(hipMemset(cgates, 0, (1 + TCC_NODA_MAX) * sizeof(State)));
+    TccWork w{};
+    w.gj = GJWork{cP.p, cR.p, cC.p, nullptr, nullptr};
+    w.D2 = D2;
+    w.A = cA.p;
+    w.Mi = cMi.p;
+    w.S = cS.p;
+    double* v = cvec.p;
+    for (double** slot : {&w.x, &w.y, &w.u, &w.z, &w.vprev, &w.uprev}) {
+      *slot = v;
+      v += D2;
+    }
+    w.scal = v;
+    w.part = cpart.p;
+    w.gates = cgates;
+    cw = w;
+    ccfg = TccCfg{tmode, weight, wS, eps, mpairs};
+    Gtrek.alloc((size_t)D * D);
+    HIP_TRY(hipMemset(Gtrek.p, 0, (size_t)D * D * sizeof(double)));
+    tcfg = TrekCfg{};
+    tcfg.mode = tmode;
+    tcfg.weight = weight;
+    tcfg.m = mpairs;
+    trek_on = true;
+    trek_tcc = true;
+    ensure_probe();
     graphs_valid = false;
   }
 
@@ -947,6 +1019,16 @@ int midagma_set_trek(midagma_solver* s, int seq, int agg, int mode, double weigh
   });
 }
 
+int midagma_set_trek_tcc(midagma_solver* s, int mode, double weight, double w, double eps, const int64_t* pairs,
+                         int64_t m) {
+  if (!s || (m > 0 && !pairs) || m < 0) return fail(s, MIDAGMA_E_ARG, "set_trek_tcc: bad arguments");
+  return guarded(s, [&] {
+    s->set_trek_tcc(mode, weight, w, eps, pairs, m);
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
 int midagma_trek(midagma_solver* s, const double* W, double* value, double* G) {
   if (!s || !W || !value) return fail(s, MIDAGMA_E_ARG, "trek: null argument");
   return guarded(s, [&] {
@@ -959,12 +1041,21 @@ int midagma_trek(midagma_solver* s, const double* W, double* value, double* G) {
     s->scratch.alloc(DD);
     HIP_TRY(hipMemsetAsync(s->scratch.p, 0, DD * sizeof(double), s->stream));
     s->upload_matrix(s->scratch, W, d);
-    TrekCfg c = s->tcfg;
-    c.weight = 1.0;  // the bare gradient, as trek_value_grad returns it
-    launch_trek_pst(s->scratch.p, d, D, c, s->tw, s->d_state_probe, s->Gtrek.p, s->stream);
-    HIP_TRY(hipMemcpyAsync(value, s->tw.scal, sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    const double* scal;
+    if (s->trek_tcc) {
+      TccCfg c = s->ccfg;
+      c.weight = 1.0;  // the bare gradient, as trek_value_grad returns it
+      launch_trek_tcc(s->scratch.p, d, D, c, s->cw, s->d_state_probe, s->Gtrek.p, s->stream);
+      scal = s->cw.scal;
+    } else {
+      TrekCfg c = s->tcfg;
+      c.weight = 1.0;
+      launch_trek_pst(s->scratch.p, d, D, c, s->tw, s->d_state_probe, s->Gtrek.p, s->stream);
+      scal = s->tw.scal;
+    }
+    HIP_TRY(hipMemcpyAsync(value, scal, sizeof(double), hipMemcpyDeviceToHost, s->stream));
     if (G) {
-      if (c.mode == 2) {
+      if (s->tcfg.mode == 2) {
         HIP_TRY(hipMemcpy2DAsync(G, d * sizeof(double), s->Gtrek.p, D * sizeof(double), d * sizeof(double), d,
                                  hipMemcpyDeviceToHost, s->stream));
       } else {

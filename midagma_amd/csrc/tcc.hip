@@ -1,0 +1,364 @@
+// TCC trek regularizer on the GPU (fbleile/midagma src/notreks/notreks.py:
+// trek_cycle_coupling_value_gradW as trek_value_grad calls it inside the loop, i.e. with its
+// defaults: spectral penalty, version 'approx_trek_graph', Perron pairs of eig_numpy):
+//
+//     W2 = W o W,  A = [[W2, w S], [I, W2^T]]  (2d x 2d, nonnegative),  B = A without w S
+//     rho, v, u  = Perron root, right / left Perron vectors of A (unit, positive sum)
+//     value = (rho - u^T B u / (u^T u + eps)) / m
+//     grad  = (2W o (G11 + G22^T) - 2W o (u1 u1^T + u2 u2^T) / (u^T u + eps)) / m,
+//             G = u v^T / (u^T v + eps)
+//
+// The reference takes the Perron pair from two dense non-symmetric eigendecompositions.  Here
+// it comes from Noda's iteration (T. Noda, Numer. Math. 17 (1971)), which needs nothing but
+// the M-matrix inverse the log-det already has:
+//     sigma_0 = max_i (A x)_i / x_i  (Collatz-Wielandt upper bound, x > 0),
+//     (sigma_k I - A) y = x_k,  x_{k+1} = y / |y|,  sigma_{k+1} = sigma_k - min_i x_{k,i} / y_i
+// sigma_k decreases to rho from above (so sigma_k I - A stays a nonsingular M-matrix and the
+// unpivoted Gauss-Jordan of gj.hip applies), quadratically once close; sigma_k - max_i x/y is
+// a lower bound, and the iteration stops when the two bounds agree to 1e-13 (or the upper one
+// stalls: reducible A).  The iterate of the previous slot is the warm start, so a slot usually
+// takes 2-3 inverses; a cold start from ones can take up to ~16 (small W).  A final inverse
+// at the converged shift gives v and (its transpose) u by two inverse-iteration sweeps each;
+// rho is the two-sided Rayleigh quotient u^T A v / u^T v.
+//
+// Every kernel obeys a gate word: gate 0 (this slot runs: every slot in 'opt' mode,
+// checkpoint slots in 'log' mode), gates 1..TCC_NODA_MAX (Noda step k runs; the update kernel
+// turns the later ones off on convergence), so the sequence is graph-capturable.
+#include <cmath>
+
+#include "launch.h"
+
+namespace midagma {
+
+namespace {
+
+constexpr int EB = NTHREADS;
+
+__device__ __forceinline__ bool gate_on(const State* g) { return g->status == ST_RUNNING; }
+
+// one-workgroup sum / min / max (fixed order: strided partials, then a tree)
+template <class Op>
+__device__ double wg_reduce(double v, double* sh, Op op) {
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = EB / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sh[threadIdx.x] = op(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  const double r = sh[0];
+  __syncthreads();
+  return r;
+}
+struct Add {
+  __device__ double operator()(double a, double b) const { return a + b; }
+};
+struct Min {
+  __device__ double operator()(double a, double b) const { return fmin(a, b); }
+};
+struct Max {
+  __device__ double operator()(double a, double b) const { return fmax(a, b); }
+};
+
+__global__ void tcc_gate_kernel(const State* __restrict__ st, int mode, State* __restrict__ gates, int nmax) {
+  if (threadIdx.x != 0) return;
+  const bool on = st->status == ST_RUNNING && (mode == 2 || st->ckpt_pending);
+  for (int t = 0; t <= nmax; ++t) gates[t].status = on ? ST_RUNNING : ST_DONE;
+}
+
+// A = [[W o W, w S], [I, (W o W)^T]] on the logical 2d x 2d block, zero padding (D2 x D2)
+__global__ void tcc_build_kernel(const double* __restrict__ W, const double* __restrict__ S, double ws, int64_t d,
+                                 int64_t D, int64_t D2, double* __restrict__ A, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  const int64_t n = D2 * D2;
+  for (int64_t e = (int64_t)blockIdx.x * EB + threadIdx.x; e < n; e += (int64_t)gridDim.x * EB) {
+    const int64_t i = e / D2, j = e - i * D2;
+    double a = 0.0;
+    if (i < d) {
+      if (j < d) {
+        const double x = W[i * D + j];
+        a = x * x;
+      } else if (j < 2 * d) {
+        a = ws * S[i * D + (j - d)];
+      }
+    } else if (i < 2 * d) {
+      if (j < d) {
+        a = (i - d == j) ? 1.0 : 0.0;
+      } else if (j < 2 * d) {
+        const double x = W[(j - d) * D + (i - d)];
+        a = x * x;
+      }
+    }
+    A[e] = a;
+  }
+}
+
+// x0: the previous slot's Perron vector when that solve converged and the vector is well
+// inside the positive cone (a tiny entry would put the Collatz-Wielandt start far above rho),
+// else ones
+__global__ void tcc_init_kernel(const double* __restrict__ vprev, double* __restrict__ x, int64_t n,
+                                const double* __restrict__ scal, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  __shared__ double sh[EB];
+  double mn = INFINITY, mx = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += EB) {
+    mn = fmin(mn, vprev[i]);
+    mx = fmax(mx, vprev[i]);
+  }
+  mn = wg_reduce(mn, sh, Min());
+  mx = wg_reduce(mx, sh, Max());
+  const bool warm = scal[8] != 0.0 && scal[9] != 0.0 && mn > 1e-8 * mx && isfinite(mx);
+  for (int64_t i = threadIdx.x; i < n; i += EB) x[i] = warm ? vprev[i] : 1.0;
+}
+
+// y = M x on rows < n (one wave per row, fixed-order lane tree); skip_tr: B instead of A
+// (the top-right d x d block treated as zero)
+__global__ void tcc_gemv_kernel(const double* __restrict__ M, int64_t ld, int64_t n, int64_t d, int skip_tr,
+                                const double* __restrict__ x, double* __restrict__ y, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t jend = (skip_tr && i < d) ? d : n;
+  double acc = 0.0;
+  for (int64_t j = lane; j < jend; j += 64) acc += M[i * ld + j] * x[j];
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) y[i] = acc;
+}
+
+// y = M^T x on columns < n: stage 1, partial sums over 64-row chunks
+__global__ void tcc_gemv_t_partial_kernel(const double* __restrict__ M, int64_t ld, int64_t n,
+                                          const double* __restrict__ x, double* __restrict__ part,
+                                          const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  const int64_t j = (int64_t)blockIdx.x * EB + threadIdx.x;
+  const int64_t c = blockIdx.y;
+  if (j >= n) return;
+  const int64_t i1 = min(n, (c + 1) * 64);
+  double acc = 0.0;
+  for (int64_t i = c * 64; i < i1; ++i) acc += M[i * ld + j] * x[i];
+  part[c * ld + j] = acc;
+}
+
+__global__ void tcc_gemv_t_sum_kernel(const double* __restrict__ part, int64_t ld, int64_t n, int64_t nchunks,
+                                      double* __restrict__ y, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  const int64_t j = (int64_t)blockIdx.x * EB + threadIdx.x;
+  if (j >= n) return;
+  double acc = 0.0;
+  for (int64_t c = 0; c < nchunks; ++c) acc += part[c * ld + j];
+  y[j] = acc;
+}
+
+// sigma_0 = max_i (A x)_i / x_i  (y = A x)
+__global__ void tcc_sigma0_kernel(const double* __restrict__ x, const double* __restrict__ y, int64_t n,
+                                  double* __restrict__ scal, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  __shared__ double sh[EB];
+  double mx = -INFINITY;
+  for (int64_t i = threadIdx.x; i < n; i += EB) mx = fmax(mx, y[i] / x[i]);
+  mx = wg_reduce(mx, sh, Max());
+  if (threadIdx.x == 0) {
+    scal[1] = mx;
+    scal[2] = 0.0;  // lower bound (A >= 0)
+    scal[7] = 0.0;  // breakdown flag
+    scal[9] = 0.0;  // converged flag
+  }
+}
+
+// Mi = sigma (1 + margin) I - A on the logical block, identity padding
+__global__ void tcc_shift_kernel(const double* __restrict__ A, double* __restrict__ Mi, int64_t n, int64_t D2,
+                                 const double* __restrict__ scal, double margin, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  const double sig = scal[1] * (1.0 + margin);
+  const int64_t tot = D2 * D2;
+  for (int64_t e = (int64_t)blockIdx.x * EB + threadIdx.x; e < tot; e += (int64_t)gridDim.x * EB) {
+    const int64_t i = e / D2, j = e - i * D2;
+    double m;
+    if (i < n && j < n)
+      m = (i == j ? sig : 0.0) - A[e];
+    else
+      m = (i == j) ? 1.0 : 0.0;
+    Mi[e] = m;
+  }
+}
+
+// Noda update from y = (sigma_k I - A)^-1 x_k; turns gates k+1.. off when the bounds meet
+__global__ void tcc_noda_kernel(double* __restrict__ x, const double* __restrict__ y, int64_t n,
+                                double* __restrict__ scal, State* __restrict__ gates, int k, int nmax,
+                                const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  __shared__ double sh[EB];
+  double rmin = INFINITY, rmax = -INFINITY, ss = 0.0, bad = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += EB) {
+    const double yi = y[i];
+    if (!(yi > 0.0) || !isfinite(yi)) bad = 1.0;
+    const double r = x[i] / yi;
+    rmin = fmin(rmin, r);
+    rmax = fmax(rmax, r);
+    ss += yi * yi;
+  }
+  rmin = wg_reduce(rmin, sh, Min());
+  rmax = wg_reduce(rmax, sh, Max());
+  ss = wg_reduce(ss, sh, Add());
+  bad = wg_reduce(bad, sh, Max());
+  const double sig = scal[1];
+  bool stop;
+  if (bad != 0.0 || !(ss > 0.0) || !isfinite(ss)) {  // keep x_k, sigma_k: the final inverse uses them
+    stop = true;
+    if (threadIdx.x == 0) scal[7] = 1.0;
+  } else {
+    const double inv = 1.0 / sqrt(ss);
+    for (int64_t i = threadIdx.x; i < n; i += EB) x[i] = y[i] * inv;
+    const double up = sig - rmin, lo = sig - rmax;
+    // bounds met, or (reducible A: the lower bound need not tighten) the upper bound stalled
+    stop = !(up - lo > 1e-13 * fabs(up)) || !(sig - up > 1e-14 * fabs(up));
+    if (threadIdx.x == 0) {
+      scal[1] = up;
+      scal[2] = lo;
+      if (stop) scal[9] = 1.0;  // converged
+    }
+  }
+  if (stop && threadIdx.x == 0)
+    for (int t = k + 2; t <= nmax; ++t) gates[t].status = ST_DONE;
+}
+
+// out = y / |y|, sign such that sum(out) > 0 (notreks _make_positive_vector)
+__global__ void tcc_normalize_kernel(const double* __restrict__ y, double* __restrict__ out, int64_t n,
+                                     const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  __shared__ double sh[EB];
+  double ss = 0.0, s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += EB) {
+    ss += y[i] * y[i];
+    s += y[i];
+  }
+  ss = wg_reduce(ss, sh, Add());
+  s = wg_reduce(s, sh, Add());
+  const double inv = (s < 0.0 ? -1.0 : 1.0) / sqrt(ss);
+  for (int64_t i = threadIdx.x; i < n; i += EB) out[i] = y[i] * inv;
+}
+
+// value = (rho - u^T B u / (u^T u + eps)) / m with rho = u^T A v / u^T v; keeps the
+// denominators for the gradient and the vectors for the next slot's warm start
+__global__ void tcc_value_kernel(const double* __restrict__ u, const double* __restrict__ v,
+                                 const double* __restrict__ Av, const double* __restrict__ Bu, int64_t n, double eps,
+                                 double m, double* __restrict__ scal, double* __restrict__ vprev,
+                                 double* __restrict__ uprev, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  __shared__ double sh[EB];
+  double uav = 0.0, uv = 0.0, uu = 0.0, ubu = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += EB) {
+    uav += u[i] * Av[i];
+    uv += u[i] * v[i];
+    uu += u[i] * u[i];
+    ubu += u[i] * Bu[i];
+    vprev[i] = v[i];
+    uprev[i] = u[i];
+  }
+  uav = wg_reduce(uav, sh, Add());
+  uv = wg_reduce(uv, sh, Add());
+  uu = wg_reduce(uu, sh, Add());
+  ubu = wg_reduce(ubu, sh, Add());
+  if (threadIdx.x == 0) {
+    const double rho = uav / uv;
+    const double rho_lb = ubu / (uu + eps);
+    const double val = (rho - rho_lb) / m;
+    if (isfinite(val)) {
+      scal[0] = val;
+      scal[3] = rho;
+      scal[4] = uv + eps;  // u^T v + eps
+      scal[5] = uu + eps;  // u^T u + eps
+      scal[8] = 1.0;       // warm start available
+    } else {
+      // no Perron gap at all (W o W and S nilpotent, e.g. W = 0 at a fit's start): the shifted
+      // inverses overflow.  Value 0 and, through infinite denominators, gradient 0 -- the
+      // gradient 2 W o G is 0 there anyway; no warm start is kept
+      scal[0] = 0.0;
+      scal[3] = 0.0;
+      scal[4] = INFINITY;
+      scal[5] = INFINITY;
+      scal[8] = 0.0;
+    }
+  }
+}
+
+// Gtrek[i][j] = weight * (2W o G_W2(A) - 2W o G_W2(lb)) / m on the logical block, 0 elsewhere
+__global__ void tcc_grad_kernel(const double* __restrict__ W, const double* __restrict__ u,
+                                const double* __restrict__ v, const double* __restrict__ scal, int64_t d, int64_t D,
+                                double m, double weight, double* __restrict__ G, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  const double denA = scal[4], denB = scal[5];
+  const int64_t n = D * D;
+  for (int64_t e = (int64_t)blockIdx.x * EB + threadIdx.x; e < n; e += (int64_t)gridDim.x * EB) {
+    const int64_t i = e / D, j = e - i * D;
+    double g = 0.0;
+    if (i < d && j < d) {
+      const double w = W[e];
+      if (w != 0.0) {
+        const double gA = u[i] * v[j] / denA + u[d + j] * v[d + i] / denA;
+        const double gB = (u[i] * u[j] + u[d + i] * u[d + j]) / denB;
+        g = weight * (((2.0 * w) * gA - (2.0 * w) * gB) / m);
+      }
+    }
+    G[e] = g;
+  }
+}
+
+int grid_for(int64_t n) { return (int)std::min<int64_t>((n + EB - 1) / EB, 2048); }
+
+}  // namespace
+
+void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, const TccWork& w, const State* st,
+                     double* Gtrek, hipStream_t stream) {
+  const int64_t n = 2 * d, D2 = w.D2;
+  State* g0 = w.gates;
+  const double m = (double)cfg.m;
+  hipLaunchKernelGGL(tcc_gate_kernel, dim3(1), dim3(64), 0, stream, st, cfg.mode, w.gates, TCC_NODA_MAX);
+  hipLaunchKernelGGL(tcc_build_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, W, w.S, cfg.w, d, D, D2, w.A,
+                     g0);
+  const dim3 gv((unsigned)((n + 3) / 4));
+  const dim3 gt((unsigned)((n + EB - 1) / EB), (unsigned)((n + 63) / 64));
+  const dim3 gts((unsigned)((n + EB - 1) / EB));
+  const int64_t nchunks = (n + 63) / 64;
+  GJWork gj = w.gj;
+  gj.pivlog = nullptr;
+  gj.Pstore = nullptr;
+  // sigma_0 from the warm start
+  hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.vprev, w.x, n, w.scal, g0);
+  hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 0, w.x, w.y, g0);
+  hipLaunchKernelGGL(tcc_sigma0_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, g0);
+  for (int k = 0; k < TCC_NODA_MAX; ++k) {
+    const State* gk = &w.gates[1 + k];
+    hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, w.Mi, n, D2, w.scal, 0.0,
+                       gk);
+    launch_gj_inverse(w.Mi, D2, D2, gj, gk, stream);
+    hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gk);
+    hipLaunchKernelGGL(tcc_noda_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, w.gates, k, TCC_NODA_MAX,
+                       gk);
+  }
+  // final inverse just above the converged root: two sweeps for v, two (transposed) for u
+  hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, w.Mi, n, D2, w.scal, 1e-14,
+                     g0);
+  launch_gj_inverse(w.Mi, D2, D2, gj, g0, stream);
+  for (int r = 0; r < 2; ++r) {
+    hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, g0);
+    hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.x, n, g0);
+  }
+  hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.uprev, w.u, n, w.scal, g0);
+  for (int r = 0; r < 2; ++r) {
+    hipLaunchKernelGGL(tcc_gemv_t_partial_kernel, gt, dim3(EB), 0, stream, w.Mi, D2, n, w.u, w.part, g0);
+    hipLaunchKernelGGL(tcc_gemv_t_sum_kernel, gts, dim3(EB), 0, stream, w.part, D2, n, nchunks, w.y, g0);
+    hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.u, n, g0);
+  }
+  // rho (Rayleigh), the lower bound through B, value; then the gradient
+  hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 0, w.x, w.y, g0);
+  hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 1, w.u, w.z, g0);
+  hipLaunchKernelGGL(tcc_value_kernel, dim3(1), dim3(EB), 0, stream, w.u, w.x, w.y, w.z, n, cfg.eps, m, w.scal,
+                     w.vprev, w.uprev, g0);
+  if (cfg.mode == 2)
+    hipLaunchKernelGGL(tcc_grad_kernel, dim3(grid_for(D * D)), dim3(EB), 0, stream, W, w.u, w.x, w.scal, d, D, m,
+                       cfg.weight, Gtrek, g0);
+  HIP_TRY(hipGetLastError());
+}
+
+}  // namespace midagma

@@ -15,9 +15,10 @@ the C ABI.  Extra keyword-only constructor arguments:
 
 Trek regularizers (`trek_reg`, linear.py:251-258): the PST family of
 `notreks.PSTRegularizer` (seq exp / inv / log / binom, agg mean / sum / max / lse,
-modes 'opt' and 'log') runs on the GPU inside the loop (csrc/trek.hip).  The TCC
-regularizer (spectral Perron eigenvectors of a 2d x 2d non-symmetric matrix every
-step, numpy `eig` in the reference) has no GPU path yet; passing an enabled one raises.
+modes 'opt' and 'log') runs on the GPU inside the loop (csrc/trek.hip), and so does
+`notreks.TCCRegularizer` (csrc/tcc.hip): the Perron pair of the 2d x 2d block matrix,
+which the reference takes from numpy `eig` every step, comes from Noda's iteration on
+the Gauss-Jordan M-matrix inverse.
 """
 from __future__ import annotations
 
@@ -63,8 +64,8 @@ class DagmaLinear:
         assert loss_type in losses, f"loss_type should be one of {losses}"
         if dtype is not np.float64:
             raise ValueError("the HIP inner solver computes in float64 only (as the reference's cov/X)")
-        if trek_reg is not None and trek_reg.enabled() and str(trek_reg.name).lower().strip() != "pst":
-            raise NotImplementedError(f"trek regularizer {trek_reg.name!r}: only 'pst' runs on the GPU path")
+        if trek_reg is not None and trek_reg.enabled() and str(trek_reg.name).lower().strip() not in ("pst", "tcc"):
+            raise ValueError(f"Unknown trek regularizer: {trek_reg.name}. Has to be in ['pst', 'tcc']")
         self.loss_type = loss_type
         self.dtype = dtype
         self.vprint = print if verbose else (lambda *a, **k: None)
@@ -120,9 +121,15 @@ class DagmaLinear:
         s.set_cov(self.cov)
         tr = self.trek_reg
         if tr is not None and tr.enabled() and tr.cfg.get("I") is not None and len(tr.cfg["I"]) > 0:
-            kw = dict(tr.cfg.get("kwargs") or {})
-            s.set_trek(tr.cfg["I"], tr.cfg.get("seq", "exp"), agg=kw.get("agg", "mean"), mode=tr.mode,
-                       weight=tr.weight, eps_inv=kw.get("eps_inv", 1e-8), K_log=kw.get("K_log"))
+            if str(tr.name).lower().strip() == "tcc":
+                # trek_value_grad runs TCC with its defaults whatever the regularizer's
+                # cycle_penalty / version / method (notreks.py:691-698): only w and eps reach it
+                s.set_trek_tcc(tr.cfg["I"], mode=tr.mode, weight=tr.weight, w=tr.cfg.get("w", 1.0),
+                               eps=tr.cfg.get("eps", 1e-12))
+            else:
+                kw = dict(tr.cfg.get("kwargs") or {})
+                s.set_trek(tr.cfg["I"], tr.cfg.get("seq", "exp"), agg=kw.get("agg", "mean"), mode=tr.mode,
+                           weight=tr.weight, eps_inv=kw.get("eps_inv", 1e-8), K_log=kw.get("K_log"))
         self._solver = s
 
     # ------------------------------------------------------- reference methods

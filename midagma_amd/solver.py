@@ -113,6 +113,18 @@ class HipSolver:
                                       float(weight), float(eps_inv), K, P.ctypes.data_as(C.POINTER(C.c_int64)),
                                       int(P.shape[0])), self.h, "set_trek")
 
+    def set_trek_tcc(self, pairs, *, mode: str = "opt", weight: float = 0.0, w: float = 1.0, eps: float = 1e-12):
+        """The TCC trek regularizer as the reference's loop runs it (trek_value_grad -> spectral,
+        'approx_trek_graph'); mode 'off' or no pairs disables it."""
+        P = np.ascontiguousarray(np.asarray(pairs, dtype=np.int64).reshape(-1, 2)) if pairs is not None \
+            else np.zeros((0, 2), dtype=np.int64)
+        mode = mode.lower().strip()
+        if mode not in self.TREK_MODE:
+            raise ValueError(f"unsupported TCC mode {mode!r}")
+        check(self.L.midagma_set_trek_tcc(self.h, self.TREK_MODE[mode], float(weight), float(w), float(eps),
+                                          P.ctypes.data_as(C.POINTER(C.c_int64)), int(P.shape[0])), self.h,
+              "set_trek_tcc")
+
     def trek_value(self, W: np.ndarray, grad: bool = True):
         """notreks.trek_value_grad(W, tr) for the configured regularizer: (value, grad or None)."""
         W = _as_f64(W)

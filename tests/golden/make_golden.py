@@ -277,6 +277,46 @@ def gen_trek():
     np.savez_compressed(os.path.join(HERE, "trek_pst.npz"), **out)
 
 
+def tcc_cases(d, rng):
+    """(name, W) inputs for the TCC fixtures: dense in-domain, tiny (start of a fit), and a
+    weighted DAG (W o W nilpotent: the Perron structure comes from the S / I coupling)."""
+    dense = in_domain_W(d, rng, 0.35)
+    tiny = in_domain_W(d, rng, 1e-3)
+    B = np.tril(rng.uniform(size=(d, d)) < 0.2, -1)
+    dag = B * rng.uniform(0.5, 1.5, (d, d)) * rng.choice([-1.0, 1.0], (d, d))
+    p = rng.permutation(d)
+    return [("dense", dense), ("tiny", tiny), ("dag", dag[np.ix_(p, p)])]
+
+
+def gen_tcc(X20):
+    """TCC trek regularizer from the reference: trek_value_grad (the loop's entry: spectral,
+    approx_trek_graph, numpy eig) on several W, and minimize trajectories with it at d=20."""
+    from notreks.notreks import TCCRegularizer, trek_value_grad
+    rng = np.random.default_rng(23)
+    out = {}
+    for d in (8, 20):
+        pairs = np.array([(i, j) for i in range(d) for j in range(i + 1, d) if rng.uniform() < 0.3], dtype=np.int64)
+        out[f"pairs_d{d}"] = pairs
+        for name, W in tcc_cases(d, rng):
+            out[f"W_{name}_d{d}"] = W
+            for w in (1.0, 2.0):
+                tr = TCCRegularizer(I=pairs, weight=0.5, w=w, mode="opt")
+                v, g = trek_value_grad(W.copy(), tr)
+                out[f"val_{name}_w{w:g}_d{d}"] = np.array(v)
+                out[f"grad_{name}_w{w:g}_d{d}"] = g
+    # the loop (linear.py:251-258, 122-133): opt mode (gradient every step) and log mode
+    d = X20.shape[1]
+    pairs = out["pairs_d20"]
+    out["traj_Ks"] = np.array([1, 10, 90])
+    for mode in ("opt", "log"):
+        for K in (1, 10, 90):
+            m = setup_model(X20, "l2", checkpoint=40)
+            m.trek_reg = TCCRegularizer(I=pairs, weight=0.2, mode=mode)
+            W, ok, it = run_minimize(m, np.zeros((d, d)), 1.0, K, 1.0, 3e-4)
+            out[f"traj_{mode}_W_K{K}"], out[f"traj_{mode}_it_K{K}"] = W, np.array(it)
+    np.savez_compressed(os.path.join(HERE, "trek_tcc.npz"), **out)
+
+
 def gen_mlp():
     """DagmaMLP.h_func value and autograd gradient (nonlinear.py:68-86).
 
@@ -315,9 +355,17 @@ def main():
         gen_fit(X20)
         gen_fit_envelope(X20)
         gen_trek()
+        gen_tcc(X20)
         gen_mlp()
     print("golden fixtures written to", HERE)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:  # regenerate selected fixtures: make_golden.py gen_tcc ...
+        with threadpool_limits(limits=1):
+            X20 = np.load(os.path.join(HERE, "data_d20_n1000_seed0.npz"))["X"]
+            for name in sys.argv[1:]:
+                fn = globals()[name]
+                fn(X20) if name == "gen_tcc" else fn()
+    else:
+        main()

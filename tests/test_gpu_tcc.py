@@ -1,0 +1,140 @@
+"""TCC trek regularizer on the GPU (csrc/tcc.hip: Noda iteration on the Gauss-Jordan M-matrix
+inverse) vs the reference's trek_value_grad / minimize (tests/golden/trek_tcc.npz) and the
+oracle (oracle/trek_oracle.py::tcc_value_grad, numpy eig as the reference).
+
+Tolerances: the Perron pair comes from a different (iterative) algorithm than LAPACK's
+eigendecomposition, so value and gradient agree to the eigenvector conditioning, not bit for
+bit: 1e-10 relative; W after the loop 1e-9 (the north star asks 1e-5)."""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle.dagma_oracle import LinearOracle  # noqa: E402
+from oracle.trek_oracle import tcc_value_grad  # noqa: E402
+
+
+def _solver(d, cov):
+    from midagma_amd.solver import HipSolver
+    s = HipSolver(d, "l2", "cov", device=0)
+    s.set_cov(cov)
+    return s
+
+
+@pytest.mark.parametrize("d", [8, 20])
+@pytest.mark.parametrize("case", ["dense", "tiny", "dag"])
+@pytest.mark.parametrize("w", [1.0, 2.0])
+def test_tcc_value_grad_matches_reference(golden, d, case, w):
+    f = golden("trek_tcc.npz")
+    W, pairs = f[f"W_{case}_d{d}"], f[f"pairs_d{d}"]
+    s = _solver(d, np.eye(d))
+    s.set_trek_tcc(pairs, mode="opt", weight=0.5, w=w)
+    v, g = s.trek_value(W)
+    v_ref, g_ref = float(f[f"val_{case}_w{w:g}_d{d}"]), f[f"grad_{case}_w{w:g}_d{d}"]
+    assert abs(v - v_ref) <= 1e-10 * abs(v_ref)
+    assert np.abs(g - g_ref).max() <= 1e-10 * np.abs(g_ref).max()
+    # again from the warm start the first call left: same answer
+    v2, g2 = s.trek_value(W)
+    assert abs(v2 - v_ref) <= 1e-10 * abs(v_ref)
+    assert np.abs(g2 - g_ref).max() <= 1e-10 * np.abs(g_ref).max()
+    s.close()
+
+
+@pytest.mark.parametrize("d", [64, 300])
+def test_tcc_value_grad_matches_oracle_larger(d):
+    rng = np.random.default_rng(d)
+    W = rng.uniform(-1, 1, (d, d)) * (0.6 / np.sqrt(d))
+    np.fill_diagonal(W, 0)
+    iu = np.array(np.triu_indices(d, 1)).T
+    pairs = iu[rng.uniform(size=len(iu)) < 0.1]
+    s = _solver(d, np.eye(d))
+    s.set_trek_tcc(pairs, mode="opt", weight=1.0)
+    v, g = s.trek_value(W)
+    vr, gr = tcc_value_grad(W, pairs)
+    assert abs(v - vr) <= 1e-10 * abs(vr)
+    assert np.abs(g - gr).max() <= 1e-10 * np.abs(gr).max()
+    s.close()
+
+
+def test_tcc_at_zero_and_log_mode(golden):
+    """W = 0 (a fit's start): A is nilpotent (no Perron gap) -- the gradient 2 W o G is exactly 0
+    and the value finite; 'log' mode returns a zero gradient as the reference does."""
+    f = golden("trek_tcc.npz")
+    pairs = f["pairs_d20"]
+    s = _solver(20, np.eye(20))
+    s.set_trek_tcc(pairs, mode="opt", weight=0.5)
+    v, g = s.trek_value(np.zeros((20, 20)))
+    assert np.isfinite(v) and not g.any()
+    s.set_trek_tcc(pairs, mode="log", weight=0.5)
+    W = f["W_dense_d20"]
+    v, g = s.trek_value(W)
+    assert abs(v - float(f["val_dense_w1_d20"])) <= 1e-10 * abs(v) and not g.any()
+    s.set_trek_tcc(np.zeros((0, 2), dtype=np.int64), mode="opt", weight=0.5)
+    v, g = s.trek_value(W)
+    assert v == 0.0 and not g.any()
+    s.close()
+
+
+@pytest.mark.parametrize("mode", ["opt", "log"])
+@pytest.mark.parametrize("K", [1, 10, 90])
+def test_minimize_with_tcc_matches_reference(golden, mode, K):
+    f = golden("trek_tcc.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"]
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 40)
+    s = _solver(20, o.cov)
+    s.set_trek_tcc(f["pairs_d20"], mode=mode, weight=0.2)
+    W = np.zeros((20, 20))
+    res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=40)
+    assert res.iters == int(f[f"traj_{mode}_it_K{K}"])
+    assert np.abs(W - f[f"traj_{mode}_W_K{K}"]).max() <= 1e-9
+    s.close()
+
+
+@pytest.mark.parametrize("d,mode", [(20, "opt"), (20, "log"), (300, "opt")])
+def test_minimize_with_tcc_checkpoints_match_oracle(golden, d, mode):
+    """Checkpoint records with TCC: objective (+ weight * value in 'opt'), reg_trek_value,
+    grad_trek_norm.  d=300 runs the blocked fast path with the 600 x 600 Perron problem."""
+    from midagma_amd.simulate import make_dataset
+    X, _, _ = make_dataset(d, 1000 if d == 20 else 600, seed=5)
+    rng = np.random.default_rng(5)
+    iu = np.array(np.triu_indices(d, 1)).T
+    pairs = iu[rng.uniform(size=len(iu)) < 0.3]
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 40)
+    o.trek = dict(kind="tcc", pairs=pairs, mode=mode, weight=0.2)
+    K = 90 if d == 20 else 45
+    s = _solver(d, o.cov)
+    s.set_trek_tcc(pairs, mode=mode, weight=0.2)
+    W = np.zeros((d, d))
+    res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=40, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert res.iters == tr.iters == K
+    assert np.abs(W - Wr).max() <= 1e-9
+    assert [c.iter for c in res.checkpoints] == [r["iter"] for r in tr.records]
+    for c, r in zip(res.checkpoints, tr.records):
+        assert abs(c.obj - r["obj_total"]) <= 1e-10 * abs(r["obj_total"])
+        assert abs(c.reg_trek_value - r["reg_trek_value"]) <= 1e-9 * abs(r["reg_trek_value"])
+        assert abs(c.grad_trek_norm - r["grad_trek_norm"]) <= 1e-9 * r["grad_trek_norm"] + 1e-15
+    s.close()
+
+
+def test_dagma_linear_tcc_fit_runs(golden):
+    from midagma_amd import DagmaLinear
+    f = golden("trek_tcc.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"]
+    pairs = f["pairs_d20"]
+    reg = SimpleNamespace(name="tcc", mode="opt", weight=0.1, cycle_penalty="logdet",
+                          cfg={"I": pairs, "version": "exact_trek_graph", "w": 1.0, "n_iter": 10, "eps": 1e-12,
+                               "s": 1.0}, enabled=lambda: True)
+    m = DagmaLinear("l2", trek_reg=reg)
+    W = m.fit(X, lambda1=0.03, T=2, warm_iter=200, max_iter=300)
+    assert W.shape == (20, 20) and np.isfinite(W).all()
+    Wd = f["W_dense_d20"]
+    obj, sc, h, tv = m._func(Wd, 0.1, 1.0)
+    v_ref, _ = tcc_value_grad(Wd, pairs)   # the loop ignores cycle_penalty / version (notreks.py:691)
+    assert abs(tv - v_ref) <= 1e-10 * abs(v_ref)

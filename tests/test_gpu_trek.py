@@ -93,7 +93,7 @@ def test_minimize_with_trek_matches_oracle(hip, d, seq, mode):
 
 
 def test_dagma_linear_pst_fit_runs(hip):
-    """DagmaLinear(trek_reg=PSTRegularizer-like) configures the GPU regularizer; TCC raises."""
+    """DagmaLinear(trek_reg=PSTRegularizer-like) configures the GPU regularizer; unknown names raise."""
     from types import SimpleNamespace
     from midagma_amd import DagmaLinear
     X, pairs = _trek_case(20, 7)
@@ -110,5 +110,5 @@ def test_dagma_linear_pst_fit_runs(hip):
     obj, sc, h, tv = m._func(Wr, 0.1, 0.9)
     v_ref, _ = pst_value_grad(Wr, pairs, "exp", grad=False)
     assert abs(tv - v_ref) <= 1e-11 * v_ref
-    with pytest.raises(NotImplementedError):
-        DagmaLinear("l2", trek_reg=reg("tcc"))
+    with pytest.raises(ValueError):
+        DagmaLinear("l2", trek_reg=reg("nope"))

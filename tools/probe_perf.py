@@ -60,7 +60,11 @@ def trek_case(d, seq, K):
     s.set_cov(X.T @ X / X.shape[0])
     rng = np.random.default_rng(0)
     iu = np.array(np.triu_indices(d, 1)).T
-    s.set_trek(iu[rng.uniform(size=len(iu)) < 0.3], seq, agg="mean", mode="opt", weight=0.1, K_log=20)
+    pairs = iu[rng.uniform(size=len(iu)) < 0.3]
+    if seq == "tcc":
+        s.set_trek_tcc(pairs, mode="opt", weight=0.1)
+    else:
+        s.set_trek(pairs, seq, agg="mean", mode="opt", weight=0.1, K_log=20)
     s.begin(np.zeros((d, d)), 1.0, K + 1000, 1.0, 3e-4, tol=-1.0)
     s.run_slots(3)
     s.sync()
@@ -68,7 +72,7 @@ def trek_case(d, seq, K):
     s.run_slots(K)
     s.sync()
     dt = time.perf_counter() - t0
-    print(f"cov+PST-{seq} d={d}: {K / dt:.1f} steps/s ({dt / K * 1e3:.3f} ms/step)", flush=True)
+    print(f"cov+{'TCC' if seq == 'tcc' else 'PST-' + seq} d={d}: {K / dt:.1f} steps/s ({dt / K * 1e3:.3f} ms/step)", flush=True)
     s.close()
 
 
@@ -84,5 +88,8 @@ if __name__ == "__main__":
     if which == "trek":
         for seq in ("exp", "inv", "log"):
             trek_case(1000, seq, 50)
+    if which == "tcc":
+        for d, K in ((20, 2000), (100, 500), (300, 200), (1000, 50)):
+            trek_case(d, "tcc", K)
     if which in ("all", "data"):
         data_case(1000, 100000, 2, 10)
