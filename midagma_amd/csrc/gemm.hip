@@ -272,7 +272,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
         const int64_t row = m0 + mb + i * 16 + acc_row(lane, tt);
         const int64_t col = n0 + nbs + j * 16 + acc_col(lane);
         const double v = acc[i][j][tt];
-        if (want_loss && row < m_valid && col < n_valid) part += logaddexp0(v) - A[row * lda + col] * v;
+        if (want_loss && row < m_valid && col < n_valid)  // X[row][col]: A's (m, k) = (row, col)
+          part += logaddexp0(v) - (ATRANS ? A[col * lda + row] : A[row * lda + col]) * v;
         Ct[row * ldc + col] = 1.0 / (1.0 + exp(-v));
       }
   if (!want_loss) return;
@@ -309,6 +310,7 @@ void gemm_setup_attributes() {
   set_attr128<true, B_PLAIN, EPI_STORE>();
   set_attr128<true, B_IMINUS, EPI_STORE>();
   set_attr128<false, B_PLAIN, EPI_SIGMOID>();
+  set_attr128<true, B_PLAIN, EPI_SIGMOID>();
   set_attr128<false, B_PLAIN, EPI_SUB_BAND>();
   set_attr<false, B_PLAIN, EPI_STORE>();
   set_attr<false, B_IMINUS, EPI_STORE>();
@@ -333,8 +335,12 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
   hipLaunchKernelGGL((gemm128_kernel<AT, BM, EP>), dim3((unsigned)nwg), dim3(NTHREADS), kGemm128Lds, stream, K, \
                      kslice, tm, tn, A, lda, B, ldb, C, ldc, slice_stride, loss_part, m_valid, n_valid, st)
     if (epi == EPI_SIGMOID) {
-      if (a_trans || bmode != B_PLAIN || nsplit != 1) throw std::invalid_argument("launch_gemm: sigmoid form");
-      MIDAGMA_GEMM128(false, B_PLAIN, EPI_SIGMOID);
+      if (bmode != B_PLAIN || nsplit != 1 || (a_trans && N != K))
+        throw std::invalid_argument("launch_gemm: sigmoid form");
+      if (a_trans)
+        MIDAGMA_GEMM128(true, B_PLAIN, EPI_SIGMOID);
+      else
+        MIDAGMA_GEMM128(false, B_PLAIN, EPI_SIGMOID);
     } else if (epi == EPI_SUB_BAND) {
       throw std::invalid_argument("launch_gemm: use launch_trail128");
     } else if (!a_trans && bmode == B_PLAIN) {
@@ -384,6 +390,31 @@ void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int
   hipLaunchKernelGGL((gemm128_kernel<false, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
                      kGemm128Lds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
                      (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
+  HIP_TRY(hipGetLastError());
+}
+
+// dst[c][r] = src[r][c] for r < rows, c < cols (64 x 64 tiles through LDS)
+__global__ __launch_bounds__(NTHREADS) void transpose_kernel(const double* __restrict__ src, int64_t ld_src,
+                                                             int64_t rows, int64_t cols, double* __restrict__ dst,
+                                                             int64_t ld_dst) {
+  __shared__ double t[64][65];
+  const int64_t r0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    t[i][tx] = (r < rows && c < cols) ? src[r * ld_src + c] : 0.0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows) dst[c * ld_dst + r] = t[tx][i];
+  }
+}
+
+void launch_transpose(const double* src, int64_t ld_src, int64_t rows, int64_t cols, double* dst, int64_t ld_dst,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((rows + 63) / 64), (unsigned)((cols + 63) / 64)),
+                     dim3(NTHREADS), 0, stream, src, ld_src, rows, cols, dst, ld_dst);
   HIP_TRY(hipGetLastError());
 }
 

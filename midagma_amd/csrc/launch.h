@@ -150,6 +150,9 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
 // with `check`, ORs the domain flags of the outputs into st->flags.
 void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
                      hipStream_t stream);
+// dst[c][r] = src[r][c] (rows x cols)
+void launch_transpose(const double* src, int64_t ld_src, int64_t rows, int64_t cols, double* dst, int64_t ld_dst,
+                      hipStream_t stream);
 // out[i] = sum_z parts[z*stride + i] (fixed order) for i < count.
 void launch_sum_slices(const double* parts, int split, int64_t stride, int64_t count, double* out,
                        const State* st, hipStream_t stream);

@@ -74,6 +74,12 @@ struct midagma_solver {
   DevBuf X, Y, Zparts, loss_part, cov_parts;
   int cov_split = 1;
   int64_t n_local = 0, n_pad = 0, n_global = 0;
+  // X^T (D x n_pad), the xw GEMM's A operand in the m-contiguous layout (the X^T Y GEMM reads
+  // X itself that way); kept when the device has the room (MIDAGMA_NO_XT disables it)
+  DevBuf XT;
+  bool use_xt = false;
+  const double* xw_a() const { return use_xt ? XT.p : X.p; }
+  int64_t xw_lda() const { return use_xt ? n_pad : D; }
   int split = 1;
   int64_t loss_part_count = 0;
 
@@ -100,7 +106,7 @@ struct midagma_solver {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2,
-                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart})
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT})
       b->release();
     for (DevBuf& b : tbufs) b.release();
     for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices, &cA, &cMi, &cS, &cvec, &cpart, &cP, &cR, &cC}) b->release();
@@ -182,9 +188,9 @@ struct midagma_solver {
   // Z_k = X_k^T (X_k (I - W))  (l2)   or   X_k^T expit(X_k W)  (logistic, + loss partial)
   void enqueue_data_partial(const double* Wp, const State* st) {
     if (loss == MIDAGMA_LOSS_L2) {
-      launch_gemm(n_pad, D, D, X.p, D, false, Wp, D, B_IMINUS, Y.p, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
+      launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, Wp, D, B_IMINUS, Y.p, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
     } else {
-      launch_gemm(n_pad, D, D, X.p, D, false, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, 1, 0, loss_part.p, n_local, d,
+      launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, 1, 0, loss_part.p, n_local, d,
                   st, stream);
       launch_sum_vector(loss_part.p, loss_part_count, zbuf + D * D, st, stream);
     }
@@ -755,6 +761,17 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     HIP_TRY(hipMemsetAsync(s->X.p, 0, nx * sizeof(double), s->stream));
     HIP_TRY(hipMemcpy2DAsync(s->X.p, D * sizeof(double), X, s->d * sizeof(double), s->d * sizeof(double), n_local,
                              on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s->stream));
+    size_t mem_free = 0, mem_total = 0;
+    HIP_TRY(hipMemGetInfo(&mem_free, &mem_total));
+    // (the 128-tile GEMM only: D % 128 == 0; smaller problems are not worth the copy)
+    s->use_xt = getenv("MIDAGMA_NO_XT") == nullptr && D % 128 == 0 &&
+                mem_free > nx * sizeof(double) + (size_t(2) << 30);
+    if (s->use_xt) {
+      s->XT.alloc(nx);
+      launch_transpose(s->X.p, D, s->n_pad, D, s->XT.p, s->n_pad, s->stream);
+    } else {
+      s->XT.release();
+    }
     // split-K over the rows so the X^T Y GEMM fills the chip: (D/64)^2 tiles x split >= ~1024 workgroups
     const int64_t tiles = (D % 128 == 0) ? (D / 128) * (D / 128) : (D / 64) * (D / 64);
     const int64_t ktiles = s->n_pad / 64;
@@ -886,10 +903,10 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
       ms_out[2] = timed([&] { s->enqueue_data_partial(s->W.p, s->d_state); });
       ms_out[4] = timed([&] {
         if (s->loss == MIDAGMA_LOSS_L2)
-          launch_gemm(s->n_pad, D, D, s->X.p, D, false, s->W.p, D, B_IMINUS, s->Y.p, D, EPI_STORE, 1, 0, nullptr, 0,
+          launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_IMINUS, s->Y.p, D, EPI_STORE, 1, 0, nullptr, 0,
                       0, s->d_state, s->stream);
         else
-          launch_gemm(s->n_pad, D, D, s->X.p, D, false, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID, 1, 0,
+          launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID, 1, 0,
                       s->loss_part.p, s->n_local, s->d, s->d_state, s->stream);
       });
       ms_out[5] = timed([&] {
