@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--no-fit", action="store_true", help="skip the full-fit wall-clock leg (config 2)")
     p.add_argument("--no-data", action="store_true", help="skip the data-mode leg (profiling the other legs)")
     p.add_argument("--no-large", action="store_true", help="skip the config 3 leg (d=5000, n=5e4, cov mode)")
+    p.add_argument("--no-mlp", action="store_true", help="skip the config 5 leg (DagmaNonlinear, dims [200,10,1])")
+    p.add_argument("--mlp-steps", type=int, default=300)
     p.add_argument("--large-d", type=int, default=5000)
     p.add_argument("--large-n", type=int, default=50_000)
     p.add_argument("--large-steps", type=int, default=100)
@@ -187,6 +189,82 @@ def bench_cov(args, device):
     s.close()
     return dict(value=K / (t1 - t0), ms_per_step=(t1 - t0) / K * 1e3, steps=K, verified=(r.status == 0 and
                 r.iters == K + 20), prof=prof, cov=cov)
+
+
+_MLP_CPU_CHILD = r"""
+import json, sys, time
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+from oracle.mlp_oracle import OracleMLP, load_params, nonlinear_minimize
+th, d, n = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+torch.set_num_threads(th)
+P = np.load(sys.argv[5])
+m = OracleMLP([d, 10, 1])
+load_params(m, {k: P[k] for k in P.files if k != "X"})
+X = torch.from_numpy(P["X"])
+nonlinear_minimize(m, X, 2, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
+K = 20
+t0 = time.perf_counter()
+ok, it = nonlinear_minimize(m, X, K, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1, checkpoint=10 ** 9)
+assert ok and it == K, (ok, it)
+print(json.dumps({"t": (time.perf_counter() - t0) / K}))
+"""
+
+
+def bench_mlp(args, device, with_cpu):
+    """Config 5 (BASELINE): DagmaNonlinear Adam steps at dims [200, 10, 1], n=1000 -- the
+    reference's minimize loop in PyTorch-ROCm with the HIP log-det h_func; replicas only
+    (SURVEY 8e).  CPU: the oracle restatement (torch CPU, slogdet) in child processes."""
+    import subprocess
+    import tempfile
+    import torch
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    from midagma_amd.simulate import make_dataset
+    d, n = 200, 1000
+    X, _, _ = make_dataset(d, n, seed=args.seed)
+    torch.manual_seed(args.seed)
+    model = DagmaMLP(dims=[d, 10, 1]).to(torch.device("cuda", device))
+    with torch.no_grad():
+        model.fc1.weight.normal_(0, 0.3 / np.sqrt(10 * d))
+    params = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items() if k != "I"}
+    dn = DagmaNonlinear(model, device=device)
+    dn.X = torch.from_numpy(X).to(torch.device("cuda", device))
+    dn.checkpoint = 10 ** 9
+    dn.minimize(20, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
+    torch.cuda.synchronize(device)
+    K = args.mlp_steps
+    t0 = time.perf_counter()
+    ok = dn.minimize(K, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    out = dict(value=K / dt, unit="steps/s", ms_per_step=dt / K * 1e3, steps=K, verified=bool(ok),
+               workload="config5: DagmaNonlinear.minimize, DagmaMLP dims [200, 10, 1], n=1000, 1 GPU "
+                        "(PyTorch-ROCm model + Adam, HIP log-det h_func)")
+    if with_cpu:
+        best = None
+        ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+        share = min(ncpu, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "mlp.npz")
+            np.savez(path, X=X, **params)
+            for th in sorted({1, 4, 8, share} & set(range(1, share + 1))):
+                env = dict(os.environ, OMP_NUM_THREADS=str(th), HIP_VISIBLE_DEVICES="")
+                try:
+                    r = subprocess.run([sys.executable, "-c", _MLP_CPU_CHILD, REPO, str(th), str(d), str(n), path],
+                                       capture_output=True, text=True, timeout=600, env=env)
+                    t = json.loads(r.stdout.strip().splitlines()[-1])["t"]
+                    log(f"cpu oracle MLP d={d}: {1 / t:.1f} steps/s at {th} threads")
+                    if best is None or t < best[0]:
+                        best = (t, th)
+                except Exception as e:  # noqa: BLE001
+                    log(f"cpu oracle MLP at {th} threads failed: {e!r}")
+        if best is not None:
+            out["cpu_baseline"] = dict(value=1.0 / best[0], unit="steps/s", cores=best[1], kind="port",
+                                       sample="oracle DagmaNonlinear.minimize (torch CPU, slogdet h_func as "
+                                              "nonlinear.py:84), 20 steps per thread count, best shown")
+            out["vs_cpu"] = out["value"] * best[0]
+    return out
 
 
 def bench_cov_large(args, device):
@@ -383,12 +461,15 @@ def main():
     large_res = None
     if rank == 0 and world == 1 and not args.no_large and args.workload == "data":
         large_res = bench_cov_large(args, local)
+    mlp_res = None
+    if rank == 0 and world == 1 and not args.no_mlp and args.workload == "data":
+        mlp_res = bench_mlp(args, local, with_cpu=not args.no_cpu)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and cov_res is not None:
         cpu = cpu_baseline(args, cov_res["cov"])
     if rank == 0 and res is None and cov_res is None:   # --no-data --no-cov: a profiling run of the other legs
         out = {k: v for k, v in (large_res or {}).items() if k != "cov"}
-        print(json.dumps({"config3": out, "full_fit": fit_res}), flush=True)
+        print(json.dumps({"config3": out, "full_fit": fit_res, "config5": mlp_res}), flush=True)
         return
     if rank == 0:
         d = args.d
@@ -474,6 +555,8 @@ def main():
                                f"(checkpoint cost cancelled), {th} threads")
                     lr_["vs_cpu"] = lr_["value"] * tt
             line["config3"] = lr_
+        if mlp_res is not None:
+            line["config5"] = mlp_res
         if fit_res is not None:
             fr = dict(fit_res)
             fr["workload"] = f"config2: DagmaLinear('l2').fit(X) defaults, d={d}, n={args.cov_n}, 1 GPU (cov mode)"

@@ -1,9 +1,9 @@
-"""`DagmaMLP` whose log-det acyclicity term runs on the HIP GJ/log-det kernel.
+"""`DagmaMLP` / `DagmaNonlinear` whose log-det acyclicity term runs on the HIP GJ/log-det kernel.
 
-Mirrors `dagma.nonlinear.DagmaMLP` (fbleile/midagma, src/dagma/nonlinear.py:14-115)
-and `LocallyConnected` (src/dagma/locally_connected.py).  The MLP forward and
-the score stay PyTorch-ROCm; only
-``h_func`` (nonlinear.py:68-86) is replaced:
+Mirrors `dagma.nonlinear.DagmaMLP`, `DagmaNonlinear` (fbleile/midagma,
+src/dagma/nonlinear.py:14-331) and `LocallyConnected` (src/dagma/locally_connected.py).
+The MLP forward, the score and Adam stay PyTorch-ROCm on the GPU (SURVEY.md section 2,
+row 4; BASELINE config 5); only ``h_func`` (nonlinear.py:68-86) is replaced:
 
     A = sum_m fc1_w[j, m, i]^2   (transposed: [i, j])
     h = -log|det(sI - A)| + d log s          forward  : HIP blocked Gauss-Jordan
@@ -14,6 +14,7 @@ and current HIP stream; it never synchronizes with the host.
 """
 from __future__ import annotations
 
+import copy
 import ctypes as C
 import math
 import typing
@@ -24,7 +25,7 @@ import torch.nn as nn
 
 from . import _lib
 
-__all__ = ["LocallyConnected", "DagmaMLP", "logdet_h"]
+__all__ = ["LocallyConnected", "DagmaMLP", "DagmaNonlinear", "logdet_h"]
 
 
 class _LogdetH(torch.autograd.Function):
@@ -79,7 +80,14 @@ class LocallyConnected(nn.Module):
             nn.init.uniform_(self.bias, -bound, bound)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = torch.matmul(x.unsqueeze(dim=2), self.weight.unsqueeze(dim=0)).squeeze(dim=2)
+        # out[n, j, o] = sum_m x[n, j, m] w[j, m, o] (+ b[j, o]): the reference's broadcast matmul
+        # (locally_connected.py:55-85) is n*d tiny (1 x m1) @ (m1 x m2) products, which the GPU
+        # runs as a batched GEMM of n*d batches; a width-1 output is a multiply-and-reduce over m,
+        # wider outputs one GEMM per node (same sums, at most an ulp of reordering apart)
+        if self.output_features == 1:
+            out = torch.sum(x * self.weight.squeeze(dim=2), dim=2, keepdim=True)
+        else:
+            out = torch.einsum("njm,jmo->njo", x, self.weight)
         if self.bias is not None:
             out = out + self.bias
         return out
@@ -123,3 +131,105 @@ class DagmaMLP(nn.Module):
     @torch.no_grad()
     def fc1_to_adj(self) -> np.ndarray:
         return torch.sqrt(self._adjacency_sq()).cpu().numpy()
+
+
+class _NoBar:
+    def update(self, k=1):
+        pass
+
+
+class DagmaNonlinear:
+    """DAGMA for nonlinear SEMs (nonlinear.py:118-331): the reference's outer loop and Adam
+    over the model's parameters, on the model's ROCm device (moved there by `fit`), with the
+    HIP log-det in ``model.h_func``.  ``device``: HIP ordinal (default: the current device)."""
+
+    def __init__(self, model: nn.Module, verbose: bool = False, dtype: torch.dtype = torch.double, *,
+                 device: typing.Optional[int] = None):
+        self.vprint = print if verbose else (lambda *a, **k: None)
+        self.model = model
+        self.dtype = dtype
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+
+    def log_mse_loss(self, output: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        """d/2 log(1/n sum (output - target)^2)  (nonlinear.py:139-159)."""
+        n, d = target.shape
+        return 0.5 * d * torch.log(1 / n * torch.sum((output - target) ** 2))
+
+    def minimize(self, max_iter: float, lr: float, lambda1: float, lambda2: float, mu: float, s: float,
+                 lr_decay: float = False, tol: float = 1e-6, pbar=None) -> bool:
+        """Adam on mu * (score + lambda1 |fc1|_1) + h (nonlinear.py:161-236); False when h < 0."""
+        pbar = pbar or _NoBar()
+        self.vprint(f"\nMinimize s={s} -- lr={lr}")
+        optimizer = torch.optim.Adam(self.model.parameters(), lr=lr, betas=(.99, .999), weight_decay=mu * lambda2)
+        if lr_decay is True:
+            scheduler = torch.optim.lr_scheduler.ExponentialLR(optimizer, gamma=0.8)
+        obj_prev = 1e16
+        for i in range(max_iter):
+            optimizer.zero_grad()
+            h_val = self.model.h_func(s)
+            if h_val.item() < 0:
+                self.vprint(f"Found h negative {h_val.item()} at iter {i}")
+                return False
+            X_hat = self.model(self.X)
+            score = self.log_mse_loss(X_hat, self.X)
+            l1_reg = lambda1 * self.model.fc1_l1_reg()
+            obj = mu * (score + l1_reg) + h_val
+            obj.backward()
+            optimizer.step()
+            if lr_decay and (i + 1) % 1000 == 0:
+                scheduler.step()
+            if i % self.checkpoint == 0 or i == max_iter - 1:
+                obj_new = obj.item()
+                self.vprint(f"\nInner iteration {i}")
+                self.vprint(f"\th(W(model)): {h_val.item()}")
+                self.vprint(f"\tscore(model): {obj_new}")
+                if np.abs((obj_prev - obj_new) / obj_prev) <= tol:
+                    pbar.update(max_iter - i)
+                    break
+                obj_prev = obj_new
+            pbar.update(1)
+        return True
+
+    def fit(self, X, lambda1: float = .02, lambda2: float = .005, T: int = 4, mu_init: float = .1,
+            mu_factor: float = .1, s: float = 1.0, warm_iter: int = 5e4, max_iter: int = 8e4, lr: float = .0002,
+            w_threshold: float = 0.3, checkpoint: int = 1000) -> np.ndarray:
+        """The reference's path following (nonlinear.py:238-331); X: (n, d) numpy or torch."""
+        torch.set_default_dtype(self.dtype)
+        if isinstance(X, torch.Tensor):
+            self.X = X.type(self.dtype)
+        elif isinstance(X, np.ndarray):
+            self.X = torch.from_numpy(X).type(self.dtype)
+        else:
+            ValueError("X should be numpy array or torch Tensor.")  # built, not raised (as the reference)
+        self.model.to(self.device)
+        self.X = self.X.to(self.device)
+        self.checkpoint = checkpoint
+        mu = mu_init
+        if type(s) == list:
+            if len(s) < T:
+                self.vprint(f"Length of s is {len(s)}, using last value in s for iteration t >= {len(s)}")
+                s = s + (T - len(s)) * [s[-1]]
+        elif type(s) in [int, float]:
+            s = T * [s]
+        else:
+            ValueError("s should be a list, int, or float.")
+        pbar = _NoBar()
+        for i in range(int(T)):
+            self.vprint(f"\nDagma iter t={i + 1} -- mu: {mu}", 30 * "-")
+            success, s_cur = False, s[i]
+            inner_iter = int(max_iter) if i == T - 1 else int(warm_iter)
+            model_copy = copy.deepcopy(self.model)
+            lr_decay = False
+            while success is False:
+                success = self.minimize(inner_iter, lr, lambda1, lambda2, mu, s_cur, lr_decay, pbar=pbar)
+                if success is False:
+                    self.model.load_state_dict(model_copy.state_dict().copy())
+                    lr *= 0.5
+                    lr_decay = True
+                    if lr < 1e-10:
+                        break
+                    s_cur = 1
+            mu *= mu_factor
+        W_est = self.model.fc1_to_adj()
+        W_est[np.abs(W_est) < w_threshold] = 0
+        return W_est

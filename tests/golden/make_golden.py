@@ -317,6 +317,42 @@ def gen_tcc(X20):
     np.savez_compressed(os.path.join(HERE, "trek_tcc.npz"), **out)
 
 
+def gen_mlp_traj(X20):
+    """DagmaNonlinear.minimize (nonlinear.py:161-236) from fixed parameters, and a short fit,
+    at dims [20, 10, 1]: every parameter after K Adam steps."""
+    import torch
+    from dagma.nonlinear import DagmaMLP, DagmaNonlinear
+    from tests.golden.inputs import mlp_params
+    torch.set_default_dtype(torch.double)
+    d, m1 = X20.shape[1], 10
+    P0 = mlp_params(d, m1)
+    out = {f"p0_{k}": v for k, v in P0.items()}
+
+    def fresh():
+        model = DagmaMLP(dims=[d, m1, 1], bias=True, dtype=torch.double)
+        sd = model.state_dict()
+        with torch.no_grad():
+            for k, v in P0.items():
+                sd[k].copy_(torch.from_numpy(v))
+        dn = DagmaNonlinear(model)
+        dn.X = torch.from_numpy(X20).type(torch.double)
+        dn.checkpoint = 1000
+        return model, dn
+
+    for K in (1, 10, 100):
+        model, dn = fresh()
+        ok = dn.minimize(K, 2e-4, 0.02, 0.005, 0.1, 1.0, pbar=Recorder())
+        out[f"ok_K{K}"] = np.array(ok)
+        for k, v in model.state_dict().items():
+            out[f"K{K}_{k}"] = v.detach().numpy().copy()
+    model, dn = fresh()
+    W = dn.fit(X20, T=2, warm_iter=300, max_iter=500)
+    out["fit_W"] = W
+    for k, v in model.state_dict().items():
+        out[f"fit_{k}"] = v.detach().numpy().copy()
+    np.savez_compressed(os.path.join(HERE, "mlp_traj.npz"), **out)
+
+
 def gen_mlp():
     """DagmaMLP.h_func value and autograd gradient (nonlinear.py:68-86).
 
@@ -357,6 +393,7 @@ def main():
         gen_trek()
         gen_tcc(X20)
         gen_mlp()
+        gen_mlp_traj(X20)
     print("golden fixtures written to", HERE)
 
 
@@ -366,6 +403,6 @@ if __name__ == "__main__":
             X20 = np.load(os.path.join(HERE, "data_d20_n1000_seed0.npz"))["X"]
             for name in sys.argv[1:]:
                 fn = globals()[name]
-                fn(X20) if name == "gen_tcc" else fn()
+                fn(X20) if name in ("gen_tcc", "gen_mlp_traj") else fn()
     else:
         main()

@@ -1,0 +1,63 @@
+"""DagmaNonlinear / DagmaMLP on the GPU (midagma_amd/nonlinear.py: PyTorch-ROCm model and Adam,
+HIP log-det h_func) against the reference's own trajectories (tests/golden/mlp_traj.npz).
+Tolerance: GPU GEMM / reduction order vs the CPU's, 1e-9 relative to the largest parameter."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+KEYS = ["fc1.weight", "fc1.bias", "fc2.0.weight", "fc2.0.bias"]
+
+
+def _dn(f, X):
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    from oracle.mlp_oracle import load_params
+    model = DagmaMLP(dims=[20, 10, 1], bias=True).to("cuda:0")
+    load_params(model, {k: f[f"p0_{k}"] for k in KEYS})
+    dn = DagmaNonlinear(model, device=0)
+    dn.X = torch.from_numpy(X).to("cuda:0")
+    dn.checkpoint = 1000
+    return model, dn
+
+
+@pytest.mark.parametrize("K", [1, 10, 100])
+def test_nonlinear_minimize_matches_reference(golden, K):
+    f = golden("mlp_traj.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"]
+    model, dn = _dn(f, X)
+    assert dn.minimize(K, 2e-4, 0.02, 0.005, 0.1, 1.0) == bool(f[f"ok_K{K}"])
+    sd = model.state_dict()
+    for k in KEYS:
+        ref = f[f"K{K}_{k}"]
+        assert np.abs(sd[k].cpu().numpy() - ref).max() <= 1e-9 * max(1.0, np.abs(ref).max()), k
+
+
+def test_nonlinear_fit_matches_reference(golden):
+    f = golden("mlp_traj.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"]
+    model, dn = _dn(f, X)
+    W = dn.fit(X, T=2, warm_iter=300, max_iter=500)
+    sd = model.state_dict()
+    for k in KEYS:
+        ref = f[f"fit_{k}"]
+        assert np.abs(sd[k].cpu().numpy() - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max()), k
+    np.testing.assert_allclose(W, f["fit_W"], rtol=0, atol=1e-8)
+
+
+def test_nonlinear_h_negative_returns_false():
+    """h < 0 outside the M-matrix domain: minimize returns False before stepping (nonlinear.py:216)."""
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    model = DagmaMLP(dims=[5, 4, 1]).to("cuda:0")
+    with torch.no_grad():
+        model.fc1.weight.fill_(0.6)   # spectral radius of A well above s
+    dn = DagmaNonlinear(model, device=0)
+    dn.X = torch.randn(50, 5, dtype=torch.float64, device="cuda:0")
+    dn.checkpoint = 1000
+    w0 = model.fc1.weight.detach().clone()
+    h = model.h_func(1.0).item()
+    ok = dn.minimize(3, 2e-4, 0.02, 0.005, 0.1, 1.0)
+    assert (h < 0) == (not ok)
+    if not ok:
+        assert torch.equal(w0, model.fc1.weight.detach())
