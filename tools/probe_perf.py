@@ -93,3 +93,5 @@ if __name__ == "__main__":
             trek_case(d, "tcc", K)
     if which in ("all", "data"):
         data_case(1000, 100000, 2, 10)
+    if which == "data250":
+        data_case(1000, 250000, 2, 20)
