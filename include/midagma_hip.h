@@ -168,6 +168,22 @@ int midagma_logdet_inv_dev(const double* A, int64_t d, int64_t lda, double s_dom
 int midagma_sem_linear(const double* W, int64_t d, int64_t row0, int64_t n_rows, int sem_type,
                        const double* noise_scale, uint64_t seed, double* X_dev, int64_t ldx, void* stream);
 
+/* One torch.optim.Adam step (single-tensor algorithm, L2 weight decay wd) on n doubles of
+ * device memory, enqueued on `stream`; coefficients host-rounded as torch computes them:
+ * step_size = lr / (1 - b1^t), w1 = 1 - b1, c2 = 1 - b2, bc2_sqrt = sqrt(1 - b2^t).
+ * Skipped when gate != NULL and *gate < 0 (device scalar: DagmaNonlinear's h, nonlinear.py:216). */
+int midagma_adam_step(double* p, const double* g, double* m, double* v, int64_t n, double step_size, double w1,
+                      double beta2, double c2, double bc2_sqrt, double eps, double wd, const double* gate,
+                      void* stream);
+
+/* The same step with the per-step coefficients from a device table at a device step counter:
+ * step_size = table[2 t], sqrt(1 - b2^t) = table[2 t + 1], t = *counter (graph-replayable);
+ * midagma_counter_advance adds 1 to *counter on `stream`. */
+int midagma_adam_step_table(double* p, const double* g, double* m, double* v, int64_t n, const double* table,
+                            const int64_t* counter, double w1, double beta2, double c2, double eps, double wd,
+                            const double* gate, void* stream);
+int midagma_counter_advance(int64_t* counter, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

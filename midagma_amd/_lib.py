@@ -87,6 +87,9 @@ EXPORTED = {
     "midagma_score_finish": (_int, [_vp, _dp, _dp]),
     "midagma_logdet_inv_dev": (_int, [_vp, _i64, _i64, _d, _vp, _vp, _i64, _vp]),
     "midagma_sem_linear": (_int, [_dp, _i64, _i64, _i64, _int, _dp, C.c_uint64, _vp, _i64, _vp]),
+    "midagma_adam_step": (_int, [_vp, _vp, _vp, _vp, _i64, _d, _d, _d, _d, _d, _d, _d, _vp, _vp]),
+    "midagma_adam_step_table": (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _d, _d, _d, _d, _d, _vp, _vp]),
+    "midagma_counter_advance": (_int, [_vp, _vp]),
 }
 
 _lock = threading.Lock()

@@ -113,6 +113,18 @@ struct TccWork {
 void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, const TccWork& w, const State* st,
                      double* Gtrek, hipStream_t stream);
 
+// --- adam.hip ---------------------------------------------------------------
+struct AdamCoef {  // host-rounded as torch.optim.Adam computes them in Python floats
+  double step_size, w1, beta2, c2, bc2_sqrt, eps, wd;
+};
+// one torch-Adam step on n doubles, skipped when gate != nullptr and *gate < 0
+void launch_adam_gated(double* p, const double* g, double* m, double* v, int64_t n, const AdamCoef& c,
+                       const double* gate, hipStream_t stream);
+// the same with step_size = table[2 t], sqrt(1 - b2^t) = table[2 t + 1], t = *counter
+void launch_adam_gated_table(double* p, const double* g, double* m, double* v, int64_t n, const AdamCoef& c,
+                             const double* table, const int64_t* counter, const double* gate, hipStream_t stream);
+void launch_counter_advance(int64_t* counter, hipStream_t stream);
+
 // --- sem.hip ----------------------------------------------------------------
 // Parents (CSR over columns of W, ascending) and topological levels of a weighted DAG.
 struct SemGraph {

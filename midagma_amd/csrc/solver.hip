@@ -1307,3 +1307,37 @@ extern "C" int midagma_sem_linear(const double* W, int64_t d, int64_t row0, int6
     return MIDAGMA_OK;
   });
 }
+
+// ---------------------------------------------------------------------------
+// Gated Adam step (adam.hip) for DagmaNonlinear on torch tensors
+extern "C" int midagma_adam_step(double* p, const double* g, double* m, double* v, int64_t n, double step_size,
+                                 double w1, double beta2, double c2, double bc2_sqrt, double eps, double wd,
+                                 const double* gate, void* stream) {
+  if (!p || !g || !m || !v || n < 0) return fail(nullptr, MIDAGMA_E_ARG, "adam_step: bad arguments");
+  if (n == 0) return MIDAGMA_OK;
+  return guarded(nullptr, [&] {
+    launch_adam_gated(p, g, m, v, n, AdamCoef{step_size, w1, beta2, c2, bc2_sqrt, eps, wd}, gate,
+                      reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_adam_step_table(double* p, const double* g, double* m, double* v, int64_t n,
+                                       const double* table, const int64_t* counter, double w1, double beta2,
+                                       double c2, double eps, double wd, const double* gate, void* stream) {
+  if (!p || !g || !m || !v || !table || !counter || n < 0) return fail(nullptr, MIDAGMA_E_ARG, "adam_step_table: bad arguments");
+  if (n == 0) return MIDAGMA_OK;
+  return guarded(nullptr, [&] {
+    launch_adam_gated_table(p, g, m, v, n, AdamCoef{0.0, w1, beta2, c2, 1.0, eps, wd}, table, counter, gate,
+                            reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_counter_advance(int64_t* counter, void* stream) {
+  if (!counter) return fail(nullptr, MIDAGMA_E_ARG, "counter_advance: null counter");
+  return guarded(nullptr, [&] {
+    launch_counter_advance(counter, reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}

@@ -17,6 +17,7 @@ from __future__ import annotations
 import copy
 import ctypes as C
 import math
+import os
 import typing
 
 import numpy as np
@@ -133,6 +134,10 @@ class DagmaMLP(nn.Module):
         return torch.sqrt(self._adjacency_sq()).cpu().numpy()
 
 
+class _GraphCaptureError(RuntimeError):
+    pass
+
+
 class _NoBar:
     def update(self, k=1):
         pass
@@ -144,11 +149,13 @@ class DagmaNonlinear:
     HIP log-det in ``model.h_func``.  ``device``: HIP ordinal (default: the current device)."""
 
     def __init__(self, model: nn.Module, verbose: bool = False, dtype: torch.dtype = torch.double, *,
-                 device: typing.Optional[int] = None):
+                 device: typing.Optional[int] = None, graph: bool = True):
         self.vprint = print if verbose else (lambda *a, **k: None)
         self.model = model
         self.dtype = dtype
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        # one Adam step captured once per minimize call and replayed (hipGraph); False: eager steps
+        self.graph = graph and not os.environ.get("MIDAGMA_NO_GRAPH")
 
     def log_mse_loss(self, output: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         """d/2 log(1/n sum (output - target)^2)  (nonlinear.py:139-159)."""
@@ -157,31 +164,57 @@ class DagmaNonlinear:
 
     def minimize(self, max_iter: float, lr: float, lambda1: float, lambda2: float, mu: float, s: float,
                  lr_decay: float = False, tol: float = 1e-6, pbar=None) -> bool:
-        """Adam on mu * (score + lambda1 |fc1|_1) + h (nonlinear.py:161-236); False when h < 0."""
+        """Adam on mu * (score + lambda1 |fc1|_1) + h (nonlinear.py:161-236); False when h < 0.
+
+        The step is torch.optim.Adam's single-tensor algorithm (betas .99/.999, eps 1e-8, L2
+        weight decay mu * lambda2) in one HIP kernel per parameter (`midagma_adam_step`), gated
+        on the device value of h: the reference returns before stepping when h < 0, so a
+        negative h freezes the parameters (and h) and is seen on the host at the next
+        checkpoint instead of through a host read every step."""
         pbar = pbar or _NoBar()
         self.vprint(f"\nMinimize s={s} -- lr={lr}")
-        optimizer = torch.optim.Adam(self.model.parameters(), lr=lr, betas=(.99, .999), weight_decay=mu * lambda2)
-        if lr_decay is True:
-            scheduler = torch.optim.lr_scheduler.ExponentialLR(optimizer, gamma=0.8)
+        if self.graph and max_iter > 2:
+            try:
+                return self._minimize_graph(max_iter, lr, lambda1, lambda2, mu, s, lr_decay, tol, pbar)
+            except _GraphCaptureError as e:  # not capturable here: the same steps, launched eagerly
+                self.vprint(f"hipGraph capture unavailable ({e}); eager steps")
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        exp_avg = [torch.zeros_like(p) for p in params]
+        exp_avg_sq = [torch.zeros_like(p) for p in params]
+        beta1, beta2, eps, wd = 0.99, 0.999, 1e-8, mu * lambda2
+        L = _lib.lib()
+        lr_cur = lr
         obj_prev = 1e16
         for i in range(max_iter):
-            optimizer.zero_grad()
+            for p in params:
+                p.grad = None
             h_val = self.model.h_func(s)
-            if h_val.item() < 0:
-                self.vprint(f"Found h negative {h_val.item()} at iter {i}")
-                return False
             X_hat = self.model(self.X)
             score = self.log_mse_loss(X_hat, self.X)
             l1_reg = lambda1 * self.model.fc1_l1_reg()
             obj = mu * (score + l1_reg) + h_val
             obj.backward()
-            optimizer.step()
+            step = i + 1
+            bc1 = 1 - beta1 ** step
+            bc2 = 1 - beta2 ** step
+            stream = torch.cuda.current_stream(h_val.device).cuda_stream
+            gate = C.c_void_p(h_val.data_ptr())
+            for p, m, v in zip(params, exp_avg, exp_avg_sq):
+                g = p.grad.contiguous()
+                _lib.check(L.midagma_adam_step(C.c_void_p(p.data_ptr()), C.c_void_p(g.data_ptr()),
+                                               C.c_void_p(m.data_ptr()), C.c_void_p(v.data_ptr()), p.numel(),
+                                               lr_cur / bc1, 1 - beta1, beta2, 1 - beta2, bc2 ** 0.5, eps, wd, gate,
+                                               C.c_void_p(stream) if stream else None), None, "adam_step")
             if lr_decay and (i + 1) % 1000 == 0:
-                scheduler.step()
+                lr_cur = lr_cur * 0.8   # ExponentialLR(gamma=0.8)
             if i % self.checkpoint == 0 or i == max_iter - 1:
+                h_host = h_val.item()
+                if h_host < 0:
+                    self.vprint(f"Found h negative {h_host} at or before iter {i}")
+                    return False
                 obj_new = obj.item()
                 self.vprint(f"\nInner iteration {i}")
-                self.vprint(f"\th(W(model)): {h_val.item()}")
+                self.vprint(f"\th(W(model)): {h_host}")
                 self.vprint(f"\tscore(model): {obj_new}")
                 if np.abs((obj_prev - obj_new) / obj_prev) <= tol:
                     pbar.update(max_iter - i)
@@ -189,6 +222,89 @@ class DagmaNonlinear:
                 obj_prev = obj_new
             pbar.update(1)
         return True
+
+    def _minimize_graph(self, max_iter, lr, lambda1, lambda2, mu, s, lr_decay, tol, pbar) -> bool:
+        """`minimize` with one step captured into a hipGraph and replayed: the same kernels as the
+        eager loop, the per-step Adam coefficients (lr schedule and bias corrections, host-rounded
+        as torch computes them) from a device table at a device step counter."""
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        exp_avg = [torch.zeros_like(p) for p in params]
+        exp_avg_sq = [torch.zeros_like(p) for p in params]
+        beta1, beta2, eps, wd = 0.99, 0.999, 1e-8, mu * lambda2
+        table = np.empty(2 * int(max_iter))
+        lr_cur = lr
+        for i in range(int(max_iter)):
+            step = i + 1
+            table[2 * i] = lr_cur / (1 - beta1 ** step)
+            table[2 * i + 1] = (1 - beta2 ** step) ** 0.5
+            if lr_decay and (i + 1) % 1000 == 0:
+                lr_cur = lr_cur * 0.8
+        dev = params[0].device
+        table_d = torch.from_numpy(table).to(dev)
+        counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        no_step = torch.full((), -1.0, dtype=torch.float64, device=dev)
+        L = _lib.lib()
+
+        def body(gate):
+            for p in params:
+                p.grad = None
+            h_val = self.model.h_func(s)
+            obj = mu * (self.log_mse_loss(self.model(self.X), self.X) + lambda1 * self.model.fc1_l1_reg()) + h_val
+            obj.backward()
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            st = C.c_void_p(stream) if stream else None
+            g_ptr = C.c_void_p((h_val if gate is None else gate).data_ptr())
+            for p, m, v in zip(params, exp_avg, exp_avg_sq):
+                g = p.grad.contiguous()
+                _lib.check(L.midagma_adam_step_table(C.c_void_p(p.data_ptr()), C.c_void_p(g.data_ptr()),
+                                                     C.c_void_p(m.data_ptr()), C.c_void_p(v.data_ptr()), p.numel(),
+                                                     C.c_void_p(table_d.data_ptr()),
+                                                     C.c_void_p(counter.data_ptr()), 1 - beta1, beta2, 1 - beta2,
+                                                     eps, wd, g_ptr, st), None, "adam_step_table")
+            _lib.check(L.midagma_counter_advance(C.c_void_p(counter.data_ptr()), st), None, "counter_advance")
+            return h_val, obj
+
+        try:
+            # warm-up on a side stream with the step gated off: lazy allocations (the log-det
+            # workspace, BLAS handles) happen outside the capture and the parameters stay put
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    body(no_step)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            counter.zero_()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                h_static, obj_static = body(None)
+        except Exception as e:  # noqa: BLE001
+            for p in params:
+                p.grad = None
+            raise _GraphCaptureError(repr(e)) from e
+        obj_prev = 1e16
+        try:
+            for i in range(max_iter):
+                graph.replay()
+                if i % self.checkpoint == 0 or i == max_iter - 1:
+                    h_host = h_static.item()
+                    if h_host < 0:
+                        self.vprint(f"Found h negative {h_host} at or before iter {i}")
+                        return False
+                    obj_new = obj_static.item()
+                    self.vprint(f"\nInner iteration {i}")
+                    self.vprint(f"\th(W(model)): {h_host}")
+                    self.vprint(f"\tscore(model): {obj_new}")
+                    if np.abs((obj_prev - obj_new) / obj_prev) <= tol:
+                        pbar.update(max_iter - i)
+                        break
+                    obj_prev = obj_new
+                pbar.update(1)
+            return True
+        finally:
+            torch.cuda.current_stream(dev).synchronize()
+            for p in params:
+                p.grad = None
+            del graph
 
     def fit(self, X, lambda1: float = .02, lambda2: float = .005, T: int = 4, mu_init: float = .1,
             mu_factor: float = .1, s: float = 1.0, warm_iter: int = 5e4, max_iter: int = 8e4, lr: float = .0002,
