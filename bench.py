@@ -6,11 +6,15 @@ SEM, l2 loss, "data mode": X row-sharded over the N ranks, each step computes
 Z_k = X_k^T (X_k (I - W)) on MFMA, all-reduces Z over RCCL/xGMI, then runs the
 replicated log-det/inverse and fused Adam update.  Strong scaling (n fixed).
 
-On rank 0 at N=1 it also reports
-  * cov_mode : BASELINE config 2 (d=1000, n=1e4), the reference's own algorithm
-    (cov = X^T X / n once, O(d^3) per step) on one GPU,
-  * cpu_baseline : the reference algorithm on the host cores (CPU oracle
-    restatement, bit-identical to the reference at 1 thread), timed in this run.
+On rank 0 at N=1 it also reports (same run, same box)
+  * cpu_baseline : the workload's own math (data-mode step) on the host cores, CPU oracle;
+  * cpu_reference_algorithm / cov_mode : BASELINE config 2 (d=1000, n=1e4) with the
+    reference's own algorithm (cov = X^T X / n once, O(d^3) per step) on the CPU and the GPU;
+  * full_fit : DagmaLinear('l2').fit defaults at config 2, wall-clock (the metric's 2nd half);
+  * config3 : d=5000, n=5e4 cov mode, with its CPU reference-algorithm baseline;
+  * config5 : DagmaNonlinear Adam steps at dims [200, 10, 1], n=1000, with its CPU oracle;
+  * sem_generator : the GPU SEM generator's time for this rank's X shard;
+  * roofline : the dominant data-mode GEMM vs the FP64 MFMA peak, PMC HBM traffic.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -39,8 +43,8 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", choices=["data", "cov"], default="data")
     p.add_argument("--d", type=int, default=1000)
     p.add_argument("--n", type=int, default=1_000_000)
