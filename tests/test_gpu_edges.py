@@ -1,0 +1,69 @@
+"""Edge sizes of the GPU inner loop against the oracle: tiny d (1, 2, 3), the padding and
+path boundaries (D = round_up(d, 64) up to 192, round_up(d, 128) above; the two-level
+blocked inverse from D >= 256 with B2 = 256 or 128), and data mode with a row count that is
+not a multiple of the 128-row GEMM tile."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from midagma_amd.simulate import make_dataset  # noqa: E402
+from oracle.dagma_oracle import LinearOracle  # noqa: E402
+
+
+def _case(d, n, seed=3):
+    if d <= 3:
+        rng = np.random.default_rng(seed)
+        X = rng.standard_normal((n, d))
+        if d > 1:
+            X[:, 1] += 0.8 * X[:, 0]
+        return X
+    X, _, _ = make_dataset(d, n, seed=seed)
+    return X
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 63, 65, 191, 192, 193, 255, 257, 384])
+def test_cov_minimize_edge_sizes(d):
+    from midagma_amd.solver import HipSolver
+    X = _case(d, max(60, 2 * d + 10))
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 10)
+    K = 45
+    s = HipSolver(d, "l2", "cov", device=0)
+    s.set_cov(o.cov)
+    W = np.zeros((d, d))
+    res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=10, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert res.iters == tr.iters == K
+    assert np.abs(W - Wr).max() <= 1e-9
+    assert [c.iter for c in res.checkpoints] == [r["iter"] for r in tr.records]
+    for c, r in zip(res.checkpoints, tr.records):
+        assert abs(c.obj - r["obj_total"]) <= 1e-10 * abs(r["obj_total"]) + 1e-14
+    s.close()
+
+
+@pytest.mark.parametrize("d,n", [(2, 77), (20, 1001), (130, 300)])
+def test_data_mode_ragged_rows(d, n):
+    """Data mode with n not a multiple of 128: the padded rows are zero and drop out."""
+    from midagma_amd.solver import HipSolver
+    X = _case(d, n)
+    X = X - X.mean(axis=0, keepdims=True)
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 10)
+    s = HipSolver(d, "l2", "data", device=0)
+    s.set_data(X, n_global=n)
+    W = np.zeros((d, d))
+    res = s.minimize(W, 1.0, 30, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=10)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, 30, 1.0, 3e-4, tol=-1.0)
+    assert res.iters == tr.iters
+    assert np.abs(W - Wr).max() <= 1e-9
+    s.close()
+
+
+def test_dagma_linear_fit_tiny():
+    from midagma_amd import DagmaLinear
+    X = _case(2, 200)
+    W = DagmaLinear("l2").fit(X, lambda1=0.02, T=2, warm_iter=500, max_iter=800)
+    assert W.shape == (2, 2) and np.isfinite(W).all() and W[0, 0] == 0 and W[1, 1] == 0
