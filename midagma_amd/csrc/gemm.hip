@@ -290,6 +290,231 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
 
 constexpr size_t kGemm128Lds = 4 * G_IMG * sizeof(double);
 
+// ---- pipelined 128 x 128 tile GEMM (data-mode and cov-mode score GEMMs) --------------------
+// The A tile goes through a double-buffered LDS image shared by the 4 waves; each wave owns all
+// 128 rows x 32 columns (8 x 2 accumulators) and loads its B values straight into MFMA operand
+// registers.  The software pipeline follows the vendor DGEMM's (measured: rocBLAS 94% on the
+// X(I-W) shape where the 2 x 2-wave gemm128 above reached 83%):
+//   * k is permuted inside a 16-deep tile: lane quarter kq takes k = 4 kq + kk at k-step kk, so
+//     one lane's B values of a k-step sit in one row of B, and its two columns 2r, 2r+1 (output
+//     column c of accumulator j is n = 2c + j) are one 16-B load;
+//   * A image [k][m] with row stride 132 doubles: rows 4 apart differ by 16 mod 32 doubles, so
+//     the two kq halves of a 32-lane group use disjoint banks (conflict-free fragment reads);
+//   * fragments are read one k-step ahead, interleaved with the MFMAs by sched_group_barrier;
+//     the next tile is staged into the other LDS buffer during k-step 1 from registers loaded
+//     one tile earlier; one barrier per tile, before the last k-step, so the next tile's first
+//     fragments are read while that k-step's MFMAs run;
+//   * B row kk of the next tile is reloaded into the same registers right after k-step kk's
+//     MFMAs are issued (no loop-carried register copies, which made hipcc drain the loads).
+// AMODE 1: A stored [k][m] (lda), AMODE 0: A stored [m][k].  BMODE B_IMINUS forms I - B in
+// registers.  Split-K slices as gemm128.  Measured at n = 1e6, d = 1000 (MI355X): X(I-W) from
+// X^T 29.1 ms (B = I - W pre-formed, 91.7% of FP64 peak), X^T Y split 16 28.7 ms (92.8%).
+constexpr int P_S = 132;
+constexpr int P_IMG = 16 * P_S;
+constexpr size_t kGemmPipeLds = 2 * P_IMG * sizeof(double);
+
+template <int AMODE, int BMODE, int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64_t kslice, int tiles_m, int tiles_n,
+                                                                const double* __restrict__ A, int64_t lda,
+                                                                const double* __restrict__ B, int64_t ldb,
+                                                                double* __restrict__ C, int64_t ldc,
+                                                                int64_t slice_stride, double* __restrict__ loss_part,
+                                                                int64_t m_valid, int64_t n_valid,
+                                                                const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_slice = tiles_m * tiles_n;
+  const int z = t / per_slice, rem = t % per_slice;
+  const int bm = rem / tiles_n, bn = rem % tiles_n;
+  const int64_t m0 = (int64_t)bm * 128, n0 = (int64_t)bn * 128;
+  const int64_t k_begin = (int64_t)z * kslice;
+  const int64_t k_end = (k_begin + kslice < K) ? k_begin + kslice : K;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, kq = lane >> 4;
+  const int64_t nw = n0 + 32 * w;
+
+  // A staging, 4 x 16 B per thread per tile.  AMODE 1: item i_ -> k = i_ >> 6, m = 2 (i_ & 63)
+  // (+1), one ds_write_b128.  AMODE 0: item i_ -> k = 2 (i_ >> 7) (+1), m = i_ & 127, two
+  // ds_write_b64 (consecutive lanes on consecutive m: conflict-free).
+  const double* Ablk = AMODE ? A + m0 : A + m0 * lda;
+  int offA[4], ldsA[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int i_ = it * NTHREADS + tid;
+    if (AMODE) {
+      offA[it] = (i_ >> 6) * (int)lda + 2 * (i_ & 63);
+      ldsA[it] = (i_ >> 6) * P_S + 2 * (i_ & 63);
+    } else {
+      offA[it] = (i_ & 127) * (int)lda + 2 * (i_ >> 7);
+      ldsA[it] = 2 * (i_ >> 7) * P_S + (i_ & 127);
+    }
+  }
+  const int64_t a_kstride = AMODE ? lda : 1;
+  const double* Bw = B + (int64_t)(4 * kq) * ldb + nw + 2 * r;
+  const int fo = 4 * kq * P_S + r;  // fragment of block i at k-step kk: fo + kk P_S + 16 i
+
+  double2 ra0, ra1, ra2, ra3;
+  double2 fb[4];
+  double fa0[8], fa1[8];
+#define GP_LOADA(KT)                                                                              \
+  {                                                                                               \
+    const double* ap_ = Ablk + (KT) * a_kstride;                                                  \
+    ra0 = *reinterpret_cast<const double2*>(ap_ + offA[0]);                                       \
+    ra1 = *reinterpret_cast<const double2*>(ap_ + offA[1]);                                       \
+    ra2 = *reinterpret_cast<const double2*>(ap_ + offA[2]);                                       \
+    ra3 = *reinterpret_cast<const double2*>(ap_ + offA[3]);                                       \
+  }
+#define GP_LOADB1(KT, KK) fb[KK] = *reinterpret_cast<const double2*>(Bw + ((KT) + (KK)) * ldb);
+#define GP_STA1(AS, I, RA)                                                                        \
+  if (AMODE) {                                                                                    \
+    *reinterpret_cast<double2*>((AS) + ldsA[I]) = RA;                                             \
+  } else {                                                                                        \
+    (AS)[ldsA[I]] = RA.x;                                                                         \
+    (AS)[ldsA[I] + P_S] = RA.y;                                                                   \
+  }
+#define GP_STOREA(AS)                                                                             \
+  {                                                                                               \
+    GP_STA1(AS, 0, ra0) GP_STA1(AS, 1, ra1) GP_STA1(AS, 2, ra2) GP_STA1(AS, 3, ra3)               \
+  }
+#define GP_FRAG(DST, AS, KK)                                                                      \
+  {                                                                                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) DST[i_] = (AS)[fo + (KK) * P_S + 16 * i_];   \
+  }
+#define GP_MMA(FA, KT, KK)                                                                        \
+  {                                                                                               \
+    double b0_ = fb[KK].x, b1_ = fb[KK].y;                                                        \
+    if (BMODE == B_IMINUS) {                                                                      \
+      const int64_t kg_ = (KT) + 4 * kq + (KK), ng_ = nw + 2 * r;                                 \
+      b0_ = (kg_ == ng_ ? 1.0 : 0.0) - b0_;                                                       \
+      b1_ = (kg_ == ng_ + 1 ? 1.0 : 0.0) - b1_;                                                   \
+    }                                                                                             \
+    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                            \
+      acc[i_][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(FA[i_], b0_, acc[i_][0], 0, 0, 0);         \
+      acc[i_][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(FA[i_], b1_, acc[i_][1], 0, 0, 0);         \
+    }                                                                                             \
+  }
+  // instruction interleave of one k-step: its 8 fragment reads (for the next k-step) between the
+  // first MFMAs, then NW LDS stores and NV global loads between the following ones
+#define GP_SCHED(NW, NV)                                                                          \
+  {                                                                                               \
+    _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_) {                                            \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                          \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                          \
+    }                                                                                             \
+    _Pragma("unroll") for (int q_ = 0; q_ < (NW); ++q_) {                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                          \
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                                          \
+    }                                                                                             \
+    _Pragma("unroll") for (int q_ = 0; q_ < (NV); ++q_) {                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                          \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                          \
+    }                                                                                             \
+    __builtin_amdgcn_sched_group_barrier(0x008, 16 - 8 - (NW) - (NV), 0);                        \
+  }
+
+  dbl4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  double* As0 = smem;
+  double* As1 = smem + P_IMG;
+  if (k_begin < k_end) {
+    GP_LOADA(k_begin)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) GP_LOADB1(k_begin, q)
+    GP_STOREA(As0)
+    GP_LOADA((k_begin + 16 < k_end) ? k_begin + 16 : k_begin)
+    __syncthreads();
+    GP_FRAG(fa0, As0, 0)
+  }
+  __builtin_amdgcn_s_setprio(3);
+  for (int64_t kt = k_begin; kt < k_end; kt += 16) {
+    const int64_t k1 = kt + 16 < k_end ? kt + 16 : kt;
+    const int64_t k2 = kt + 32 < k_end ? kt + 32 : k1;
+    GP_FRAG(fa1, As0, 1)  // k-step 0
+    GP_MMA(fa0, kt, 0)
+    GP_LOADB1(k1, 0)
+    GP_SCHED(0, 1)
+    __builtin_amdgcn_sched_barrier(0);
+    GP_STOREA(As1)  // k-step 1: stage the next tile, then load the one after it
+    GP_FRAG(fa0, As0, 2)
+    GP_MMA(fa1, kt, 1)
+    GP_LOADB1(k1, 1)
+    GP_LOADA(k2)
+    GP_SCHED(AMODE ? 4 : 8, 5)
+    __builtin_amdgcn_sched_barrier(0);
+    GP_FRAG(fa1, As0, 3)  // k-step 2
+    GP_MMA(fa0, kt, 2)
+    GP_LOADB1(k1, 2)
+    GP_SCHED(0, 1)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __syncthreads();
+    __builtin_amdgcn_s_setprio(3);
+    GP_FRAG(fa0, As1, 0)  // k-step 3, reading the next tile's first fragments meanwhile
+    GP_MMA(fa1, kt, 3)
+    GP_LOADB1(k1, 3)
+    GP_SCHED(0, 1)
+    __builtin_amdgcn_sched_barrier(0);
+    double* tmp = As0;
+    As0 = As1;
+    As1 = tmp;
+  }
+  __builtin_amdgcn_s_setprio(0);
+#undef GP_LOADA
+#undef GP_LOADB1
+#undef GP_STA1
+#undef GP_STOREA
+#undef GP_FRAG
+#undef GP_MMA
+#undef GP_SCHED
+  double* Ct = C + (int64_t)z * slice_stride;
+  if (EPI == EPI_STORE) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int64_t row = m0 + 16 * i + acc_row(lane, tt);
+        const int64_t col = nw + 2 * acc_col(lane);
+        *reinterpret_cast<double2*>(Ct + row * ldc + col) = double2{acc[i][0][tt], acc[i][1][tt]};
+      }
+    return;
+  }
+  // EPI_SIGMOID: C = expit(acc); loss partial sum(logaddexp(0, acc) - X * acc) over the valid
+  // block, X = op(A) at (row, col)
+  const bool want_loss = loss_part != nullptr && (st == nullptr || st->ckpt_pending);
+  double part = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int64_t row = m0 + 16 * i + acc_row(lane, tt);
+      const int64_t col = nw + 2 * acc_col(lane);
+      double2 o;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const double v = acc[i][j][tt];
+        if (want_loss && row < m_valid && col + j < n_valid)
+          part += logaddexp0(v) - (AMODE ? A[(col + j) * lda + row] : A[row * lda + col + j]) * v;
+        (j ? o.y : o.x) = 1.0 / (1.0 + exp(-v));
+      }
+      *reinterpret_cast<double2*>(Ct + row * ldc + col) = o;
+    }
+  if (!want_loss) return;
+  __syncthreads();
+  double* red = smem;
+  red[tid] = part;
+  __syncthreads();
+  for (int s2 = NTHREADS / 2; s2 > 0; s2 >>= 1) {
+    if (tid < s2) red[tid] += red[tid + s2];
+    __syncthreads();
+  }
+  if (tid == 0) loss_part[blockIdx.x] = red[0];
+}
+
+
 constexpr size_t kGemmLds = (2 * 64 * SB) * sizeof(double);
 
 template <bool AT, int BM, int EP>
@@ -304,7 +529,19 @@ static void set_attr128() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemm128Lds));
 }
 
+template <int AM, int BM, int EP>
+static void set_attr_pipe() {
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pipe_kernel<AM, BM, EP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmPipeLds));
+}
+
 void gemm_setup_attributes() {
+  set_attr_pipe<1, B_PLAIN, EPI_STORE>();
+  set_attr_pipe<1, B_IMINUS, EPI_STORE>();
+  set_attr_pipe<0, B_PLAIN, EPI_STORE>();
+  set_attr_pipe<0, B_IMINUS, EPI_STORE>();
+  set_attr_pipe<1, B_PLAIN, EPI_SIGMOID>();
+  set_attr_pipe<0, B_PLAIN, EPI_SIGMOID>();
   set_attr128<false, B_PLAIN, EPI_STORE>();
   set_attr128<false, B_IMINUS, EPI_STORE>();
   set_attr128<true, B_PLAIN, EPI_STORE>();
@@ -323,7 +560,38 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
                  int64_t ldb, GemmB bmode, double* C, int64_t ldc, GemmEpi epi, int split, int64_t slice_stride,
                  double* loss_part, int64_t m_valid, int64_t n_valid, const State* st, hipStream_t stream) {
   if (M % 64 || N % 64 || K % 64 || split < 1) throw std::invalid_argument("launch_gemm: bad shape");
-  static const bool force64 = getenv("MIDAGMA_EXP_GEMM64") != nullptr;  // experiment knob
+  static const bool force64 = getenv("MIDAGMA_EXP_GEMM64") != nullptr;  // experiment knobs
+  static const bool no_pipe = getenv("MIDAGMA_EXP_NO_PIPE") != nullptr;
+  if (M % 128 == 0 && N % 128 == 0 && K % 16 == 0 && !force64 && !no_pipe &&
+      (epi == EPI_STORE || (epi == EPI_SIGMOID && split == 1 && bmode == B_PLAIN))) {
+    const int64_t ktiles16 = K / 16;
+    const int64_t per16 = (ktiles16 + split - 1) / split;
+    const int nsplit = (int)((ktiles16 + per16 - 1) / per16);
+    const int tm = (int)(M / 128), tn = (int)(N / 128);
+    const int64_t nwg = (int64_t)tm * tn * nsplit;
+    const int64_t kslice = per16 * 16;
+#define MIDAGMA_GEMMP(AM, BM, EP)                                                                         \
+  hipLaunchKernelGGL((gemm_pipe_kernel<AM, BM, EP>), dim3((unsigned)nwg), dim3(NTHREADS), kGemmPipeLds, stream, K, \
+                     kslice, tm, tn, A, lda, B, ldb, C, ldc, slice_stride, loss_part, m_valid, n_valid, st)
+    if (epi == EPI_SIGMOID) {
+      if (a_trans && N != K) throw std::invalid_argument("launch_gemm: sigmoid form");
+      if (a_trans)
+        MIDAGMA_GEMMP(1, B_PLAIN, EPI_SIGMOID);
+      else
+        MIDAGMA_GEMMP(0, B_PLAIN, EPI_SIGMOID);
+    } else if (a_trans && bmode == B_PLAIN) {
+      MIDAGMA_GEMMP(1, B_PLAIN, EPI_STORE);
+    } else if (a_trans) {
+      MIDAGMA_GEMMP(1, B_IMINUS, EPI_STORE);
+    } else if (bmode == B_PLAIN) {
+      MIDAGMA_GEMMP(0, B_PLAIN, EPI_STORE);
+    } else {
+      MIDAGMA_GEMMP(0, B_IMINUS, EPI_STORE);
+    }
+#undef MIDAGMA_GEMMP
+    HIP_TRY(hipGetLastError());
+    return;
+  }
   if (M % 128 == 0 && N % 128 == 0 && K % 128 == 0 && !force64) {
     const int64_t ktiles16 = K / G_BK;
     const int64_t per16 = (ktiles16 + split - 1) / split;

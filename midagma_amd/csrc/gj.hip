@@ -48,7 +48,7 @@ template <bool SQUARE>
 __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __restrict__ X, int64_t ldx,
                                                             double* __restrict__ At, int64_t D, int64_t d,
                                                             double s_arg, const Params* __restrict__ pr,
-                                                            const State* __restrict__ st) {
+                                                            const State* __restrict__ st, double* __restrict__ IW) {
   if (st && st->status != ST_RUNNING) return;
   // s comes from device Params when given: graph replays must see each call's s
   const double s = pr ? pr->s : s_arg;
@@ -61,13 +61,15 @@ __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __rest
     const int r = e >> 6, c = e & 63;
     const int64_t I = (int64_t)bi * 64 + r, J = (int64_t)bj * 64 + c;
     double v;
+    const double x = (I < d && J < d) ? X[I * ldx + J] : 0.0;
     if (I < d && J < d) {
-      const double x = X[I * ldx + J];
       const double f = SQUARE ? x * x : x;
       v = (I == J ? s : 0.0) - f;
     } else {
       v = (I == J) ? 1.0 : 0.0;
     }
+    // I - X, the B operand of the data-mode score GEMM X (I - W) (identity in the padding)
+    if (IW) IW[I * D + J] = (I == J ? 1.0 : 0.0) - x;
     tile[c][r] = v;
   }
   __syncthreads();
@@ -356,13 +358,13 @@ extern "C" int midagma_debug_stamps(unsigned long long* out) {
 #endif
 
 void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int64_t D, int64_t d, double s,
-                     const Params* pr, const State* st, hipStream_t stream) {
+                     const Params* pr, const State* st, hipStream_t stream, double* IW) {
   const int K = (int)(D / 64);
   dim3 grid(K, K);
   if (square)
-    hipLaunchKernelGGL(build_at_kernel<true>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, pr, st);
+    hipLaunchKernelGGL(build_at_kernel<true>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, pr, st, IW);
   else
-    hipLaunchKernelGGL(build_at_kernel<false>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, pr, st);
+    hipLaunchKernelGGL(build_at_kernel<false>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, pr, st, IW);
   HIP_TRY(hipGetLastError());
 }
 

@@ -30,8 +30,9 @@ struct GJWork {
 void gj_setup_attributes();
 // At = (s*I - f(X))^T on the logical d x d block, identity padding; f = x^2 if square.
 // s is read from pr->s when pr != nullptr (graph-replayed slots), else the argument.
+// IW (nullable, D x D): also writes I - X (identity padding).
 void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int64_t D, int64_t d, double s,
-                     const Params* pr, const State* st, hipStream_t stream);
+                     const Params* pr, const State* st, hipStream_t stream, double* IW = nullptr);
 // In place: A <- inv(A) (unpivoted blocked Gauss-Jordan) on the D x D matrix at A with
 // leading dimension lda (D multiple of 32), pivot logs into w.pivlog.
 void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);

@@ -77,6 +77,7 @@ struct midagma_solver {
   // X^T (D x n_pad), the xw GEMM's A operand in the m-contiguous layout (the X^T Y GEMM reads
   // X itself that way); kept when the device has the room (MIDAGMA_NO_XT disables it)
   DevBuf XT;
+  DevBuf IW;  // I - W of the slot, written by build_at for the data-mode X (I - W) GEMM
   bool use_xt = false;
   const double* xw_a() const { return use_xt ? XT.p : X.p; }
   int64_t xw_lda() const { return use_xt ? n_pad : D; }
@@ -106,7 +107,7 @@ struct midagma_solver {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2,
-                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT})
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW})
       b->release();
     for (DevBuf& b : tbufs) b.release();
     for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices, &cA, &cMi, &cS, &cvec, &cpart, &cP, &cR, &cC}) b->release();
@@ -148,10 +149,10 @@ struct midagma_solver {
   void enqueue_part1(bool fast = false) {
     if (blocked()) {
       launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
-                      stream);
+                      stream, IW.p);
       launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream);
     } else {
-      launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, 0.0, d_params, d_state, stream);
+      launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, 0.0, d_params, d_state, stream, IW.p);
       launch_gj_inverse(Mt.p, D, D, gj(), d_state, stream);
     }
     // (a fork/join of the score GEMMs onto a second stream inside the graph measured slower:
@@ -161,7 +162,7 @@ struct midagma_solver {
       // for fused_update to sum (its only reader there)
       enqueue_cov_gemm(covs.p, W.p, zbuf, d_state, /*sum=*/!(fast && blocked()));
     } else {
-      enqueue_data_partial(W.p, d_state);
+      enqueue_data_partial(W.p, d_state, IW.p);
     }
     // trek regularizer of this slot's W (linear.py:251-258): every slot in 'opt' mode; in 'log'
     // mode only checkpoint slots, which are never fast slots
@@ -186,9 +187,11 @@ struct midagma_solver {
   }
 
   // Z_k = X_k^T (X_k (I - W))  (l2)   or   X_k^T expit(X_k W)  (logistic, + loss partial)
-  void enqueue_data_partial(const double* Wp, const State* st) {
+  // iw (nullable): I - W already formed (build_at), the plain-B form of the GEMM
+  void enqueue_data_partial(const double* Wp, const State* st, const double* iw = nullptr) {
     if (loss == MIDAGMA_LOSS_L2) {
-      launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, Wp, D, B_IMINUS, Y.p, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
+      launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, iw ? iw : Wp, D, iw ? B_PLAIN : B_IMINUS, Y.p, D, EPI_STORE, 1,
+                  0, nullptr, 0, 0, st, stream);
     } else {
       launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, 1, 0, loss_part.p, n_local, d,
                   st, stream);
@@ -772,6 +775,10 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     } else {
       s->XT.release();
     }
+    if (s->loss == MIDAGMA_LOSS_L2 && D % 128 == 0)
+      s->IW.alloc((size_t)D * D);
+    else
+      s->IW.release();
     // split-K over the rows so the X^T Y GEMM fills the chip: (D/64)^2 tiles x split >= ~1024 workgroups
     const int64_t tiles = (D % 128 == 0) ? (D / 128) * (D / 128) : (D / 64) * (D / 64);
     const int64_t ktiles = s->n_pad / 64;
@@ -894,17 +901,17 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
     // [0] build (sI - W o W)^T   [1] GJ inverse   [2] score GEMM(s)   [3] whole slot (graph)
     // data mode: [4] Y = X (I - W) GEMM   [5] Z = X^T Y GEMM (+ slice sum)
     ms_out[0] = timed([&] { launch_build_at(s->W.p, D, true, s->Mt.p, D, s->d, 0.0, s->d_params, s->d_state,
-                                            s->stream); });
+                                            s->stream, s->IW.p); });
     ms_out[1] = timed([&] { launch_gj_inverse(s->Mt.p, D, D, s->gj(), s->d_state, s->stream); });
     if (s->mode == MIDAGMA_MODE_COV) {
       ms_out[2] = timed([&] { s->enqueue_cov_gemm(s->covs.p, s->W.p, s->zbuf, s->d_state); });
       ms_out[4] = ms_out[5] = 0.0;
     } else {
-      ms_out[2] = timed([&] { s->enqueue_data_partial(s->W.p, s->d_state); });
+      ms_out[2] = timed([&] { s->enqueue_data_partial(s->W.p, s->d_state, s->IW.p); });
       ms_out[4] = timed([&] {
         if (s->loss == MIDAGMA_LOSS_L2)
-          launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_IMINUS, s->Y.p, D, EPI_STORE, 1, 0, nullptr, 0,
-                      0, s->d_state, s->stream);
+          launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->IW.p ? s->IW.p : s->W.p, D,
+                      s->IW.p ? B_PLAIN : B_IMINUS, s->Y.p, D, EPI_STORE, 1, 0, nullptr, 0, 0, s->d_state, s->stream);
         else
           launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID, 1, 0,
                       s->loss_part.p, s->n_local, s->d, s->d_state, s->stream);
