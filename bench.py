@@ -430,10 +430,19 @@ def cpu_baseline(args, cov):
     return res
 
 
-_PMC_KERNEL = {"gemm_xw": "midagma::gemm128_kernel<true, 1, 0>", "gemm_xty": "midagma::gemm128_kernel<true, 0, 0>"}
+def _pmc_kernel(kernel, d, n_k):
+    """Name under which tools/pmc_summary.py files the data-mode GEMM: both GEMMs are
+    gemm_pipe_kernel<1, 0, 0> (A from X^T / X, plain B), told apart by their grids."""
+    D = -(-d // 128) * 128
+    if kernel == "gemm_xw":
+        grid = (-(-n_k // 128)) * (D // 128)
+    else:
+        split = max(1, min(-(-n_k // 128) * 128 // 64 // 8, -(-1024 // (D // 128) ** 2), 32))
+        grid = (D // 128) ** 2 * split
+    return f"midagma::gemm_pipe_kernel<1, 0, 0> grid={grid}"
 
 
-def _pmc_traffic(kernel, d, n, world):
+def _pmc_traffic(kernel, d, n, world, n_k):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this exact
     workload (profiles/*_pmc_bench_data_*.json; FETCH_SIZE x2 + WRITE_SIZE), else None."""
     import glob
@@ -443,7 +452,7 @@ def _pmc_traffic(kernel, d, n, world):
             w = j.get("workload", {})
             if (w.get("d"), w.get("n"), w.get("world")) != (d, n, world):
                 continue
-            k = j["kernels"].get(_PMC_KERNEL.get(kernel, ""))
+            k = j["kernels"].get(_pmc_kernel(kernel, d, n_k))
             if k:
                 return k["hbm_bytes_corrected"], os.path.relpath(f, REPO)
         except Exception:  # noqa: BLE001
@@ -490,7 +499,7 @@ def main():
             cfg = {"workload": f"config4: d={d}, n={args.n} linear-Gaussian SEM, l2, data mode, rows sharded over "
                                f"{world} GPU(s)", "d": d, "n": args.n, "n_per_gpu": n_k,
                    "parallelism": f"dp{world} (row shards, W replicated)"}
-            traffic, traffic_src = _pmc_traffic(dom, d, args.n, world)
+            traffic, traffic_src = _pmc_traffic(dom, d, args.n, world, n_k)
             roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                     "frac": (ach / FP64_MFMA_PEAK_TF) if ach else None, "traffic": traffic,
                     "traffic_source": traffic_src,

@@ -326,7 +326,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int per_slice = tiles_m * tiles_n;
   const int z = t / per_slice, rem = t % per_slice;
-  const int bm = rem / tiles_n, bn = rem % tiles_n;
+  int bm = rem / tiles_n, bn = rem % tiles_n;
+  if (EPI == EPI_SUB_BAND) {
+    // trailing update of the blocked inverse: the tile grid skips the pivot band
+    // [m_valid, m_valid + n_valid) (in 128-tiles) in both rows and columns
+    bm += bm >= (int)m_valid ? (int)n_valid : 0;
+    bn += bn >= (int)m_valid ? (int)n_valid : 0;
+  }
   const int64_t m0 = (int64_t)bm * 128, n0 = (int64_t)bn * 128;
   const int64_t k_begin = (int64_t)z * kslice;
   const int64_t k_end = (k_begin + kslice < K) ? k_begin + kslice : K;
@@ -470,6 +476,24 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64
 #undef GP_FRAG
 #undef GP_MMA
 #undef GP_SCHED
+  if (EPI == EPI_SUB_BAND) {  // C = C0 - acc, C0 passed as loss_part; slice_stride = check flags
+    const double* C0 = loss_part;
+    int flag = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int64_t row = m0 + 16 * i + acc_row(lane, tt);
+        const int64_t col = nw + 2 * acc_col(lane);
+        const double2 c0 = *reinterpret_cast<const double2*>(C0 + row * ldc + col);
+        const double2 v = double2{c0.x - acc[i][0][tt], c0.y - acc[i][1][tt]};
+        *reinterpret_cast<double2*>(C + row * ldc + col) = v;
+        flag |= (v.x + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v.x) ? 0 : 2);
+        flag |= (v.y + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v.y) ? 0 : 2);
+      }
+    if (slice_stride && flag) atomicOr(const_cast<int32_t*>(&st->flags), flag);
+    return;
+  }
   double* Ct = C + (int64_t)z * slice_stride;
   if (EPI == EPI_STORE) {
 #pragma unroll
@@ -542,6 +566,7 @@ void gemm_setup_attributes() {
   set_attr_pipe<0, B_IMINUS, EPI_STORE>();
   set_attr_pipe<1, B_PLAIN, EPI_SIGMOID>();
   set_attr_pipe<0, B_PLAIN, EPI_SIGMOID>();
+  set_attr_pipe<0, B_PLAIN, EPI_SUB_BAND>();
   set_attr128<false, B_PLAIN, EPI_STORE>();
   set_attr128<false, B_IMINUS, EPI_STORE>();
   set_attr128<true, B_PLAIN, EPI_STORE>();
@@ -655,9 +680,16 @@ void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int
   if (tm <= 0) return;
   const int64_t G0 = g * B2;
   // A = Ain[:, G] (lda D), B = Aout[G, :] (the row panel), C = Aout, C0 = Ain; K = B2
-  hipLaunchKernelGGL((gemm128_kernel<false, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
-                     kGemm128Lds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
-                     (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
+  static const bool no_pipe = getenv("MIDAGMA_EXP_NO_PIPE") != nullptr;  // experiment knob
+  if (!no_pipe)
+    hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
+                       kGemmPipeLds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
+                       (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128),
+                       st);
+  else
+    hipLaunchKernelGGL((gemm128_kernel<false, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
+                       kGemm128Lds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
+                       (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
   HIP_TRY(hipGetLastError());
 }
 

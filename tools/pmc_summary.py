@@ -21,6 +21,8 @@ def load(d, counter):
         if r["Counter_Name"] != counter:
             continue
         name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "")
+        if "gemm" in name:  # one template serves several GEMM shapes: key by grid as well
+            name += f" grid={int(r['Grid_Size']) // int(r['Workgroup_Size'])}"
         agg[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
 

@@ -83,6 +83,8 @@ if __name__ == "__main__":
         cov_case(200, 2000, 20, 500)
     if which in ("all", "d1000"):
         cov_case(1000, 2000, 10, 300)
+    if which == "d2000":
+        cov_case(2000, 4000, 5, 100)
     if which in ("all", "d5000"):
         cov_case(5000, 6000, 2, 10)
     if which == "trek":
