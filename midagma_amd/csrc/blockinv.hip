@@ -347,7 +347,8 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
   double* part = bw.part + (int64_t)g * (NM_PASSES + 1) * PART_STRIDE;  // per block: kept for diagnostics
   hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Ain + G0 * D + G0, D, Pst,
                      bw.Q[0], part, done, st);
-  for (int p = 1; p <= NM_PASSES; ++p) {
+  static const int passes = getenv("MIDAGMA_EXP_NM_PASSES") ? atoi(getenv("MIDAGMA_EXP_NM_PASSES")) : NM_PASSES_RUN;
+  for (int p = 1; p <= passes && p <= NM_PASSES; ++p) {
     const double* Y = p == 1 ? Pst : bw.Y[(p - 1) & 1];
     hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Y, bw.Q[(p - 1) & 1],
                        bw.Y[p & 1], bw.Q[p & 1], bw.P, part + (p - 1) * PART_STRIDE, part + p * PART_STRIDE,

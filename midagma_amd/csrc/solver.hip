@@ -565,6 +565,8 @@ struct midagma_solver {
     }
     handback_count += handbacks;
     fast_batch = bmax;
+    static const bool dbg = getenv("MIDAGMA_DEBUG_HANDBACKS") != nullptr;  // diagnostics
+    if (dbg) fprintf(stderr, "drive_blocked: %lld slots, %lld hand-backs\n", (long long)launched, (long long)handbacks);
   }
   int64_t handback_count = 0;
   int64_t fast_batch = 64;

@@ -76,6 +76,17 @@ def trek_case(d, seq, K):
     s.close()
 
 
+def fit_case(d, n):
+    from midagma_amd import DagmaLinear
+    X, _, _ = make_dataset(d, n, seed=0)
+    m = DagmaLinear("l2")
+    t0 = time.perf_counter()
+    m.fit(X.copy(), lambda1=0.03)
+    dt = time.perf_counter() - t0
+    its = [e["iters"] for e in m.minimize_log]
+    print(f"fit d={d} n={n}: {dt:.2f} s, iters {its} = {sum(its)}, {dt / sum(its) * 1e3:.3f} ms/iter", flush=True)
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "small"):
@@ -83,6 +94,8 @@ if __name__ == "__main__":
         cov_case(200, 2000, 20, 500)
     if which in ("all", "d1000"):
         cov_case(1000, 2000, 10, 300)
+    if which == "fit":
+        fit_case(1000, 10000)
     if which == "d2000":
         cov_case(2000, 4000, 5, 100)
     if which in ("all", "d5000"):
