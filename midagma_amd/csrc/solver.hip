@@ -49,6 +49,9 @@ struct midagma_solver {
   std::string err;
 
   DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
+  // ((-mu) cov)^T: the cov-mode score GEMM reads its A operand k-major (coalesced tile rows)
+  DevBuf covsT;
+  bool cov_at = getenv("MIDAGMA_EXP_COV_AMODE0") == nullptr;  // experiment knob
   DevBuf npart;  // checkpoint-step norm partials (fused_update -> control)
   // PST trek regularizer (trek.hip)
   TrekCfg tcfg{};
@@ -105,7 +108,7 @@ struct midagma_solver {
 
   ~midagma_solver() {
     destroy_graphs();
-    for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
+    for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW})
       b->release();
@@ -160,7 +163,10 @@ struct midagma_solver {
     if (mode == MIDAGMA_MODE_COV) {
       // rhs = ((-mu) cov) @ (I - W)    (linear.py:244); a fast slot leaves the split-K slices
       // for fused_update to sum (its only reader there)
-      enqueue_cov_gemm(covs.p, W.p, zbuf, d_state, /*sum=*/!(fast && blocked()));
+      if (cov_at)
+        enqueue_cov_gemm(covsT.p, W.p, zbuf, d_state, /*sum=*/!(fast && blocked()), /*a_trans=*/true);
+      else
+        enqueue_cov_gemm(covs.p, W.p, zbuf, d_state, /*sum=*/!(fast && blocked()));
     } else {
       enqueue_data_partial(W.p, d_state, IW.p);
     }
@@ -176,13 +182,15 @@ struct midagma_solver {
 
   // out = Cm @ (I - Wp) on the d x d problem; split-K over fixed slices when the tile grid
   // alone cannot fill the chip (summed in fixed order: deterministic)
-  void enqueue_cov_gemm(const double* Cm, const double* Wp, double* out, const State* st, bool sum = true) {
+  // a_trans: Cm holds the transpose of the left operand
+  void enqueue_cov_gemm(const double* Cm, const double* Wp, double* out, const State* st, bool sum = true,
+                        bool a_trans = false) {
     if (cov_split > 1) {
-      launch_gemm(D, D, D, Cm, D, false, Wp, D, B_IMINUS, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
+      launch_gemm(D, D, D, Cm, D, a_trans, Wp, D, B_IMINUS, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
                   0, st, stream);
       if (sum) launch_sum_slices(cov_parts.p, cov_split, D * D, D * D, out, st, stream);
     } else {
-      launch_gemm(D, D, D, Cm, D, false, Wp, D, B_IMINUS, out, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
+      launch_gemm(D, D, D, Cm, D, a_trans, Wp, D, B_IMINUS, out, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
     }
   }
 
@@ -382,7 +390,7 @@ struct midagma_solver {
   // ---- buffers -------------------------------------------------------------
   void alloc_core() {
     const size_t DD = (size_t)D * D;
-    for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs}) {
+    for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &covsT}) {
       b->alloc(DD);
       HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
     }
@@ -505,7 +513,10 @@ struct midagma_solver {
     st.obj_prev = 1e16;
     h_state[0] = st;
     HIP_TRY(hipMemcpyAsync(d_state, &h_state[0], sizeof(State), hipMemcpyHostToDevice, stream));
-    if (mode == MIDAGMA_MODE_COV) launch_scale(cov.p, -mu_, covs.p, D * D, stream);  // (-mu) * cov
+    if (mode == MIDAGMA_MODE_COV) {
+      launch_scale(cov.p, -mu_, covs.p, D * D, stream);  // (-mu) * cov
+      launch_transpose(covs.p, D, D, D, covsT.p, D, stream);
+    }
     upload_matrix(W, Wh, d);
     const size_t DD = (size_t)D * D;
     for (DevBuf* b : {&m, &v, &g}) HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
@@ -906,7 +917,12 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
                                             s->stream, s->IW.p); });
     ms_out[1] = timed([&] { launch_gj_inverse(s->Mt.p, D, D, s->gj(), s->d_state, s->stream); });
     if (s->mode == MIDAGMA_MODE_COV) {
-      ms_out[2] = timed([&] { s->enqueue_cov_gemm(s->covs.p, s->W.p, s->zbuf, s->d_state); });
+      ms_out[2] = timed([&] {
+        if (s->cov_at)
+          s->enqueue_cov_gemm(s->covsT.p, s->W.p, s->zbuf, s->d_state, true, true);
+        else
+          s->enqueue_cov_gemm(s->covs.p, s->W.p, s->zbuf, s->d_state);
+      });
       ms_out[4] = ms_out[5] = 0.0;
     } else {
       ms_out[2] = timed([&] { s->enqueue_data_partial(s->W.p, s->d_state, s->IW.p); });
