@@ -52,6 +52,7 @@ struct midagma_solver {
   // ((-mu) cov)^T: the cov-mode score GEMM reads its A operand k-major (coalesced tile rows)
   DevBuf covsT;
   bool cov_at = getenv("MIDAGMA_EXP_COV_AMODE0") == nullptr;  // experiment knob
+  bool cov_iw = getenv("MIDAGMA_EXP_COV_IW") != nullptr;      // experiment knob
   DevBuf npart;  // checkpoint-step norm partials (fused_update -> control)
   // PST trek regularizer (trek.hip)
   TrekCfg tcfg{};
@@ -103,7 +104,8 @@ struct midagma_solver {
   double mu = 1.0;
   Params hp{};
 
-  hipGraphExec_t g_part1 = nullptr, g_part2 = nullptr, g_full = nullptr, g_fast = nullptr;
+  // g_fastN: FAST_GROUP fast slots in one graph (no inter-graph dispatch gap between them)
+  hipGraphExec_t g_part1 = nullptr, g_part2 = nullptr, g_full = nullptr, g_fast = nullptr, g_fastN = nullptr;
   bool graphs_valid = false;
 
   ~midagma_solver() {
@@ -127,7 +129,7 @@ struct midagma_solver {
   }
 
   void destroy_graphs() {
-    for (hipGraphExec_t* ge : {&g_part1, &g_part2, &g_full, &g_fast})
+    for (hipGraphExec_t* ge : {&g_part1, &g_part2, &g_full, &g_fast, &g_fastN})
       if (*ge) {
         (void)hipGraphExecDestroy(*ge);
         *ge = nullptr;
@@ -163,10 +165,7 @@ struct midagma_solver {
     if (mode == MIDAGMA_MODE_COV) {
       // rhs = ((-mu) cov) @ (I - W)    (linear.py:244); a fast slot leaves the split-K slices
       // for fused_update to sum (its only reader there)
-      if (cov_at)
-        enqueue_cov_gemm(covsT.p, W.p, zbuf, d_state, /*sum=*/!(fast && blocked()), /*a_trans=*/true);
-      else
-        enqueue_cov_gemm(covs.p, W.p, zbuf, d_state, /*sum=*/!(fast && blocked()));
+      enqueue_score_cov(zbuf, d_state, /*sum=*/!(fast && blocked()));
     } else {
       enqueue_data_partial(W.p, d_state, IW.p);
     }
@@ -180,17 +179,28 @@ struct midagma_solver {
     }
   }
 
+  // rhs = ((-mu) cov) @ (I - W) from the slot's operands: A read k-major from ((-mu) cov)^T
+  // (cov_at), B = I - W formed by build_at (IW, plain B) when the slot keeps it
+  void enqueue_score_cov(double* out, const State* st, bool sum) {
+    const double* A = cov_at ? covsT.p : covs.p;
+    if (IW.p)
+      enqueue_cov_gemm(A, IW.p, out, st, sum, cov_at, B_PLAIN);
+    else
+      enqueue_cov_gemm(A, W.p, out, st, sum, cov_at, B_IMINUS);
+  }
+
   // out = Cm @ (I - Wp) on the d x d problem; split-K over fixed slices when the tile grid
   // alone cannot fill the chip (summed in fixed order: deterministic)
   // a_trans: Cm holds the transpose of the left operand
+  // (bmode B_PLAIN: Wp already holds I - W)
   void enqueue_cov_gemm(const double* Cm, const double* Wp, double* out, const State* st, bool sum = true,
-                        bool a_trans = false) {
+                        bool a_trans = false, GemmB bmode = B_IMINUS) {
     if (cov_split > 1) {
-      launch_gemm(D, D, D, Cm, D, a_trans, Wp, D, B_IMINUS, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
+      launch_gemm(D, D, D, Cm, D, a_trans, Wp, D, bmode, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
                   0, st, stream);
       if (sum) launch_sum_slices(cov_parts.p, cov_split, D * D, D * D, out, st, stream);
     } else {
-      launch_gemm(D, D, D, Cm, D, a_trans, Wp, D, B_IMINUS, out, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
+      launch_gemm(D, D, D, Cm, D, a_trans, Wp, D, bmode, out, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
     }
   }
 
@@ -227,12 +237,14 @@ struct midagma_solver {
                         trek_on && tcfg.mode == 2 ? Gtrek.p : nullptr, d, D, npart.p, stream);
   }
 
-  hipGraphExec_t capture(int which) {
+  hipGraphExec_t capture(int which, int reps = 1) {
     hipGraph_t graph = nullptr;
     HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
-      if (which & 1) enqueue_part1((which & 4) != 0);
-      if (which & 2) enqueue_part2((which & 4) != 0);
+      for (int r = 0; r < reps; ++r) {
+        if (which & 1) enqueue_part1((which & 4) != 0);
+        if (which & 2) enqueue_part2((which & 4) != 0);
+      }
     } catch (...) {
       (void)hipStreamEndCapture(stream, &graph);
       if (graph) (void)hipGraphDestroy(graph);
@@ -251,7 +263,10 @@ struct midagma_solver {
     g_full = capture(3);
     g_part1 = capture(1);
     g_part2 = capture(2);
-    if (blocked()) g_fast = capture(3 | 4);
+    if (blocked()) {
+      g_fast = capture(3 | 4);
+      if (fast_group > 1) g_fastN = capture(3 | 4, fast_group);
+    }
     graphs_valid = true;
   }
 
@@ -408,6 +423,8 @@ struct midagma_solver {
       if (cov_split > 1) cov_parts.alloc((size_t)cov_split * DD);
     }
     if (mode == MIDAGMA_MODE_COV) B2 = binv_block(D);
+    // cov mode: build_at also writes I - W for the score GEMM's plain-B form
+    if (mode == MIDAGMA_MODE_COV && D % 128 == 0 && cov_iw) IW.alloc(DD);
     if (blocked()) {
       Malt.alloc(DD);
       Pst2.alloc((size_t)D * B2);
@@ -567,7 +584,11 @@ struct midagma_solver {
       const int64_t next_ck = std::min(max_iter, (it_hi / checkpoint + 1) * checkpoint);
       int64_t B = std::min<int64_t>(bmax, next_ck - it_hi);
       if (n_slots >= 0) B = std::min<int64_t>(B, n_slots - launched);
-      for (int64_t b = 0; b < B; ++b) HIP_TRY(hipGraphLaunch(g_fast, stream));
+      // (a hand-back inside a group turns the group's later slots into no-op launches)
+      int64_t b = 0;
+      if (g_fastN)
+        for (; b + fast_group <= B; b += fast_group) HIP_TRY(hipGraphLaunch(g_fastN, stream));
+      for (; b < B; ++b) HIP_TRY(hipGraphLaunch(g_fast, stream));
       launched += std::max<int64_t>(B, 0);
       HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
@@ -580,6 +601,7 @@ struct midagma_solver {
     if (dbg) fprintf(stderr, "drive_blocked: %lld slots, %lld hand-backs\n", (long long)launched, (long long)handbacks);
   }
   int64_t handback_count = 0;
+  int fast_group = getenv("MIDAGMA_EXP_FAST_GROUP") ? std::max(1, atoi(getenv("MIDAGMA_EXP_FAST_GROUP"))) : 4;
   int64_t fast_batch = 64;
 
   void run_loop(int64_t max_iter, int64_t checkpoint) {
@@ -917,12 +939,7 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
                                             s->stream, s->IW.p); });
     ms_out[1] = timed([&] { launch_gj_inverse(s->Mt.p, D, D, s->gj(), s->d_state, s->stream); });
     if (s->mode == MIDAGMA_MODE_COV) {
-      ms_out[2] = timed([&] {
-        if (s->cov_at)
-          s->enqueue_cov_gemm(s->covsT.p, s->W.p, s->zbuf, s->d_state, true, true);
-        else
-          s->enqueue_cov_gemm(s->covs.p, s->W.p, s->zbuf, s->d_state);
-      });
+      ms_out[2] = timed([&] { s->enqueue_score_cov(s->zbuf, s->d_state, true); });
       ms_out[4] = ms_out[5] = 0.0;
     } else {
       ms_out[2] = timed([&] { s->enqueue_data_partial(s->W.p, s->d_state, s->IW.p); });

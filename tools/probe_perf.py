@@ -93,13 +93,13 @@ if __name__ == "__main__":
         cov_case(20, 1000, 50, 2000)
         cov_case(200, 2000, 20, 500)
     if which in ("all", "d1000"):
-        cov_case(1000, 2000, 10, 300)
+        cov_case(1000, 2000, 10, 2000)
     if which == "fit":
         fit_case(1000, 10000)
     if which == "d2000":
         cov_case(2000, 4000, 5, 100)
     if which in ("all", "d5000"):
-        cov_case(5000, 6000, 2, 10)
+        cov_case(5000, 6000, 2, 30)
     if which == "trek":
         for seq in ("exp", "inv", "log"):
             trek_case(1000, seq, 50)
