@@ -46,6 +46,11 @@ struct midagma_solver {
   int64_t d = 0, D = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  // data mode: the inverse runs on a high-priority side stream beside the score GEMMs (it
+  // depends on W only); fork / join are events inside the captured slot graph
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool fork_inv = getenv("MIDAGMA_EXP_NO_FORK") == nullptr;  // experiment knob
   std::string err;
 
   DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
@@ -126,6 +131,9 @@ struct midagma_solver {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
+    if (side) (void)hipStreamDestroy(side);
+    for (hipEvent_t e : {ev_fork, ev_join})
+      if (e) (void)hipEventDestroy(e);
   }
 
   void destroy_graphs() {
@@ -148,6 +156,7 @@ struct midagma_solver {
                     reinterpret_cast<int*>(nmDone.p)};
   }
   bool blocked() const { return B2 > 0; }
+  bool forked_inverse() const { return side != nullptr && !blocked() && mode == MIDAGMA_MODE_DATA; }
 
   // ---- the slot -----------------------------------------------------------
   // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
@@ -158,7 +167,16 @@ struct midagma_solver {
       launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream);
     } else {
       launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, 0.0, d_params, d_state, stream, IW.p);
-      launch_gj_inverse(Mt.p, D, D, gj(), d_state, stream);
+      if (forked_inverse()) {
+        // fork: the GJ chain (latency-bound, ~2% of the chip) on the side stream, the n x d
+        // GEMMs on the main one; joined before anything reads Mt
+        HIP_TRY(hipEventRecord(ev_fork, stream));
+        HIP_TRY(hipStreamWaitEvent(side, ev_fork, 0));
+        launch_gj_inverse(Mt.p, D, D, gj(), d_state, side);
+        HIP_TRY(hipEventRecord(ev_join, side));
+      } else {
+        launch_gj_inverse(Mt.p, D, D, gj(), d_state, stream);
+      }
     }
     // (a fork/join of the score GEMMs onto a second stream inside the graph measured slower:
     // the cross-queue dependencies cost more than the overlap gains)
@@ -168,6 +186,7 @@ struct midagma_solver {
       enqueue_score_cov(zbuf, d_state, /*sum=*/!(fast && blocked()));
     } else {
       enqueue_data_partial(W.p, d_state, IW.p);
+      if (forked_inverse()) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
     }
     // trek regularizer of this slot's W (linear.py:251-258): every slot in 'opt' mode; in 'log'
     // mode only checkpoint slots, which are never fast slots
@@ -440,6 +459,13 @@ struct midagma_solver {
     HIP_TRY(hipMalloc(&d_state, sizeof(State)));
     HIP_TRY(hipHostMalloc(&h_state, 2 * sizeof(State), hipHostMallocDefault));
     for (auto& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (mode == MIDAGMA_MODE_DATA && fork_inv) {
+      int lo = 0, hi = 0;  // hi: the greatest priority (numerically least)
+      HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_TRY(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, hi));
+      HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
   }
 
   void upload_matrix(DevBuf& dst, const double* src, int64_t ld_src) {

@@ -1,0 +1,15 @@
+#!/bin/bash
+# data-mode parity subset with the GJ inverse forked beside the GEMMs, then timings fork vs no fork
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edges.py tests/test_gpu_distributed.py -x -q --timeout 120 --timeout-method thread -k "data or logistic or ragged or two_ranks" > gpurun_out/fork_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/fork_tests.log
+[ $rc -ne 0 ] && exit $rc
+L=gpurun_out/probe_fork.log
+echo "--- FORK" > $L
+timeout -k 10 300 python tools/probe_perf.py data125k >> $L 2>&1 && \
+timeout -k 10 300 python tools/probe_perf.py data1m >> $L 2>&1 && \
+echo "--- NO FORK" >> $L && MIDAGMA_EXP_NO_FORK=1 timeout -k 10 300 python tools/probe_perf.py data125k >> $L 2>&1 && \
+MIDAGMA_EXP_NO_FORK=1 timeout -k 10 300 python tools/probe_perf.py data1m >> $L 2>&1; rc=$?
+grep -a -v amdgpu.ids $L | cut -c1-300
+exit $rc

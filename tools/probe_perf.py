@@ -106,6 +106,10 @@ if __name__ == "__main__":
     if which == "tcc":
         for d, K in ((20, 2000), (100, 500), (300, 200), (1000, 50)):
             trek_case(d, "tcc", K)
+    if which == "data125k":
+        data_case(1000, 125000, 3, 60)
+    if which == "data1m":
+        data_case(1000, 1000000, 2, 20)
     if which in ("all", "data"):
         data_case(1000, 100000, 2, 10)
     if which == "data250":
