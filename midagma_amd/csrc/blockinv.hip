@@ -57,6 +57,33 @@ __device__ __forceinline__ void splitk_partial(const double* __restrict__ A, int
   acc = acc + c1;
 }
 
+// splitk_partial in two halves: the operand loads (issued before a dependent reduction so
+// their latency overlaps it) and the MFMA chains, in the same order (bit-identical)
+template <int L>
+__device__ __forceinline__ void splitk_load_a(const double* __restrict__ A, int64_t lda, int m0, double (&a)[L]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, kq = lane >> 4;
+  const double* ap = A + (int64_t)(m0 + r) * lda + w * 4 * L + kq * L;
+#pragma unroll
+  for (int q = 0; q < L; ++q) a[q] = ap[q];
+}
+template <int L>
+__device__ __forceinline__ void splitk_load_b(const double* __restrict__ B, int64_t ldb, int n0, double (&b)[L]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, kq = lane >> 4;
+  const double* bp = B + (int64_t)(w * 4 * L + kq * L) * ldb + n0 + r;
+#pragma unroll
+  for (int q = 0; q < L; ++q) b[q] = bp[(int64_t)q * ldb];
+}
+template <int L>
+__device__ __forceinline__ void splitk_mfma(const double (&a)[L], const double (&b)[L], dbl4& acc) {
+  dbl4 c1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < L; q += 2) {
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q + 1], b[q + 1], c1, 0, 0, 0);
+  }
+  acc = acc + c1;
+}
+
 // Sum the 4 waves' partials of one 16 x 16 tile in a fixed order: thread e of the workgroup
 // returns element e (t = e >> 6 register, lane e & 63 of the accumulator layout).
 __device__ __forceinline__ double splitk_sum(const dbl4& part, double* red) {
@@ -166,26 +193,32 @@ __global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restr
   __shared__ float red4[4];
   const int nt = B2 / 16, wg = blockIdx.x, tid = threadIdx.x;
   const int m0 = (wg / nt) * 16, n0 = (wg % nt) * 16;
+  // operands first: their latency overlaps the rho reduction (Y, Q are complete: the
+  // previous launch wrote them)
+  double aY[L], aQ[L], bQ[L];
+  splitk_load_a<L>(Y, B2, m0, aY);
+  splitk_load_b<L>(Q, B2, n0, bQ);
+  splitk_load_a<L>(Q, B2, m0, aQ);
+  int row, col;
+  tile_elem(tid, row, col);
+  const int gi = m0 + row, gj = n0 + col;
+  const double yold = Y[(int64_t)gi * B2 + gj];
   const double rho = inf_norm<B2>(part_prev, red4);
   if (!(rho <= 0.25)) {  // warm start too far, diverging, or not finite
     if (wg == 0 && tid == 0) st->status = ST_NEED_GJ;
     return;
   }
-  int row, col;
-  tile_elem(tid, row, col);
-  const int gi = m0 + row, gj = n0 + col;
-  const double yold = Y[(int64_t)gi * B2 + gj];
   dbl4 ay = {0.0, 0.0, 0.0, 0.0};
   if (rho <= 1e-8) {  // last factor: P = Y (I + Q)
-    splitk_partial<L>(Y, B2, Q, B2, m0, n0, ay);
+    splitk_mfma<L>(aY, bQ, ay);
     const double yq = splitk_sum(ay, red);
     st_wt(P + (int64_t)gi * B2 + gj, yold + yq);
     if (wg == 0 && tid == 0) __hip_atomic_store(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   dbl4 aq = {0.0, 0.0, 0.0, 0.0};
-  splitk_partial<L>(Y, B2, Q, B2, m0, n0, ay);
-  splitk_partial<L>(Q, B2, Q, B2, m0, n0, aq);
+  splitk_mfma<L>(aY, bQ, ay);
+  splitk_mfma<L>(aQ, bQ, aq);
   const double yq = splitk_sum(ay, red);
   __syncthreads();  // red reused
   const double qq = splitk_sum(aq, red);

@@ -44,7 +44,7 @@ constexpr int TPR = NB / EPT;             // threads per tile row (8)
 
 // A^T tile builder: At[J][I] = (I == J ? s : 0) - f(X[I][J]) on the logical
 // d x d block (f = square for W, identity for a given A), identity padding.
-template <bool SQUARE>
+template <bool SQUARE, int BT = 32>
 __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __restrict__ X, int64_t ldx,
                                                             double* __restrict__ At, int64_t D, int64_t d,
                                                             double s_arg, const Params* __restrict__ pr,
@@ -52,14 +52,15 @@ __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __rest
   if (st && st->status != ST_RUNNING) return;
   // s comes from device Params when given: graph replays must see each call's s
   const double s = pr ? pr->s : s_arg;
-  __shared__ double tile[64][65];
+  // 32 x 32 tiles: (D/32)^2 workgroups (1024 at D = 1024) keep enough loads in flight
+  __shared__ double tile[BT][BT + 1];
   const int bi = blockIdx.y, bj = blockIdx.x;  // source tile (rows bi, cols bj)
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
+  for (int it = 0; it < BT * BT / NTHREADS; ++it) {
     const int e = it * NTHREADS + tid;
-    const int r = e >> 6, c = e & 63;
-    const int64_t I = (int64_t)bi * 64 + r, J = (int64_t)bj * 64 + c;
+    const int r = e / BT, c = e % BT;
+    const int64_t I = (int64_t)bi * BT + r, J = (int64_t)bj * BT + c;
     double v;
     const double x = (I < d && J < d) ? X[I * ldx + J] : 0.0;
     if (I < d && J < d) {
@@ -74,10 +75,10 @@ __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __rest
   }
   __syncthreads();
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
+  for (int it = 0; it < BT * BT / NTHREADS; ++it) {
     const int e = it * NTHREADS + tid;
-    const int r = e >> 6, c = e & 63;  // r: row of At tile (= source col)
-    At[((int64_t)bj * 64 + r) * D + (int64_t)bi * 64 + c] = tile[r][c];
+    const int r = e / BT, c = e % BT;  // r: row of At tile (= source col)
+    At[((int64_t)bj * BT + r) * D + (int64_t)bi * BT + c] = tile[r][c];
   }
 }
 
@@ -359,7 +360,8 @@ extern "C" int midagma_debug_stamps(unsigned long long* out) {
 
 void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int64_t D, int64_t d, double s,
                      const Params* pr, const State* st, hipStream_t stream, double* IW) {
-  const int K = (int)(D / 64);
+  if (D % 32) throw std::invalid_argument("build_at: D must be a multiple of 32");
+  const int K = (int)(D / 32);
   dim3 grid(K, K);
   if (square)
     hipLaunchKernelGGL(build_at_kernel<true>, grid, dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, pr, st, IW);

@@ -251,7 +251,6 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
     if (pr->has_exc) wn = wn * mexc[idx];
     m[idx] = mm;
     v[idx] = vv;
-    g[idx] = gd;
     W[idx] = wn;
     q[NF_GOBJ] = gobj * gobj;
     q[NF_GSCORE] = gs * gs;
@@ -318,14 +317,17 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     if (pr->has_exc) wn = wn * mexc[idx];
     m[idx] = mm;
     v[idx] = vv;
-    g[idx] = gd;
     W[idx] = wn;
-  } else if (act == ACT_HALVE) {
-    const double gd = g[idx];
-    double wn = W[idx] + st->lr_a * gd;
-    W[idx] = wn - st->lr_b * gd;
-  } else {  // ACT_REVERT
-    W[idx] = W[idx] + st->lr_a * g[idx];
+  } else {
+    // the last STEP's Adam direction, recomputed from its m, v and bias terms (unchanged
+    // since: bit-identical to the value that step applied, so no d x d store per step)
+    const double gd = (m[idx] / st->bc1) / (sqrt(v[idx] / st->bc2) + 1e-8);
+    if (act == ACT_HALVE) {
+      double wn = W[idx] + st->lr_a * gd;
+      W[idx] = wn - st->lr_b * gd;
+    } else {  // ACT_REVERT
+      W[idx] = W[idx] + st->lr_a * gd;
+    }
   }
 }
 
