@@ -10,8 +10,9 @@
 // trailing kernels never read what a workgroup of the same launch writes.
 //
 // S^-1 has two sources:
-//   fast (this file)  S^-1 = X0 (I + R)(I + R^2)(I + R^4)...,  X0 = this block's P one slot
-//         earlier (W moves by ~lr per Adam step), R = I - S X0.  One residual launch and up
+//   fast (this file)  S^-1 = X0 (I + R)(I + R^2)(I + R^4)...,  X0 = 2 P(k-1) - P(k-2), the
+//         linear extrapolation of this block's P in the last two slots (W moves smoothly, by
+//         ~lr per Adam step; P(k-1) alone right after a slow start), R = I - S X0.  One residual launch and up
 //         to NM_PASSES pass launches of B2^3 products spread over (B2/16)^2 workgroups
 //         with K split over the 4 waves -- no serial chain of 32 x 32 inversions.  Pass p
 //         holds Y = X0 (I + R)...(I + R^(2^(p-1))) and Q = R^(2^p), the exact residual of
@@ -149,12 +150,19 @@ __device__ __forceinline__ double inf_norm(const double* __restrict__ rowpart, f
   return (double)block_max(f, red4);
 }
 
-// R = I - S X0 (tile (m0, n0) of the B2 x B2 block), row partials of |R| -> part0
+// X0 = the warm start of this block: with two consecutive stored slots (st->warm_run >= 2)
+// the linear extrapolation 2 P1 - P2 of the last two inverses (P1 = slot k-1's, P2 = slot
+// k-2's, by the parity of k = st->slots), else P1.  Adam moves W smoothly (beta1 = 0.99), so
+// the extrapolation leaves a residual ~100x smaller than P1 alone (2 product-form passes
+// instead of 3 at d = 1000, measured on the default fit).
+// R = I - S X0 (tile (m0, n0) of the B2 x B2 block), row partials of |R| -> part0; the
+// workgroup also writes its tile of X0 -> Y0 (the first pass's iterate).
 template <int L>
 __global__ __launch_bounds__(NTHREADS) void nm_resid_kernel(const double* __restrict__ S, int64_t lds,
-                                                            const double* __restrict__ X0, double* __restrict__ Q0,
-                                                            double* __restrict__ part0, int* __restrict__ done,
-                                                            State* __restrict__ st) {
+                                                            const double* __restrict__ Pe,
+                                                            const double* __restrict__ Po, double* __restrict__ Y0,
+                                                            double* __restrict__ Q0, double* __restrict__ part0,
+                                                            int* __restrict__ done, State* __restrict__ st) {
   if (st->status != ST_RUNNING) return;
   if (st->ckpt_pending) {  // a log-det is due: pivots come from the slow path only
     if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
@@ -165,14 +173,29 @@ __global__ __launch_bounds__(NTHREADS) void nm_resid_kernel(const double* __rest
   const int nt = B2 / 16, wg = blockIdx.x;
   const int m0 = (wg / nt) * 16, n0 = (wg % nt) * 16;
   if (wg == 0 && threadIdx.x == 0) *done = 0;
-  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  splitk_partial<L>(S, lds, X0, B2, m0, n0, acc);
-  const double sum = splitk_sum(acc, red);
+  const bool odd = (st->slots & 1) != 0;
+  const double* P1 = odd ? Pe : Po;  // slot k-1
+  const double* P2 = odd ? Po : Pe;  // slot k-2
+  const bool extrap = st->warm_run >= 2;
+  double a[L], b[L];
+  splitk_load_a<L>(S, lds, m0, a);
+  splitk_load_b<L>(P1, B2, n0, b);
+  if (extrap) {
+    double b2[L];
+    splitk_load_b<L>(P2, B2, n0, b2);
+#pragma unroll
+    for (int q = 0; q < L; ++q) b[q] = 2.0 * b[q] - b2[q];
+  }
   int row, col;
   tile_elem(threadIdx.x, row, col);
   const int gi = m0 + row, gj = n0 + col;
+  const int64_t e = (int64_t)gi * B2 + gj;
+  st_wt(Y0 + e, extrap ? 2.0 * P1[e] - P2[e] : P1[e]);
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  splitk_mfma<L>(a, b, acc);
+  const double sum = splitk_sum(acc, red);
   const double r = (gi == gj ? 1.0 : 0.0) - sum;
-  st_wt(Q0 + (int64_t)gi * B2 + gj, r);
+  st_wt(Q0 + e, r);
   store_row_partial(abs_or_inf(r), part0, m0, n0, nt);
 }
 
@@ -268,7 +291,7 @@ __device__ __forceinline__ void tile32_gemm(const double* __restrict__ A, int64_
 __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __restrict__ Ain,
                                                               double* __restrict__ Aout, int64_t D, int B2, int g,
                                                               const double* __restrict__ P, int64_t ldp,
-                                                              double* __restrict__ Pst,
+                                                              double* __restrict__ Pe, double* __restrict__ Po,
                                                               const int* __restrict__ done, int check,
                                                               State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
@@ -308,6 +331,7 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
     const int j3 = job - 2 * nu, a = j3 / gb, c = j3 % gb;
     const double* src = P + (int64_t)a * NB * ldp + (int64_t)c * NB;
     double* out = Aout + (G0 + (int64_t)a * NB) * D + G0 + (int64_t)c * NB;
+    double* Pst = (st && (st->slots & 1)) ? Po : Pe;  // this slot's store (parity of k)
     double* ps = Pst + (int64_t)a * NB * B2 + (int64_t)c * NB;
     int flag = 0;
 #pragma unroll
@@ -375,14 +399,15 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
                            hipStream_t stream) {
   constexpr int B2 = 16 * L;
   const int nwg = (B2 / 16) * (B2 / 16);
-  double* Pst = bw.Pst + (int64_t)g * B2 * B2;
+  const double* Pe = bw.Pst + (int64_t)g * B2 * B2;
+  const double* Po = bw.Pst1 + (int64_t)g * B2 * B2;
   int* done = bw.done + g;
   double* part = bw.part + (int64_t)g * (NM_PASSES + 1) * PART_STRIDE;  // per block: kept for diagnostics
-  hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Ain + G0 * D + G0, D, Pst,
-                     bw.Q[0], part, done, st);
+  hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Ain + G0 * D + G0, D, Pe, Po,
+                     bw.Y[0], bw.Q[0], part, done, st);
   static const int passes = getenv("MIDAGMA_EXP_NM_PASSES") ? atoi(getenv("MIDAGMA_EXP_NM_PASSES")) : NM_PASSES_RUN;
   for (int p = 1; p <= passes && p <= NM_PASSES; ++p) {
-    const double* Y = p == 1 ? Pst : bw.Y[(p - 1) & 1];
+    const double* Y = bw.Y[(p - 1) & 1];  // pass 1: X0 from nm_resid
     hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Y, bw.Q[(p - 1) & 1],
                        bw.Y[p & 1], bw.Q[p & 1], bw.P, part + (p - 1) * PART_STRIDE, part + p * PART_STRIDE,
                        done, st);
@@ -400,7 +425,8 @@ void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     double* Ain = bufs[g & 1];
     double* Aout = bufs[(g + 1) & 1];
     const int64_t G0 = (int64_t)g * B2;
-    double* Pst = bw.Pst + (int64_t)g * B2 * B2;
+    double* Pe = bw.Pst + (int64_t)g * B2 * B2;
+    double* Po = bw.Pst1 + (int64_t)g * B2 * B2;
     const double* P;
     int64_t ldp;
     const int* done = nullptr;
@@ -423,7 +449,7 @@ void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     // the fast slot takes the domain flags from the last outer step's outputs (no reduce_check)
     const int check = fast && g == K2 - 1;
     hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2,
-                       g, P, ldp, Pst, done, check, st);
+                       g, P, ldp, Pe, Po, done, check, st);
     if (mb > 0) {
       // large D: 128 x 128 tiles (operand reuse; enough tiles to fill the chip), else 32 x 32
       if (D - B2 >= TRAIL128_MIN)

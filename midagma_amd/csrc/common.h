@@ -70,6 +70,7 @@ struct State {
   double obj_last, score_last, h_last, l1_last;
   int32_t flags;         // bit0: inverse has an entry < 0 after +1e-16; bit1: non-finite
   int32_t warm_valid;    // Pstore holds the diagonal-block inverses of the previous slot
+  int32_t warm_run;      // consecutive slots of this call whose outer-block inverses are stored (cap 2)
   uint64_t t0;           // device real-time clock (100 MHz) at the call's first slot
 };
 

@@ -46,7 +46,8 @@ constexpr int NM_PASSES_RUN = 3;
 constexpr int PART_STRIDE = 4096;   // doubles per pass: row partials of |Q| (B2 x B2/16)
 struct BInvWork {
   double* Aalt;    // second D x D buffer (outer steps ping-pong)
-  double* Pst;     // D x B2: warm start (last inverse) of every outer diagonal block
+  double* Pst;     // D x B2: the outer diagonal blocks' inverses of the slots with even /
+  double* Pst1;    //   odd st->slots (the last two slots': the warm start extrapolates them)
   double* Y[2];    // B2 x B2 product-form iterates
   double* Q[2];
   double* P;       // B2 x B2 converged inverse of the current block

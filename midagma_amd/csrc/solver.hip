@@ -75,7 +75,7 @@ struct midagma_solver {
   State* cgates = nullptr;
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
-  DevBuf Malt, Pst2, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone;
+  DevBuf Malt, Pst2, Pst2b, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone;
   bool fast_ready = false;  // Pst2 holds the previous slot's outer-block inverses
   double* zbuf = nullptr;  // d x d (+64 tail) score partial; internal or bound
   int64_t zbuf_cap = 0;
@@ -116,7 +116,7 @@ struct midagma_solver {
   ~midagma_solver() {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
-                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2,
+                      &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW})
       b->release();
     for (DevBuf& b : tbufs) b.release();
@@ -149,6 +149,7 @@ struct midagma_solver {
   BInvWork binv() {
     return BInvWork{Malt.p,
                     Pst2.p,
+                    Pst2b.p,
                     {nmY0.p, nmY1.p},
                     {nmQ0.p, nmQ1.p},
                     nmP.p,
@@ -447,6 +448,7 @@ struct midagma_solver {
     if (blocked()) {
       Malt.alloc(DD);
       Pst2.alloc((size_t)D * B2);
+      Pst2b.alloc((size_t)D * B2);
       for (DevBuf* b : {&nmY0, &nmY1, &nmQ0, &nmQ1, &nmP}) b->alloc((size_t)B2 * B2);
       nmPart.alloc((size_t)(D / B2) * (NM_PASSES + 1) * PART_STRIDE);
       nmDone.alloc(D / B2);

@@ -115,6 +115,7 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
   if (st->slots == 0) st->t0 = __builtin_amdgcn_s_memrealtime();
   st->slots += 1;
   st->warm_valid = 1;  // this slot's GJ pass stored every diagonal-block inverse
+  st->warm_run = st->warm_run < 2 ? st->warm_run + 1 : 2;
   const int flags = st->flags;
   st->flags = 0;
   if (ck) {
@@ -174,6 +175,7 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
       st->action = ACT_NOOP;
       return;
     }
+    st->warm_run = 1;  // W turns back: the last two inverses do not extrapolate the path
     const double lr_old = st->lr;
     st->lr = lr_old * .5;
     st->halvings += 1;
