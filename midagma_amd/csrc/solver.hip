@@ -437,8 +437,20 @@ struct midagma_solver {
     partials.alloc(2 * NRED);
     npart.alloc((size_t)((d + NTHREADS - 1) / NTHREADS) * d * NORM_FIELDS);
     HIP_TRY(hipMemsetAsync(npart.p, 0, npart.n * sizeof(double), stream));
-    if (D % 128 == 0 && (D / 128) * (D / 128) < 256) {
-      cov_split = (int)std::min<int64_t>(4, D / 128);
+    if (D % 128 == 0) {
+      // split-K of the cov score GEMM: small grids get slices to fill the chip; large ones the
+      // split that best rounds the last wave of 128-tiles (2 workgroups per CU resident:
+      // 1600 tiles at d = 5000 leave the 4th wave 1/8 full, split 4 -> 13 full-ish waves)
+      const int64_t tiles = (D / 128) * (D / 128), slots = 2 * 256;
+      if (tiles < 256) {
+        cov_split = (int)std::min<int64_t>(4, D / 128);
+      } else if (tiles >= 1024) {  // (256..1023 tiles: split 1 measured best at d = 2000)
+        double best = 1e30;
+        for (int sp = 1; sp <= 4; ++sp) {
+          const double waves = (double)((tiles * sp + slots - 1) / slots) / sp * (1.0 + 0.03 * (sp - 1));
+          if (waves < best) best = waves, cov_split = sp;
+        }
+      }
       if (const char* e = getenv("MIDAGMA_EXP_COV_SPLIT")) cov_split = atoi(e);  // experiment knob
       if (cov_split > 1) cov_parts.alloc((size_t)cov_split * DD);
     }
