@@ -395,7 +395,7 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw) {
 }
 
 template <int L>
-static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& bw, int g, State* st,
+static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& bw, int g, State* st, int passes,
                            hipStream_t stream) {
   constexpr int B2 = 16 * L;
   const int nwg = (B2 / 16) * (B2 / 16);
@@ -405,7 +405,6 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
   double* part = bw.part + (int64_t)g * (NM_PASSES + 1) * PART_STRIDE;  // per block: kept for diagnostics
   hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Ain + G0 * D + G0, D, Pe, Po,
                      bw.Y[0], bw.Q[0], part, done, st);
-  static const int passes = getenv("MIDAGMA_EXP_NM_PASSES") ? atoi(getenv("MIDAGMA_EXP_NM_PASSES")) : NM_PASSES_RUN;
   for (int p = 1; p <= passes && p <= NM_PASSES; ++p) {
     const double* Y = bw.Y[(p - 1) & 1];  // pass 1: X0 from nm_resid
     hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Y, bw.Q[(p - 1) & 1],
@@ -415,7 +414,7 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
 }
 
 void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
-                            hipStream_t stream) {
+                            hipStream_t stream, int passes) {
   const int B2 = binv_block(D);
   if (B2 == 0) throw std::invalid_argument("blocked inverse needs D >= 256, D % 128 == 0");
   const int K2 = (int)(D / B2), gb = B2 / NB, mb = (int)(D / NB) - gb;
@@ -432,9 +431,9 @@ void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     const int* done = nullptr;
     if (fast) {
       if (B2 == 256)
-        launch_neumann<16>(Ain, D, G0, bw, g, st, stream);
+        launch_neumann<16>(Ain, D, G0, bw, g, st, passes, stream);
       else
-        launch_neumann<8>(Ain, D, G0, bw, g, st, stream);
+        launch_neumann<8>(Ain, D, G0, bw, g, st, passes, stream);
       P = bw.P;
       ldp = B2;
       done = bw.done + g;

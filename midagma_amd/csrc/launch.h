@@ -62,8 +62,10 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
 // blocks by the warm-started product form (fast; sets ST_NEED_GJ when it cannot) or by the
 // 32-block Gauss-Jordan with pivots (slow).  The fast path also ORs reduce_check's domain
 // flags into st->flags from the last outer step's outputs.
+// passes: product-form pass launches per outer block on the fast path (2 covers the
+// extrapolated warm start's usual residual, 3 the rest; an unconverged block hands back).
 void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
-                            hipStream_t stream);
+                            hipStream_t stream, int passes = NM_PASSES_RUN);
 
 // --- trek.hip ---------------------------------------------------------------
 enum TrekSeq : int { TREK_EXP = 0, TREK_INV = 1, TREK_LOG = 2, TREK_BINOM = 3 };
@@ -188,8 +190,7 @@ void launch_control(const Params* pr, State* st, const double* partials, const d
                     const double* npart, int64_t d, const double* trek_val, hipStream_t stream);
 // Z: the score partial, or (zsplit > 1) split-K slices Z + z*zstride summed here in the order
 // of launch_sum_slices.  trek (nullable): weight * trek gradient, added last (linear.py:258).
-void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
-                         const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
+void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
                          const double* minc, const double* mexc, const double* trek, int64_t d, int64_t D,
                          double* npart, hipStream_t stream);
 // y = a * x elementwise over n doubles

@@ -53,7 +53,7 @@ struct midagma_solver {
   bool fork_inv = getenv("MIDAGMA_EXP_NO_FORK") == nullptr;  // experiment knob
   std::string err;
 
-  DevBuf W, m, v, g, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
+  DevBuf W, m, v, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
   // ((-mu) cov)^T: the cov-mode score GEMM reads its A operand k-major (coalesced tile rows)
   DevBuf covsT;
   bool cov_at = getenv("MIDAGMA_EXP_COV_AMODE0") == nullptr;  // experiment knob
@@ -110,12 +110,17 @@ struct midagma_solver {
   Params hp{};
 
   // g_fastN: FAST_GROUP fast slots in one graph (no inter-graph dispatch gap between them)
+  // g_fast2 / g_fastN2: the same with 2 product-form passes per outer block (the extrapolated
+  // warm start usually converges in 2); the host falls back to 3 for a while after a hand-back
   hipGraphExec_t g_part1 = nullptr, g_part2 = nullptr, g_full = nullptr, g_fast = nullptr, g_fastN = nullptr;
+  hipGraphExec_t g_fast2 = nullptr, g_fastN2 = nullptr;
+  bool nm_adapt = !(getenv("MIDAGMA_EXP_NM_ADAPT") && atoi(getenv("MIDAGMA_EXP_NM_ADAPT")) == 0);  // knob
+  int64_t three_pass_left = 0;  // fast slots still to run with 3 passes (after a 2-pass hand-back)
   bool graphs_valid = false;
 
   ~midagma_solver() {
     destroy_graphs();
-    for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
+    for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW})
       b->release();
@@ -137,7 +142,7 @@ struct midagma_solver {
   }
 
   void destroy_graphs() {
-    for (hipGraphExec_t* ge : {&g_part1, &g_part2, &g_full, &g_fast, &g_fastN})
+    for (hipGraphExec_t* ge : {&g_part1, &g_part2, &g_full, &g_fast, &g_fastN, &g_fast2, &g_fastN2})
       if (*ge) {
         (void)hipGraphExecDestroy(*ge);
         *ge = nullptr;
@@ -161,11 +166,11 @@ struct midagma_solver {
 
   // ---- the slot -----------------------------------------------------------
   // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
-  void enqueue_part1(bool fast = false) {
+  void enqueue_part1(bool fast = false, int passes = NM_PASSES_RUN) {
     if (blocked()) {
       launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
                       stream, IW.p);
-      launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream);
+      launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes);
     } else {
       launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, 0.0, d_params, d_state, stream, IW.p);
       if (forked_inverse()) {
@@ -252,17 +257,17 @@ struct midagma_solver {
     launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
                    trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream);
     const bool slices = lean && cov_split > 1;
-    launch_fused_update(d_params, d_state, W.p, m.p, v.p, g.p, Mt.p, slices ? cov_parts.p : zbuf,
+    launch_fused_update(d_params, d_state, W.p, m.p, v.p, Mt.p, slices ? cov_parts.p : zbuf,
                         slices ? cov_split : 1, D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr,
                         trek_on && tcfg.mode == 2 ? Gtrek.p : nullptr, d, D, npart.p, stream);
   }
 
-  hipGraphExec_t capture(int which, int reps = 1) {
+  hipGraphExec_t capture(int which, int reps = 1, int passes = NM_PASSES_RUN) {
     hipGraph_t graph = nullptr;
     HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     try {
       for (int r = 0; r < reps; ++r) {
-        if (which & 1) enqueue_part1((which & 4) != 0);
+        if (which & 1) enqueue_part1((which & 4) != 0, passes);
         if (which & 2) enqueue_part2((which & 4) != 0);
       }
     } catch (...) {
@@ -286,6 +291,10 @@ struct midagma_solver {
     if (blocked()) {
       g_fast = capture(3 | 4);
       if (fast_group > 1) g_fastN = capture(3 | 4, fast_group);
+      if (nm_adapt) {
+        g_fast2 = capture(3 | 4, 1, 2);
+        if (fast_group > 1) g_fastN2 = capture(3 | 4, fast_group, 2);
+      }
     }
     graphs_valid = true;
   }
@@ -425,7 +434,7 @@ struct midagma_solver {
   // ---- buffers -------------------------------------------------------------
   void alloc_core() {
     const size_t DD = (size_t)D * D;
-    for (DevBuf* b : {&W, &m, &v, &g, &Mt, &cov, &covs, &covsT}) {
+    for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT}) {
       b->alloc(DD);
       HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
     }
@@ -576,9 +585,10 @@ struct midagma_solver {
     }
     upload_matrix(W, Wh, d);
     const size_t DD = (size_t)D * D;
-    for (DevBuf* b : {&m, &v, &g}) HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
+    for (DevBuf* b : {&m, &v}) HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
     HIP_TRY(hipStreamSynchronize(stream));  // h_state[0] reused as a snapshot slot below
     fast_ready = false;  // the first slot of a call runs the GJ path (warm starts are stale)
+    three_pass_left = 0;
     begun = true;
   }
 
@@ -625,15 +635,19 @@ struct midagma_solver {
       int64_t B = std::min<int64_t>(bmax, next_ck - it_hi);
       if (n_slots >= 0) B = std::min<int64_t>(B, n_slots - launched);
       // (a hand-back inside a group turns the group's later slots into no-op launches)
+      const bool two = g_fast2 != nullptr && three_pass_left <= 0;
+      hipGraphExec_t one = two ? g_fast2 : g_fast, grp = two ? g_fastN2 : g_fastN;
       int64_t b = 0;
-      if (g_fastN)
-        for (; b + fast_group <= B; b += fast_group) HIP_TRY(hipGraphLaunch(g_fastN, stream));
-      for (; b < B; ++b) HIP_TRY(hipGraphLaunch(g_fast, stream));
+      if (grp)
+        for (; b + fast_group <= B; b += fast_group) HIP_TRY(hipGraphLaunch(grp, stream));
+      for (; b < B; ++b) HIP_TRY(hipGraphLaunch(one, stream));
+      if (!two) three_pass_left -= std::max<int64_t>(B, 0);
       launched += std::max<int64_t>(B, 0);
       HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
       cur = h_state[1];
       if (cur.status != ST_NEED_GJ) bmax = std::min<int64_t>(64, 2 * bmax);
+      else if (two) three_pass_left = 512;  // residuals this far need 3 passes: stay there a while
     }
     handback_count += handbacks;
     fast_batch = bmax;

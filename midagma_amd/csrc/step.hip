@@ -212,7 +212,7 @@ __device__ __forceinline__ double z_at(const double* __restrict__ Z, int zsplit,
 // workgroup.  Only every `checkpoint`-th slot takes this path.
 __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr, const State* __restrict__ st,
                                                    double* __restrict__ W, double* __restrict__ m,
-                                                   double* __restrict__ v, double* __restrict__ g,
+                                                   double* __restrict__ v,
                                                    const double* __restrict__ Mt, const double* __restrict__ Z,
                                                    int zsplit, int64_t zstride,
                                                    const double* __restrict__ cov, const double* __restrict__ minc,
@@ -286,7 +286,7 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
 
 __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
-    double* __restrict__ v, double* __restrict__ g, const double* __restrict__ Mt, const double* __restrict__ Z,
+    double* __restrict__ v, const double* __restrict__ Mt, const double* __restrict__ Z,
     int zsplit, int64_t zstride, const double* __restrict__ cov, const double* __restrict__ minc,
     const double* __restrict__ mexc, const double* __restrict__ trek, int64_t d, int64_t D,
     double* __restrict__ npart) {
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
   const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   const int64_t i = blockIdx.y;
   if (act == ACT_STEP && st->ckpt_pending) {  // checkpoint step: also the record's norms
-    fused_step_with_norms(pr, st, W, m, v, g, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, d, D, npart);
+    fused_step_with_norms(pr, st, W, m, v, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, d, D, npart);
     return;
   }
   if (j >= d) return;
@@ -382,12 +382,11 @@ void launch_control(const Params* pr, State* st, const double* partials, const d
   HIP_TRY(hipGetLastError());
 }
 
-void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, double* g,
-                         const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
+void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
                          const double* minc, const double* mexc, const double* trek, int64_t d, int64_t D,
                          double* npart, hipStream_t stream) {
   dim3 grid((unsigned)((d + NTHREADS - 1) / NTHREADS), (unsigned)d);
-  hipLaunchKernelGGL(fused_update_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, g, Mt, Z, zsplit,
+  hipLaunchKernelGGL(fused_update_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, Mt, Z, zsplit,
                      zstride, cov, minc, mexc, trek, d, D, npart);
   HIP_TRY(hipGetLastError());
 }
