@@ -1,6 +1,6 @@
 """Compare GPU vs oracle checkpoints for the last stage of the d=20 fit (development tool)."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
 import torch  # noqa
 from threadpoolctl import threadpool_limits

@@ -1,6 +1,6 @@
 """Which f64 MFMA C/D layout is right? (h at d=20 vs the oracle)"""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
 import torch  # noqa
 from midagma_amd.solver import HipSolver

@@ -3,10 +3,10 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python tools/layout_probe.py > gpurun_out/layout.log 2>&1; rc=$?
+timeout -k 10 300 python tests/probes/layout_probe.py > gpurun_out/layout.log 2>&1; rc=$?
 echo "layout rc=$rc"; cat gpurun_out/layout.log | tail -5
 [ $rc -ne 0 ] && exit $rc
-MIDAGMA_LIB=$PWD/midagma_amd/libmidagma_hip_alt.so timeout -k 10 300 python tools/layout_probe.py > gpurun_out/layout_alt.log 2>&1; rc=$?
+MIDAGMA_LIB=$PWD/midagma_amd/libmidagma_hip_alt.so timeout -k 10 300 python tests/probes/layout_probe.py > gpurun_out/layout_alt.log 2>&1; rc=$?
 echo "layout alt rc=$rc"; tail -5 gpurun_out/layout_alt.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python -m pytest tests -m gpu -q -rfE -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?

@@ -2,7 +2,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python tools/debug_stage5.py > gpurun_out/debug5.log 2>&1; rc=$?
+timeout -k 10 300 python tests/probes/debug_stage5.py > gpurun_out/debug5.log 2>&1; rc=$?
 echo "debug rc=$rc"; tail -40 gpurun_out/debug5.log
 [ $rc -gt 1 ] && exit $rc
 timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
