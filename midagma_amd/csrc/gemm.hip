@@ -584,7 +584,9 @@ void gemm_setup_attributes() {
 void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, bool a_trans, const double* B,
                  int64_t ldb, GemmB bmode, double* C, int64_t ldc, GemmEpi epi, int split, int64_t slice_stride,
                  double* loss_part, int64_t m_valid, int64_t n_valid, const State* st, hipStream_t stream) {
-  if (M % 64 || N % 64 || K % 64 || split < 1) throw std::invalid_argument("launch_gemm: bad shape");
+  // (K % 16 suffices for the pipelined kernel: the k loop of a padded problem may stop at the
+  // first 16-multiple past the logical size, the rest of A's k range being zero)
+  if (M % 64 || N % 64 || K % 16 || split < 1) throw std::invalid_argument("launch_gemm: bad shape");
   static const bool force64 = getenv("MIDAGMA_EXP_GEMM64") != nullptr;  // experiment knobs
   static const bool no_pipe = getenv("MIDAGMA_EXP_NO_PIPE") != nullptr;
   if (M % 128 == 0 && N % 128 == 0 && K % 16 == 0 && !force64 && !no_pipe &&
@@ -617,6 +619,7 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
     HIP_TRY(hipGetLastError());
     return;
   }
+  if (K % 64) throw std::invalid_argument("launch_gemm: K % 64 outside the pipelined kernel");
   if (M % 128 == 0 && N % 128 == 0 && K % 128 == 0 && !force64) {
     const int64_t ktiles16 = K / G_BK;
     const int64_t per16 = (ktiles16 + split - 1) / split;

@@ -162,6 +162,10 @@ struct midagma_solver {
                     reinterpret_cast<int*>(nmDone.p)};
   }
   bool blocked() const { return B2 > 0; }
+  // k extent of the GEMMs whose K is the padded node dimension: the rows of A past d are zero
+  // (X^T, ((-mu) cov)^T), so the k loop stops at the first 16-multiple >= d (the pipelined
+  // 128-tile kernel, D % 128 == 0; bit-identical: the skipped terms are exact zeros)
+  int64_t Kd() const { return D % 128 == 0 ? (d + 15) / 16 * 16 : D; }
   bool forked_inverse() const { return side != nullptr && !blocked() && mode == MIDAGMA_MODE_DATA; }
 
   // ---- the slot -----------------------------------------------------------
@@ -221,11 +225,11 @@ struct midagma_solver {
   void enqueue_cov_gemm(const double* Cm, const double* Wp, double* out, const State* st, bool sum = true,
                         bool a_trans = false, GemmB bmode = B_IMINUS) {
     if (cov_split > 1) {
-      launch_gemm(D, D, D, Cm, D, a_trans, Wp, D, bmode, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
+      launch_gemm(D, D, Kd(), Cm, D, a_trans, Wp, D, bmode, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
                   0, st, stream);
       if (sum) launch_sum_slices(cov_parts.p, cov_split, D * D, D * D, out, st, stream);
     } else {
-      launch_gemm(D, D, D, Cm, D, a_trans, Wp, D, bmode, out, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
+      launch_gemm(D, D, Kd(), Cm, D, a_trans, Wp, D, bmode, out, D, EPI_STORE, 1, 0, nullptr, 0, 0, st, stream);
     }
   }
 
@@ -233,7 +237,7 @@ struct midagma_solver {
   // iw (nullable): I - W already formed (build_at), the plain-B form of the GEMM
   void enqueue_data_partial(const double* Wp, const State* st, const double* iw = nullptr) {
     if (loss == MIDAGMA_LOSS_L2) {
-      launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, iw ? iw : Wp, D, iw ? B_PLAIN : B_IMINUS, Y.p, D, EPI_STORE, 1,
+      launch_gemm(n_pad, D, Kd(), xw_a(), xw_lda(), use_xt, iw ? iw : Wp, D, iw ? B_PLAIN : B_IMINUS, Y.p, D, EPI_STORE, 1,
                   0, nullptr, 0, 0, st, stream);
     } else {
       launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, 1, 0, loss_part.p, n_local, d,
@@ -999,7 +1003,7 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
       ms_out[2] = timed([&] { s->enqueue_data_partial(s->W.p, s->d_state, s->IW.p); });
       ms_out[4] = timed([&] {
         if (s->loss == MIDAGMA_LOSS_L2)
-          launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->IW.p ? s->IW.p : s->W.p, D,
+          launch_gemm(s->n_pad, D, s->Kd(), s->xw_a(), s->xw_lda(), s->use_xt, s->IW.p ? s->IW.p : s->W.p, D,
                       s->IW.p ? B_PLAIN : B_IMINUS, s->Y.p, D, EPI_STORE, 1, 0, nullptr, 0, 0, s->d_state, s->stream);
         else
           launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID, 1, 0,
