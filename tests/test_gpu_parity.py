@@ -330,6 +330,33 @@ def test_blocked_fast_path_trajectory(hip, d):
         assert abs(obj - obj_r) <= 1e-10 * abs(obj_r) and abs(h - h_r) <= 1e-9 * max(1.0, abs(h_r))
 
 
+def test_large_d_split_k_score_and_trajectory(hip):
+    """d=4500 -> D=4608: the cov score GEMM runs split-K 3 (1296 128-tiles, last-wave
+    rounding) with the k loop trimmed to 4512, the fast slots sum the 3 slices inside
+    fused_update, and the trailing update runs on the 128-tile GEMM over 18 outer blocks.
+    _score at a dense W and 8 Adam steps (checkpoints every 4: GJ and fast slots) against the
+    oracle (LAPACK inverse)."""
+    d = 4500
+    X, _, _ = make_dataset(d, 2 * d, seed=5)
+    o = _oracle(X)
+    o.checkpoint = 4
+    sol = _solver(d, o.cov)
+    rng = np.random.default_rng(2)
+    Wd = rng.normal(size=(d, d)) * 0.01
+    l, G = sol.score_value(Wd)
+    l_ref, G_ref = score("l2", Wd, o.cov)
+    assert abs(l - l_ref) <= 1e-12 * abs(l_ref)
+    assert _rel(G, G_ref) <= 1e-12
+    K = 8
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=4, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert res.iters == tr.iters == K and res.success
+    assert np.abs(W - Wr).max() <= 1e-9
+    for c, (_, obj_r, _, h_r) in zip(res.checkpoints, tr.checkpoints):
+        assert abs(c[1] - obj_r) <= 1e-10 * abs(obj_r) and abs(c[3] - h_r) <= 1e-9 * max(1.0, abs(h_r))
+
+
 CKPT_FIELDS = {"obj_total": "obj", "score_datafit": "score", "reg_dag_value": "h", "lr": "lr", "w_abs_sum": "l1",
                "w_norm": "w_norm", "max_abs_w": "max_abs_w", "min_abs_w_nonzero": "min_abs_w_nonzero",
                "grad_raw_norm": "grad_raw_norm", "grad_step_norm": "grad_step_norm",
