@@ -330,6 +330,25 @@ def test_blocked_fast_path_trajectory(hip, d):
         assert abs(obj - obj_r) <= 1e-10 * abs(obj_r) and abs(h - h_r) <= 1e-9 * max(1.0, abs(h_r))
 
 
+def test_blocked_path_line_search(hip):
+    """The domain line search (linear.py:230-241) on the blocked-inverse path: at d=300, lr=0.3
+    the reference halves lr three times in 60 steps.  The fast slots take the domain flags from
+    the last outer step, a halving turns the warm start back to the plain previous inverse, and
+    far warm starts hand back to the GJ slot; iterations, halvings, lr and W match the oracle."""
+    d = 300
+    X, _, _ = make_dataset(d, 2 * d, seed=7)
+    o = _oracle(X)
+    o.checkpoint = 20
+    sol = _solver(d, o.cov)
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, 60, 1.0, 0.3, tol=-1.0, lambda1=0.03, checkpoint=20)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, 60, 1.0, 0.3, tol=-1.0)
+    assert tr.halvings == 3
+    assert (res.iters, res.success, res.halvings) == (tr.iters, tr.success, tr.halvings)
+    assert res.lr_final == tr.lr_final
+    assert np.abs(W - Wr).max() <= 1e-8
+
+
 def test_large_d_split_k_score_and_trajectory(hip):
     """d=4500 -> D=4608: the cov score GEMM runs split-K 3 (1296 128-tiles, last-wave
     rounding) with the k loop trimmed to 4512, the fast slots sum the 3 slices inside
