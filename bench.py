@@ -71,9 +71,17 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (default off): every rank on cuda:0 and a gloo all-reduce, so the N > 1
+    # path runs end to end on a one-GPU box; the driver's runs use one GPU per rank over RCCL
+    if os.environ.get("MIDAGMA_BENCH_SAME_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("MIDAGMA_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     return world, rank, local
