@@ -167,6 +167,8 @@ struct midagma_solver {
   // 128-tile kernel, D % 128 == 0; bit-identical: the skipped terms are exact zeros)
   int64_t Kd() const { return D % 128 == 0 ? (d + 15) / 16 * 16 : D; }
   bool forked_inverse() const { return side != nullptr && !blocked() && mode == MIDAGMA_MODE_DATA; }
+  bool data_binv = getenv("MIDAGMA_EXP_DATA_FLAT_GJ") == nullptr;  // experiment knob
+  bool data_binv_on() const { return data_binv && mode == MIDAGMA_MODE_DATA && binv_block(D) > 0; }
 
   // ---- the slot -----------------------------------------------------------
   // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
@@ -175,18 +177,24 @@ struct midagma_solver {
       launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
                       stream, IW.p);
       launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes);
+    } else if (forked_inverse()) {
+      // fork: the inverse (latency-bound, a few % of the chip) on the side stream, the n x d
+      // GEMMs on the main one; joined before anything reads Mt.  With the blocked layout the
+      // slow (pivoted, no warm start) two-level inverse: ~5x fewer workgroup-microseconds
+      // taken from the GEMMs than the flat Gauss-Jordan's 32 x 1024 workgroups
+      const bool bl = data_binv_on();
+      launch_build_at(W.p, D, /*square=*/true, bl ? binv_build_target(Mt.p, D, binv()) : Mt.p, D, d, 0.0, d_params,
+                      d_state, stream, IW.p);
+      HIP_TRY(hipEventRecord(ev_fork, stream));
+      HIP_TRY(hipStreamWaitEvent(side, ev_fork, 0));
+      if (bl)
+        launch_blocked_inverse(Mt.p, D, binv(), /*fast=*/false, gj(), d_state, side);
+      else
+        launch_gj_inverse(Mt.p, D, D, gj(), d_state, side);
+      HIP_TRY(hipEventRecord(ev_join, side));
     } else {
       launch_build_at(W.p, D, /*square=*/true, Mt.p, D, d, 0.0, d_params, d_state, stream, IW.p);
-      if (forked_inverse()) {
-        // fork: the GJ chain (latency-bound, ~2% of the chip) on the side stream, the n x d
-        // GEMMs on the main one; joined before anything reads Mt
-        HIP_TRY(hipEventRecord(ev_fork, stream));
-        HIP_TRY(hipStreamWaitEvent(side, ev_fork, 0));
-        launch_gj_inverse(Mt.p, D, D, gj(), d_state, side);
-        HIP_TRY(hipEventRecord(ev_join, side));
-      } else {
-        launch_gj_inverse(Mt.p, D, D, gj(), d_state, stream);
-      }
+      launch_gj_inverse(Mt.p, D, D, gj(), d_state, stream);
     }
     // (a fork/join of the score GEMMs onto a second stream inside the graph measured slower:
     // the cross-queue dependencies cost more than the overlap gains)
@@ -470,13 +478,14 @@ struct midagma_solver {
     if (mode == MIDAGMA_MODE_COV) B2 = binv_block(D);
     // cov mode: build_at also writes I - W for the score GEMM's plain-B form
     if (mode == MIDAGMA_MODE_COV && D % 128 == 0 && cov_iw) IW.alloc(DD);
-    if (blocked()) {
+    if (blocked() || data_binv_on()) {
+      const int64_t b2 = binv_block(D);
       Malt.alloc(DD);
-      Pst2.alloc((size_t)D * B2);
-      Pst2b.alloc((size_t)D * B2);
-      for (DevBuf* b : {&nmY0, &nmY1, &nmQ0, &nmQ1, &nmP}) b->alloc((size_t)B2 * B2);
-      nmPart.alloc((size_t)(D / B2) * (NM_PASSES + 1) * PART_STRIDE);
-      nmDone.alloc(D / B2);
+      Pst2.alloc((size_t)D * b2);
+      Pst2b.alloc((size_t)D * b2);
+      for (DevBuf* b : {&nmY0, &nmY1, &nmQ0, &nmQ1, &nmP}) b->alloc((size_t)b2 * b2);
+      nmPart.alloc((size_t)(D / b2) * (NM_PASSES + 1) * PART_STRIDE);
+      nmDone.alloc(D / b2);
     }
     zown.alloc(DD + 64);
     HIP_TRY(hipMemsetAsync(zown.p, 0, (DD + 64) * sizeof(double), stream));
