@@ -262,6 +262,31 @@ def test_l2_data_mode_matches_cov_mode(hip):
     assert np.abs(Wb - Wr).max() <= 1e-9
 
 
+def test_data_mode_full_size_config4(hip):
+    """The headline workload at its full size on one GPU (BASELINE config 4, d=1000, n=1e6):
+    X from the GPU SEM generator, centered on the host as fit() does (linear.py:411); data
+    mode (two n x d MFMA GEMMs per step, forked blocked inverse) against the oracle's
+    reference-algorithm steps on cov = X^T X / n.  Same W after 5 Adam steps."""
+    from midagma_amd.simulate import simulate_er_dag, simulate_weights
+    from midagma_amd.utils import simulate_linear_sem_gpu
+    d, n, K = 1000, 1_000_000, 5
+    rng = np.random.default_rng(0)
+    W_true = simulate_weights(simulate_er_dag(d, d, rng), rng)
+    Xh = simulate_linear_sem_gpu(W_true, n, "gauss", seed=17, device=0).cpu().numpy()
+    o = LinearOracle("l2")
+    o.prepare(Xh, 0.03, 1000)  # centers Xh in place, cov = X^T X / n
+    sol = _solver(d, mode="data")
+    sol.set_data(Xh, n_global=n)
+    del Xh
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0)
+    o.X = None
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert res.iters == tr.iters == K and res.success
+    assert np.abs(W - Wr).max() <= 1e-9
+    sol.close()
+
+
 def test_data_mode_score_and_gram(hip):
     X, _, _ = make_dataset(70, 1000, seed=9)
     X = X - X.mean(0)
