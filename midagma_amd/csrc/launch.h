@@ -38,9 +38,9 @@ void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int6
 void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
 
 // --- blockinv.hip -----------------------------------------------------------
-// product-form pass slots per outer block (buffers) and the passes the fast graph runs: from
-// a warm start one Adam step old, 3 passes always converged in the default d=1000 fit (53k
-// slots: identical hand-backs with 3 and 4), and the 4th, a no-op launch, cost 3.5%
+// product-form pass slots per outer block (buffers) and the passes of the fallback fast graph
+// (the default fast graph runs 2: the extrapolated warm start converges in 2 almost always;
+// from a warm start one Adam step old, 3 always converged in the default d=1000 fit)
 constexpr int NM_PASSES = 4;
 constexpr int NM_PASSES_RUN = 3;
 constexpr int PART_STRIDE = 4096;   // doubles per pass: row partials of |Q| (B2 x B2/16)
