@@ -11,6 +11,11 @@ row 4; BASELINE config 5); only ``h_func`` (nonlinear.py:68-86) is replaced:
 
 The C entry point (`midagma_logdet_inv_dev`) works on torch's device memory
 and current HIP stream; it never synchronizes with the host.
+
+For the [d, m1, 1] model (BASELINE config 5) the score's squared residual sum runs as one
+fused HIP tail (`midagma_mlp_tail_fwd` / `_bwd`, csrc/mlp.hip): sigmoid, the width-1
+LocallyConnected layer with its bias, the residual sum and their backward in four launches
+instead of PyTorch's ~20 elementwise and reduction kernels (MIDAGMA_NO_MLP_TAIL=1: PyTorch).
 """
 from __future__ import annotations
 
@@ -52,6 +57,45 @@ class _LogdetH(torch.autograd.Function):
     def backward(ctx, grad_out):
         (Mt,) = ctx.saved_tensors
         return grad_out * Mt, None
+
+
+class _MLPTail(torch.autograd.Function):
+    """sum((LocallyConnected(sigmoid(Z)) - X)^2) for a [d, m1, 1] DagmaMLP, forward and
+    backward as fused HIP kernels (csrc/mlp.hip) on torch's stream."""
+
+    @staticmethod
+    def forward(ctx, Z: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, X: torch.Tensor, m1: int):
+        Z, w2, b2, X = Z.contiguous(), w2.contiguous(), b2.contiguous(), X.contiguous()
+        n, d = X.shape
+        R = torch.empty_like(X)
+        part = torch.empty((n * d + 255) // 256, dtype=torch.float64, device=X.device)
+        ssq = torch.empty((), dtype=torch.float64, device=X.device)
+        stream = torch.cuda.current_stream(X.device).cuda_stream
+        with torch.cuda.device(X.device):
+            _lib.check(_lib.lib().midagma_mlp_tail_fwd(
+                C.c_void_p(Z.data_ptr()), C.c_void_p(w2.data_ptr()), C.c_void_p(b2.data_ptr()),
+                C.c_void_p(X.data_ptr()), n, d, m1, C.c_void_p(R.data_ptr()), C.c_void_p(part.data_ptr()),
+                C.c_void_p(ssq.data_ptr()), C.c_void_p(stream) if stream else None), None, "mlp_tail_fwd")
+        ctx.save_for_backward(Z, w2, R)
+        ctx.m1 = m1
+        ctx.b2_shape = b2.shape
+        return ssq
+
+    @staticmethod
+    def backward(ctx, g):
+        Z, w2, R = ctx.saved_tensors
+        n, d = R.shape
+        g = g.contiguous()
+        dZ = torch.empty_like(Z)
+        dw2 = torch.empty_like(w2)
+        db2 = torch.empty(ctx.b2_shape, dtype=torch.float64, device=Z.device)
+        stream = torch.cuda.current_stream(Z.device).cuda_stream
+        with torch.cuda.device(Z.device):
+            _lib.check(_lib.lib().midagma_mlp_tail_bwd(
+                C.c_void_p(Z.data_ptr()), C.c_void_p(w2.data_ptr()), C.c_void_p(R.data_ptr()),
+                C.c_void_p(g.data_ptr()), n, d, ctx.m1, C.c_void_p(dZ.data_ptr()), C.c_void_p(dw2.data_ptr()),
+                C.c_void_p(db2.data_ptr()), C.c_void_p(stream) if stream else None), None, "mlp_tail_bwd")
+        return dZ, dw2, db2, None, None
 
 
 def logdet_h(A: torch.Tensor, s: float = 1.0) -> torch.Tensor:
@@ -118,6 +162,23 @@ class DagmaMLP(nn.Module):
             x = fc(x)
         return x.squeeze(dim=2)
 
+    def fused_tail(self) -> bool:
+        """True when sum((self(X) - X)^2) can run as the fused HIP tail: one hidden layer, a
+        width-1 output, biases, float64 on a ROCm device, hidden width <= 16."""
+        if len(self.fc2) != 1 or os.environ.get("MIDAGMA_NO_MLP_TAIL"):
+            return False
+        fc = self.fc2[0]
+        w = fc.weight
+        return (fc.output_features == 1 and fc.bias is not None and self.fc1.bias is not None and w.is_cuda
+                and w.dtype == torch.float64 and 1 <= self.dims[1] <= 16)
+
+    def squared_residual(self, x: torch.Tensor) -> torch.Tensor:
+        """sum((self(x) - x)^2), the sum inside the log-MSE score (nonlinear.py:139-159)."""
+        if self.fused_tail():
+            fc = self.fc2[0]
+            return _MLPTail.apply(self.fc1(x), fc.weight, fc.bias, x, self.dims[1])
+        return torch.sum((self(x) - x) ** 2)
+
     def _adjacency_sq(self) -> torch.Tensor:
         w = self.fc1.weight.view(self.d, -1, self.d)
         return torch.sum(w ** 2, dim=1).t()  # [i, j]
@@ -162,6 +223,14 @@ class DagmaNonlinear:
         n, d = target.shape
         return 0.5 * d * torch.log(1 / n * torch.sum((output - target) ** 2))
 
+    def _score(self) -> torch.Tensor:
+        """log_mse_loss(model(X), X); the squared residual sum through the model's fused tail
+        when it has one (same expression around it: 0.5 d log(1/n ssq))."""
+        if hasattr(self.model, "squared_residual"):
+            n, d = self.X.shape
+            return 0.5 * d * torch.log(1 / n * self.model.squared_residual(self.X))
+        return self.log_mse_loss(self.model(self.X), self.X)
+
     def minimize(self, max_iter: float, lr: float, lambda1: float, lambda2: float, mu: float, s: float,
                  lr_decay: float = False, tol: float = 1e-6, pbar=None) -> bool:
         """Adam on mu * (score + lambda1 |fc1|_1) + h (nonlinear.py:161-236); False when h < 0.
@@ -189,8 +258,7 @@ class DagmaNonlinear:
             for p in params:
                 p.grad = None
             h_val = self.model.h_func(s)
-            X_hat = self.model(self.X)
-            score = self.log_mse_loss(X_hat, self.X)
+            score = self._score()
             l1_reg = lambda1 * self.model.fc1_l1_reg()
             obj = mu * (score + l1_reg) + h_val
             obj.backward()
@@ -249,7 +317,7 @@ class DagmaNonlinear:
             for p in params:
                 p.grad = None
             h_val = self.model.h_func(s)
-            obj = mu * (self.log_mse_loss(self.model(self.X), self.X) + lambda1 * self.model.fc1_l1_reg()) + h_val
+            obj = mu * (self._score() + lambda1 * self.model.fc1_l1_reg()) + h_val
             obj.backward()
             stream = torch.cuda.current_stream(dev).cuda_stream
             st = C.c_void_p(stream) if stream else None

@@ -61,3 +61,27 @@ def test_nonlinear_h_negative_returns_false():
     assert (h < 0) == (not ok)
     if not ok:
         assert torch.equal(w0, model.fc1.weight.detach())
+
+
+@pytest.mark.parametrize("d,m1,n", [(20, 10, 1000), (200, 10, 1000), (7, 3, 33)])
+def test_fused_tail_matches_torch(d, m1, n):
+    """The fused HIP tail (sigmoid -> LocallyConnected(d, m1, 1) -> sum of squared residuals,
+    csrc/mlp.hip) against the same expression in PyTorch: value and every parameter gradient."""
+    from midagma_amd.nonlinear import DagmaMLP
+    torch.manual_seed(d + m1)
+    model = DagmaMLP(dims=[d, m1, 1]).to("cuda:0")
+    with torch.no_grad():
+        model.fc1.weight.normal_(0, 0.3)
+        model.fc1.bias.normal_(0, 0.1)
+    X = torch.randn(n, d, dtype=torch.float64, device="cuda:0")
+    assert model.fused_tail()
+    out = {}
+    for fused in (True, False):
+        model.zero_grad()
+        v = model.squared_residual(X) if fused else torch.sum((model(X) - X) ** 2)
+        v.backward()
+        out[fused] = (v.item(), {k: p.grad.detach().clone() for k, p in model.named_parameters()})
+    (v1, g1), (v0, g0) = out[True], out[False]
+    assert abs(v1 - v0) <= 1e-12 * abs(v0)
+    for k in g0:
+        assert torch.max(torch.abs(g1[k] - g0[k])).item() <= 1e-11 * max(1e-300, torch.max(torch.abs(g0[k])).item()), k
