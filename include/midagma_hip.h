@@ -184,15 +184,17 @@ int midagma_adam_step_table(double* p, const double* g, double* m, double* v, in
                             const double* gate, void* stream);
 int midagma_counter_advance(int64_t* counter, void* stream);
 
-/* The DagmaMLP tail of dims [d, m1, 1] (m1 <= 16), fused on torch's device memory and stream
- * (replaces sigmoid -> LocallyConnected(d, m1, 1) -> squared residual sum in
+/* The DagmaMLP tail of dims [d, m1, 1] (d * m1 <= 7936), fused on torch's device memory and
+ * stream (replaces sigmoid -> LocallyConnected(d, m1, 1) -> squared residual sum in
  * nonlinear.py:99-104, 139-159 and their autograd backward; dagma/locally_connected.py:55-85).
- * fwd: Z (n x d*m1 row-major) -> R = Xhat - X (n x d), *ssq = sum R^2 (device), part: scratch of
- * ceil(n d / 256) doubles.  bwd: *g = d loss / d ssq (device) -> dZ, dw2 (d x m1), db2 (d). */
+ * scratch: midagma_mlp_tail_scratch(n, d, m1) doubles of device memory.
+ * fwd: Z (n x d*m1 row-major) -> R = Xhat - X (n x d), *ssq = sum R^2 (device).
+ * bwd: *g = d loss / d ssq (device) -> dZ (n x d*m1), dw2 (d x m1), db2 (d). */
+int64_t midagma_mlp_tail_scratch(int64_t n, int64_t d, int64_t m1);
 int midagma_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n, int64_t d,
-                         int64_t m1, double* R, double* part, double* ssq, void* stream);
+                         int64_t m1, double* R, double* scratch, double* ssq, void* stream);
 int midagma_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n, int64_t d,
-                         int64_t m1, double* dZ, double* dw2, double* db2, void* stream);
+                         int64_t m1, double* dZ, double* dw2, double* db2, double* scratch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -122,13 +122,15 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
                      double* Gtrek, hipStream_t stream);
 
 // --- mlp.hip ----------------------------------------------------------------
-constexpr int MLP_TAIL_MAXM = 16;  // hidden width the fused DagmaMLP tail supports
-// Z (n x d*m1) -> R = Xhat - X (n x d), *ssq = sum R^2; part: ceil(n d / 256) doubles
+constexpr int64_t MLP_TAIL_MAX_DM = 7936;  // d * m1 the fused DagmaMLP tail stages per row in LDS
+// doubles of scratch the tail needs (both directions)
+int64_t mlp_tail_scratch(int64_t n, int64_t d, int64_t m1);
+// Z (n x d*m1) -> R = Xhat - X (n x d), *ssq = sum R^2
 void launch_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n, int64_t d,
-                         int m1, double* R, double* part, double* ssq, hipStream_t stream);
+                         int m1, double* R, double* scratch, double* ssq, hipStream_t stream);
 // g (device scalar) = d loss / d ssq -> dZ (n x d*m1), dw2 (d x m1), db2 (d)
 void launch_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n, int64_t d,
-                         int m1, double* dZ, double* dw2, double* db2, hipStream_t stream);
+                         int m1, double* dZ, double* dw2, double* db2, double* scratch, hipStream_t stream);
 
 // --- adam.hip ---------------------------------------------------------------
 struct AdamCoef {  // host-rounded as torch.optim.Adam computes them in Python floats

@@ -6,41 +6,53 @@
 // and its backward for d(ssq) = g:
 //     dXhat = 2 g (Xhat - X),  dZ = dXhat w2 S (1 - S),  dw2[j, m] = sum_r dXhat S,  db2 = sum_r dXhat.
 // Four launches replace the ~20 elementwise/reduction kernels PyTorch runs for the same
-// forward and backward.  Sums over rows run in a fixed order (deterministic).
+// forward and backward.  Every Z access is coalesced (consecutive threads on consecutive
+// columns c = j m1 + m); sums over rows run in a fixed order (deterministic).
+#include <algorithm>
+
 #include "launch.h"
 
 namespace midagma {
 namespace {
 
+constexpr int TAIL_ROWS = 16;  // rows per workgroup of the backward (partials per row chunk)
+
 __device__ __forceinline__ double sigmoid(double z) { return 1.0 / (1.0 + exp(-z)); }
 
-// thread per (row, j): residual R and per-workgroup partial of R^2
-__global__ __launch_bounds__(NTHREADS) void mlp_tail_fwd_kernel(const double* __restrict__ Z,
-                                                                const double* __restrict__ w2,
-                                                                const double* __restrict__ b2,
-                                                                const double* __restrict__ X, int64_t n, int64_t d,
-                                                                int m1, double* __restrict__ R,
-                                                                double* __restrict__ part) {
-  __shared__ double red[NTHREADS];
-  const int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
-  double r2 = 0.0;
-  if (t < n * d) {
-    const int64_t row = t / d, j = t % d;
-    const double* z = Z + row * d * m1 + j * m1;
-    const double* w = w2 + j * m1;
-    double acc = 0.0;
-    for (int m = 0; m < m1; ++m) acc += sigmoid(z[m]) * w[m];
-    const double r = (acc + b2[j]) - X[t];
-    R[t] = r;
-    r2 = r * r;
-  }
-  red[threadIdx.x] = r2;
+__device__ __forceinline__ double block_sum256(double v, double* red) {
+  red[threadIdx.x] = v;
   __syncthreads();
   for (int s = NTHREADS / 2; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// workgroup per row: S w2 staged in LDS (coalesced over the row's d m1 columns), then thread
+// j < d sums its m1 terms: R[row, j] = Xhat - X, part[row] = sum_j R^2
+__global__ __launch_bounds__(NTHREADS) void mlp_tail_fwd_kernel(const double* __restrict__ Z,
+                                                                const double* __restrict__ w2,
+                                                                const double* __restrict__ b2,
+                                                                const double* __restrict__ X, int64_t d, int m1,
+                                                                double* __restrict__ R, double* __restrict__ part) {
+  extern __shared__ double sw[];  // d m1 products, then the reduction scratch
+  const int64_t row = blockIdx.x, dm = d * m1;
+  const double* z = Z + row * dm;
+  for (int64_t c = threadIdx.x; c < dm; c += NTHREADS) sw[c] = sigmoid(z[c]) * w2[c];
+  __syncthreads();
+  double r2 = 0.0;
+  for (int64_t j = threadIdx.x; j < d; j += NTHREADS) {
+    double acc = 0.0;
+    for (int m = 0; m < m1; ++m) acc += sw[j * m1 + m];
+    const double r = (acc + b2[j]) - X[row * d + j];
+    R[row * d + j] = r;
+    r2 += r * r;
+  }
+  const double t = block_sum256(r2, sw + dm);
+  if (threadIdx.x == 0) part[row] = t;
 }
 
 // one workgroup: out[0] = sum of the np partials (fixed order)
@@ -49,93 +61,82 @@ __global__ __launch_bounds__(NTHREADS) void mlp_sum_kernel(const double* __restr
   __shared__ double red[NTHREADS];
   double a = 0.0;
   for (int64_t i = threadIdx.x; i < np; i += NTHREADS) a += part[i];
-  red[threadIdx.x] = a;
-  __syncthreads();
-  for (int s = NTHREADS / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[0] = red[0];
+  const double t = block_sum256(a, red);
+  if (threadIdx.x == 0) out[0] = t;
 }
 
-// thread per (row, j): dZ[row, j, :]
-__global__ __launch_bounds__(NTHREADS) void mlp_tail_dz_kernel(const double* __restrict__ Z,
-                                                               const double* __restrict__ w2,
-                                                               const double* __restrict__ R,
-                                                               const double* __restrict__ g, int64_t n, int64_t d,
-                                                               int m1, double* __restrict__ dZ) {
-  const int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
-  if (t >= n * d) return;
-  const int64_t row = t / d, j = t % d;
-  const double dxh = 2.0 * g[0] * R[t];
-  const double* z = Z + row * d * m1 + j * m1;
-  const double* w = w2 + j * m1;
-  double* dz = dZ + row * d * m1 + j * m1;
-  for (int m = 0; m < m1; ++m) {
-    const double s = sigmoid(z[m]);
-    dz[m] = dxh * w[m] * (s * (1.0 - s));
-  }
-}
-
-// workgroup per node j: dw2[j, :] and db2[j], sums over the rows in a fixed order
-template <int MAXM>
-__global__ __launch_bounds__(NTHREADS) void mlp_tail_dw_kernel(const double* __restrict__ Z,
-                                                               const double* __restrict__ R,
-                                                               const double* __restrict__ g, int64_t n, int64_t d,
-                                                               int m1, double* __restrict__ dw2,
-                                                               double* __restrict__ db2) {
-  __shared__ double red[NTHREADS];
-  const int64_t j = blockIdx.x;
-  double acc[MAXM + 1];
-#pragma unroll
-  for (int m = 0; m <= MAXM; ++m) acc[m] = 0.0;
-  const double g2 = 2.0 * g[0];
-  for (int64_t row = threadIdx.x; row < n; row += NTHREADS) {
+// grid (column tiles of 256, row chunks of TAIL_ROWS): thread per column c = j m1 + m over
+// the chunk's rows: dZ, and the chunk's partials of dw2 (pw[chunk][c]) and db2 (pb[chunk][j])
+__global__ __launch_bounds__(NTHREADS) void mlp_tail_bwd_kernel(const double* __restrict__ Z,
+                                                                const double* __restrict__ w2,
+                                                                const double* __restrict__ R,
+                                                                const double* __restrict__ g, int64_t n, int64_t d,
+                                                                int m1, double* __restrict__ dZ,
+                                                                double* __restrict__ pw, double* __restrict__ pb) {
+  const int64_t dm = d * m1;
+  const int64_t c = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  if (c >= dm) return;
+  const int64_t j = c / m1;
+  const int m = (int)(c % m1);
+  const double w = w2[c], g2 = 2.0 * g[0];
+  const int64_t r0 = (int64_t)blockIdx.y * TAIL_ROWS, r1 = r0 + TAIL_ROWS < n ? r0 + TAIL_ROWS : n;
+  double aw = 0.0, ab = 0.0;
+  for (int64_t row = r0; row < r1; ++row) {
     const double dxh = g2 * R[row * d + j];
-    const double* z = Z + row * d * m1 + j * m1;
-#pragma unroll
-    for (int m = 0; m < MAXM; ++m)
-      if (m < m1) acc[m] += dxh * sigmoid(z[m]);
-    acc[MAXM] += dxh;
+    const double s = sigmoid(Z[row * dm + c]);
+    dZ[row * dm + c] = dxh * w * (s * (1.0 - s));
+    aw += dxh * s;
+    ab += dxh;
   }
-#pragma unroll
-  for (int m = 0; m <= MAXM; ++m) {
-    if (m < m1 || m == MAXM) {
-      red[threadIdx.x] = acc[m];
-      __syncthreads();
-      for (int s = NTHREADS / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) {
-        if (m == MAXM)
-          db2[j] = red[0];
-        else
-          dw2[j * m1 + m] = red[0];
-      }
-      __syncthreads();
-    }
+  pw[(int64_t)blockIdx.y * dm + c] = aw;
+  if (m == 0) pb[(int64_t)blockIdx.y * d + j] = ab;
+}
+
+// dw2[c] = sum over chunks of pw[.][c], db2[j] likewise (fixed order)
+__global__ __launch_bounds__(NTHREADS) void mlp_tail_dw_kernel(const double* __restrict__ pw,
+                                                               const double* __restrict__ pb, int64_t nchunk,
+                                                               int64_t d, int m1, double* __restrict__ dw2,
+                                                               double* __restrict__ db2) {
+  const int64_t dm = d * m1;
+  const int64_t c = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  if (c < dm) {
+    double a = 0.0;
+    for (int64_t k = 0; k < nchunk; ++k) a += pw[k * dm + c];
+    dw2[c] = a;
+  } else if (c < dm + d) {
+    const int64_t j = c - dm;
+    double a = 0.0;
+    for (int64_t k = 0; k < nchunk; ++k) a += pb[k * d + j];
+    db2[j] = a;
   }
 }
 
 }  // namespace
 
+int64_t mlp_tail_scratch(int64_t n, int64_t d, int64_t m1) {
+  const int64_t chunks = (n + TAIL_ROWS - 1) / TAIL_ROWS;
+  return std::max<int64_t>(n, chunks * (d * m1 + d));
+}
+
 void launch_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n, int64_t d,
                          int m1, double* R, double* part, double* ssq, hipStream_t stream) {
-  const int64_t blocks = (n * d + NTHREADS - 1) / NTHREADS;
-  hipLaunchKernelGGL(mlp_tail_fwd_kernel, dim3((unsigned)blocks), dim3(NTHREADS), 0, stream, Z, w2, b2, X, n, d, m1,
-                     R, part);
-  hipLaunchKernelGGL(mlp_sum_kernel, dim3(1), dim3(NTHREADS), 0, stream, part, blocks, ssq);
+  if (d * m1 > MLP_TAIL_MAX_DM) throw std::invalid_argument("mlp tail: d * m1 above the LDS row stage");
+  const size_t lds = (size_t)(d * m1 + NTHREADS) * sizeof(double);
+  hipLaunchKernelGGL(mlp_tail_fwd_kernel, dim3((unsigned)n), dim3(NTHREADS), lds, stream, Z, w2, b2, X, d, m1, R,
+                     part);
+  hipLaunchKernelGGL(mlp_sum_kernel, dim3(1), dim3(NTHREADS), 0, stream, part, n, ssq);
   HIP_TRY(hipGetLastError());
 }
 
 void launch_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n, int64_t d,
-                         int m1, double* dZ, double* dw2, double* db2, hipStream_t stream) {
-  if (m1 > MLP_TAIL_MAXM) throw std::invalid_argument("mlp tail: hidden width above 16");
-  const int64_t blocks = (n * d + NTHREADS - 1) / NTHREADS;
-  hipLaunchKernelGGL(mlp_tail_dz_kernel, dim3((unsigned)blocks), dim3(NTHREADS), 0, stream, Z, w2, R, g, n, d, m1, dZ);
-  hipLaunchKernelGGL(mlp_tail_dw_kernel<MLP_TAIL_MAXM>, dim3((unsigned)d), dim3(NTHREADS), 0, stream, Z, R, g, n, d,
-                     m1, dw2, db2);
+                         int m1, double* dZ, double* dw2, double* db2, double* scratch, hipStream_t stream) {
+  const int64_t dm = d * m1, chunks = (n + TAIL_ROWS - 1) / TAIL_ROWS;
+  double* pw = scratch;
+  double* pb = scratch + chunks * dm;
+  hipLaunchKernelGGL(mlp_tail_bwd_kernel, dim3((unsigned)((dm + NTHREADS - 1) / NTHREADS), (unsigned)chunks),
+                     dim3(NTHREADS), 0, stream, Z, w2, R, g, n, d, m1, dZ, pw, pb);
+  hipLaunchKernelGGL(mlp_tail_dw_kernel, dim3((unsigned)((dm + d + NTHREADS - 1) / NTHREADS)), dim3(NTHREADS), 0,
+                     stream, pw, pb, chunks, d, m1, dw2, db2);
   HIP_TRY(hipGetLastError());
 }
 

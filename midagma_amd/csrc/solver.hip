@@ -1419,22 +1419,29 @@ extern "C" int midagma_sem_linear(const double* W, int64_t d, int64_t row0, int6
 
 // ---------------------------------------------------------------------------
 // Gated Adam step (adam.hip) for DagmaNonlinear on torch tensors
+extern "C" int64_t midagma_mlp_tail_scratch(int64_t n, int64_t d, int64_t m1) {
+  if (n < 1 || d < 1 || m1 < 1) return 0;
+  return mlp_tail_scratch(n, d, m1);
+}
+
 extern "C" int midagma_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n,
-                                    int64_t d, int64_t m1, double* R, double* part, double* ssq, void* stream) {
-  if (!Z || !w2 || !b2 || !X || !R || !part || !ssq || n < 1 || d < 1 || m1 < 1 || m1 > MLP_TAIL_MAXM)
+                                    int64_t d, int64_t m1, double* R, double* scratch, double* ssq, void* stream) {
+  if (!Z || !w2 || !b2 || !X || !R || !scratch || !ssq || n < 1 || d < 1 || m1 < 1 || d * m1 > MLP_TAIL_MAX_DM)
     return fail(nullptr, MIDAGMA_E_ARG, "mlp_tail_fwd: bad arguments");
   return guarded(nullptr, [&] {
-    launch_mlp_tail_fwd(Z, w2, b2, X, n, d, (int)m1, R, part, ssq, reinterpret_cast<hipStream_t>(stream));
+    launch_mlp_tail_fwd(Z, w2, b2, X, n, d, (int)m1, R, scratch, ssq, reinterpret_cast<hipStream_t>(stream));
     return MIDAGMA_OK;
   });
 }
 
 extern "C" int midagma_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n,
-                                    int64_t d, int64_t m1, double* dZ, double* dw2, double* db2, void* stream) {
-  if (!Z || !w2 || !R || !g || !dZ || !dw2 || !db2 || n < 1 || d < 1 || m1 < 1 || m1 > MLP_TAIL_MAXM)
+                                    int64_t d, int64_t m1, double* dZ, double* dw2, double* db2, double* scratch,
+                                    void* stream) {
+  if (!Z || !w2 || !R || !g || !dZ || !dw2 || !db2 || !scratch || n < 1 || d < 1 || m1 < 1 ||
+      d * m1 > MLP_TAIL_MAX_DM)
     return fail(nullptr, MIDAGMA_E_ARG, "mlp_tail_bwd: bad arguments");
   return guarded(nullptr, [&] {
-    launch_mlp_tail_bwd(Z, w2, R, g, n, d, (int)m1, dZ, dw2, db2, reinterpret_cast<hipStream_t>(stream));
+    launch_mlp_tail_bwd(Z, w2, R, g, n, d, (int)m1, dZ, dw2, db2, scratch, reinterpret_cast<hipStream_t>(stream));
     return MIDAGMA_OK;
   });
 }

@@ -68,7 +68,7 @@ class _MLPTail(torch.autograd.Function):
         Z, w2, b2, X = Z.contiguous(), w2.contiguous(), b2.contiguous(), X.contiguous()
         n, d = X.shape
         R = torch.empty_like(X)
-        part = torch.empty((n * d + 255) // 256, dtype=torch.float64, device=X.device)
+        part = torch.empty(int(_lib.lib().midagma_mlp_tail_scratch(n, d, m1)), dtype=torch.float64, device=X.device)
         ssq = torch.empty((), dtype=torch.float64, device=X.device)
         stream = torch.cuda.current_stream(X.device).cuda_stream
         with torch.cuda.device(X.device):
@@ -76,14 +76,14 @@ class _MLPTail(torch.autograd.Function):
                 C.c_void_p(Z.data_ptr()), C.c_void_p(w2.data_ptr()), C.c_void_p(b2.data_ptr()),
                 C.c_void_p(X.data_ptr()), n, d, m1, C.c_void_p(R.data_ptr()), C.c_void_p(part.data_ptr()),
                 C.c_void_p(ssq.data_ptr()), C.c_void_p(stream) if stream else None), None, "mlp_tail_fwd")
-        ctx.save_for_backward(Z, w2, R)
+        ctx.save_for_backward(Z, w2, R, part)
         ctx.m1 = m1
         ctx.b2_shape = b2.shape
         return ssq
 
     @staticmethod
     def backward(ctx, g):
-        Z, w2, R = ctx.saved_tensors
+        Z, w2, R, scratch = ctx.saved_tensors
         n, d = R.shape
         g = g.contiguous()
         dZ = torch.empty_like(Z)
@@ -94,7 +94,8 @@ class _MLPTail(torch.autograd.Function):
             _lib.check(_lib.lib().midagma_mlp_tail_bwd(
                 C.c_void_p(Z.data_ptr()), C.c_void_p(w2.data_ptr()), C.c_void_p(R.data_ptr()),
                 C.c_void_p(g.data_ptr()), n, d, ctx.m1, C.c_void_p(dZ.data_ptr()), C.c_void_p(dw2.data_ptr()),
-                C.c_void_p(db2.data_ptr()), C.c_void_p(stream) if stream else None), None, "mlp_tail_bwd")
+                C.c_void_p(db2.data_ptr()), C.c_void_p(scratch.data_ptr()), C.c_void_p(stream) if stream else None),
+                None, "mlp_tail_bwd")
         return dZ, dw2, db2, None, None
 
 
@@ -164,13 +165,13 @@ class DagmaMLP(nn.Module):
 
     def fused_tail(self) -> bool:
         """True when sum((self(X) - X)^2) can run as the fused HIP tail: one hidden layer, a
-        width-1 output, biases, float64 on a ROCm device, hidden width <= 16."""
+        width-1 output, biases, float64 on a ROCm device, d * m1 <= 7936 (one row staged in LDS)."""
         if len(self.fc2) != 1 or os.environ.get("MIDAGMA_NO_MLP_TAIL"):
             return False
         fc = self.fc2[0]
         w = fc.weight
         return (fc.output_features == 1 and fc.bias is not None and self.fc1.bias is not None and w.is_cuda
-                and w.dtype == torch.float64 and 1 <= self.dims[1] <= 16)
+                and w.dtype == torch.float64 and self.d * self.dims[1] <= 7936)
 
     def squared_residual(self, x: torch.Tensor) -> torch.Tensor:
         """sum((self(x) - x)^2), the sum inside the log-MSE score (nonlinear.py:139-159)."""
