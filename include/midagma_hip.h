@@ -193,6 +193,19 @@ int midagma_counter_advance(int64_t* counter, void* stream);
 int64_t midagma_mlp_tail_scratch(int64_t n, int64_t d, int64_t m1);
 int midagma_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n, int64_t d,
                          int64_t m1, double* R, double* scratch, double* ssq, void* stream);
+/* The rest of the [d, m1, 1] DagmaMLP objective (nonlinear.py:68-86, 139-159, 198-206):
+ * fc1_terms: A[i, j] = sum_m W1[j m1 + m, i]^2 (d x d, the log-det operand) and the |W1| partial
+ * sums l1part (midagma_fc1_terms_parts(d) doubles); its backward dW1 = 2 W1 gA^T + gl1 sign(W1).
+ * mlp_objective: *obj = mu (half_d log(inv_n *ssq) + lambda1 sum(l1part)) + *h, and its
+ * backward from *g: *gssq, gl1part[*], *gh.  All device pointers, on `stream`. */
+int64_t midagma_fc1_terms_parts(int64_t d);
+int midagma_fc1_terms(const double* W1, int64_t d, int64_t m1, double* A, double* l1part, void* stream);
+int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gl1part,
+                          double* dW1, void* stream);
+int midagma_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
+                          double lambda1, double half_d, double inv_n, double* obj, void* stream);
+int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,
+                              double inv_n, double* gssq, double* gl1part, double* gh, void* stream);
 int midagma_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n, int64_t d,
                          int64_t m1, double* dZ, double* dw2, double* db2, double* scratch, void* stream);
 

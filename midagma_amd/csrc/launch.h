@@ -132,6 +132,18 @@ void launch_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, co
 void launch_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n, int64_t d,
                          int m1, double* dZ, double* dw2, double* db2, double* scratch, hipStream_t stream);
 
+// fc1 terms of the [d, m1, 1] DagmaMLP: A[i, j] = sum_m W1[j m1 + m, i]^2, |W1| partial sums
+// (fc1_terms_parts(d) of them); backward dW1 = 2 W1 gA^T + gl1part sign(W1)
+int64_t fc1_terms_parts(int64_t d);
+void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1part, hipStream_t stream);
+void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gl1part, double* dW1,
+                          hipStream_t stream);
+// obj = mu (half_d log(inv_n ssq) + lambda1 sum(l1part)) + h and its backward
+void launch_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
+                          double lambda1, double half_d, double inv_n, double* out, hipStream_t stream);
+void launch_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,
+                              double inv_n, double* gssq, double* gl1part, double* gh, hipStream_t stream);
+
 // --- adam.hip ---------------------------------------------------------------
 struct AdamCoef {  // host-rounded as torch.optim.Adam computes them in Python floats
   double step_size, w1, beta2, c2, bc2_sqrt, eps, wd;

@@ -141,3 +141,121 @@ void launch_mlp_tail_bwd(const double* Z, const double* w2, const double* R, con
 }
 
 }  // namespace midagma
+
+// ---- the fc1 terms and the scalar objective (nonlinear.py:68-86, 139-159, 198-206) ------
+namespace midagma {
+namespace {
+
+// thread per (j, i): A[i, j] = sum_m W1[j m1 + m, i]^2 (the reference's sum of fc1_weight**2
+// over m, transposed, nonlinear.py:83-84); the workgroup's sum of |W1| -> l1part[wg]
+__global__ __launch_bounds__(NTHREADS) void fc1_terms_kernel(const double* __restrict__ W1, int64_t d, int m1,
+                                                             double* __restrict__ A, double* __restrict__ l1part) {
+  __shared__ double red[NTHREADS];
+  const int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  double al = 0.0;
+  if (t < d * d) {
+    const int64_t j = t / d, i = t % d;
+    double acc = 0.0;
+    for (int m = 0; m < m1; ++m) {
+      const double w = W1[(j * m1 + m) * d + i];
+      acc += w * w;
+      al += fabs(w);
+    }
+    A[i * d + j] = acc;
+  }
+  red[threadIdx.x] = al;
+  __syncthreads();
+  for (int s = NTHREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) l1part[blockIdx.x] = red[0];
+}
+
+// dW1[j m1 + m, i] = 2 W1 gA[i, j] + gl1[wg(j, i)] sign(W1)
+__global__ __launch_bounds__(NTHREADS) void fc1_terms_bwd_kernel(const double* __restrict__ W1, int64_t d, int m1,
+                                                                 const double* __restrict__ gA,
+                                                                 const double* __restrict__ gl1,
+                                                                 double* __restrict__ dW1) {
+  const int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  if (t >= d * d) return;
+  const int64_t j = t / d, i = t % d;
+  const double ga = gA[i * d + j], gl = gl1[blockIdx.x];
+  for (int m = 0; m < m1; ++m) {
+    const int64_t e = (j * m1 + m) * d + i;
+    const double w = W1[e];
+    const double sg = w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : 0.0);
+    dW1[e] = ga * (2.0 * w) + gl * sg;
+  }
+}
+
+// one workgroup: obj = mu (0.5 d log(1/n ssq) + lambda1 sum(l1part)) + h, the reference's
+// association (nonlinear.py:158, 203-204)
+__global__ __launch_bounds__(NTHREADS) void mlp_objective_kernel(const double* __restrict__ ssq,
+                                                                 const double* __restrict__ l1part, int64_t np,
+                                                                 const double* __restrict__ h, double mu,
+                                                                 double lambda1, double half_d, double inv_n,
+                                                                 double* __restrict__ out) {
+  __shared__ double red[NTHREADS];
+  double a = 0.0;
+  for (int64_t k = threadIdx.x; k < np; k += NTHREADS) a += l1part[k];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = NTHREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double score = half_d * log(inv_n * ssq[0]);
+    out[0] = mu * (score + lambda1 * red[0]) + h[0];
+  }
+}
+
+// g = d L / d obj -> d/d ssq, d/d l1part (every entry), d/d h, in autograd's order
+__global__ __launch_bounds__(NTHREADS) void mlp_objective_bwd_kernel(const double* __restrict__ g,
+                                                                     const double* __restrict__ ssq, int64_t np,
+                                                                     double mu, double lambda1, double half_d,
+                                                                     double inv_n, double* __restrict__ gssq,
+                                                                     double* __restrict__ gl1part,
+                                                                     double* __restrict__ gh) {
+  const double gv = g[0], inner = gv * mu;
+  const double gl1 = inner * lambda1;
+  for (int64_t k = threadIdx.x; k < np; k += NTHREADS) gl1part[k] = gl1;
+  if (threadIdx.x == 0) {
+    gh[0] = gv;
+    gssq[0] = ((inner * half_d) / (inv_n * ssq[0])) * inv_n;
+  }
+}
+
+}  // namespace
+
+int64_t fc1_terms_parts(int64_t d) { return (d * d + NTHREADS - 1) / NTHREADS; }
+
+void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1part, hipStream_t stream) {
+  hipLaunchKernelGGL(fc1_terms_kernel, dim3((unsigned)fc1_terms_parts(d)), dim3(NTHREADS), 0, stream, W1, d, m1, A,
+                     l1part);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gl1part, double* dW1,
+                          hipStream_t stream) {
+  hipLaunchKernelGGL(fc1_terms_bwd_kernel, dim3((unsigned)fc1_terms_parts(d)), dim3(NTHREADS), 0, stream, W1, d, m1,
+                     gA, gl1part, dW1);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
+                          double lambda1, double half_d, double inv_n, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(mlp_objective_kernel, dim3(1), dim3(NTHREADS), 0, stream, ssq, l1part, np, h, mu, lambda1, half_d,
+                     inv_n, out);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,
+                              double inv_n, double* gssq, double* gl1part, double* gh, hipStream_t stream) {
+  hipLaunchKernelGGL(mlp_objective_bwd_kernel, dim3(1), dim3(NTHREADS), 0, stream, g, ssq, np, mu, lambda1, half_d,
+                     inv_n, gssq, gl1part, gh);
+  HIP_TRY(hipGetLastError());
+}
+
+}  // namespace midagma

@@ -1446,6 +1446,47 @@ extern "C" int midagma_mlp_tail_bwd(const double* Z, const double* w2, const dou
   });
 }
 
+extern "C" int64_t midagma_fc1_terms_parts(int64_t d) { return d < 1 ? 0 : fc1_terms_parts(d); }
+
+extern "C" int midagma_fc1_terms(const double* W1, int64_t d, int64_t m1, double* A, double* l1part, void* stream) {
+  if (!W1 || !A || !l1part || d < 1 || m1 < 1) return fail(nullptr, MIDAGMA_E_ARG, "fc1_terms: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_fc1_terms(W1, d, (int)m1, A, l1part, reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gl1part,
+                                     double* dW1, void* stream) {
+  if (!W1 || !gA || !gl1part || !dW1 || d < 1 || m1 < 1)
+    return fail(nullptr, MIDAGMA_E_ARG, "fc1_terms_bwd: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_fc1_terms_bwd(W1, d, (int)m1, gA, gl1part, dW1, reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
+                                     double lambda1, double half_d, double inv_n, double* obj, void* stream) {
+  if (!ssq || !l1part || !h || !obj || np < 1) return fail(nullptr, MIDAGMA_E_ARG, "mlp_objective: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_mlp_objective(ssq, l1part, np, h, mu, lambda1, half_d, inv_n, obj, reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1,
+                                         double half_d, double inv_n, double* gssq, double* gl1part, double* gh,
+                                         void* stream) {
+  if (!g || !ssq || !gssq || !gl1part || !gh || np < 1)
+    return fail(nullptr, MIDAGMA_E_ARG, "mlp_objective_bwd: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_mlp_objective_bwd(g, ssq, np, mu, lambda1, half_d, inv_n, gssq, gl1part, gh,
+                             reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
 extern "C" int midagma_adam_step(double* p, const double* g, double* m, double* v, int64_t n, double step_size,
                                  double w1, double beta2, double c2, double bc2_sqrt, double eps, double wd,
                                  const double* gate, void* stream) {
