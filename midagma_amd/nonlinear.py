@@ -12,10 +12,11 @@ row 4; BASELINE config 5); only ``h_func`` (nonlinear.py:68-86) is replaced:
 The C entry point (`midagma_logdet_inv_dev`) works on torch's device memory
 and current HIP stream; it never synchronizes with the host.
 
-For the [d, m1, 1] model (BASELINE config 5) the score's squared residual sum runs as one
-fused HIP tail (`midagma_mlp_tail_fwd` / `_bwd`, csrc/mlp.hip): sigmoid, the width-1
-LocallyConnected layer with its bias, the residual sum and their backward in four launches
-instead of PyTorch's ~20 elementwise and reduction kernels (MIDAGMA_NO_MLP_TAIL=1: PyTorch).
+For the [d, m1, 1] model (BASELINE config 5) the objective runs on fused HIP kernels
+(csrc/mlp.hip): the fc1 terms (A and the |fc1| sum, one launch), the tail (sigmoid, the
+width-1 LocallyConnected layer with its bias and the squared residual sum, two launches) and
+the scalar objective (one launch), each with a fused backward, instead of PyTorch's ~40
+elementwise, reduction and scalar kernels (MIDAGMA_NO_MLP_TAIL=1: the PyTorch expressions).
 """
 from __future__ import annotations
 
@@ -97,6 +98,78 @@ class _MLPTail(torch.autograd.Function):
                 C.c_void_p(db2.data_ptr()), C.c_void_p(scratch.data_ptr()), C.c_void_p(stream) if stream else None),
                 None, "mlp_tail_bwd")
         return dZ, dw2, db2, None, None
+
+
+class _Fc1Terms(torch.autograd.Function):
+    """(A, l1 partial sums) of fc1's weight for a [d, m1, 1] DagmaMLP in one launch:
+    A[i, j] = sum_m W1[j m1 + m, i]^2 (nonlinear.py:83-84), |W1| summed per workgroup."""
+
+    @staticmethod
+    def forward(ctx, W1: torch.Tensor, d: int, m1: int):
+        W1 = W1.contiguous()
+        A = torch.empty((d, d), dtype=torch.float64, device=W1.device)
+        l1part = torch.empty(int(_lib.lib().midagma_fc1_terms_parts(d)), dtype=torch.float64, device=W1.device)
+        stream = torch.cuda.current_stream(W1.device).cuda_stream
+        with torch.cuda.device(W1.device):
+            _lib.check(_lib.lib().midagma_fc1_terms(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(A.data_ptr()),
+                                                    C.c_void_p(l1part.data_ptr()),
+                                                    C.c_void_p(stream) if stream else None), None, "fc1_terms")
+        ctx.save_for_backward(W1)
+        ctx.dims = (d, m1)
+        return A, l1part
+
+    @staticmethod
+    def backward(ctx, gA, gl1part):
+        (W1,) = ctx.saved_tensors
+        d, m1 = ctx.dims
+        gA = torch.zeros((d, d), dtype=torch.float64, device=W1.device) if gA is None else gA.contiguous()
+        if gl1part is None:
+            gl1part = torch.zeros(int(_lib.lib().midagma_fc1_terms_parts(d)), dtype=torch.float64, device=W1.device)
+        gl1part = gl1part.contiguous()
+        dW1 = torch.empty_like(W1)
+        stream = torch.cuda.current_stream(W1.device).cuda_stream
+        with torch.cuda.device(W1.device):
+            _lib.check(_lib.lib().midagma_fc1_terms_bwd(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(gA.data_ptr()),
+                                                        C.c_void_p(gl1part.data_ptr()), C.c_void_p(dW1.data_ptr()),
+                                                        C.c_void_p(stream) if stream else None), None,
+                       "fc1_terms_bwd")
+        return dW1, None, None
+
+
+class _Objective(torch.autograd.Function):
+    """mu * (0.5 d log(1/n ssq) + lambda1 * sum(l1part)) + h in one launch, and its backward in
+    one (nonlinear.py:158, 203-204): replaces a dozen scalar PyTorch kernels per direction."""
+
+    @staticmethod
+    def forward(ctx, ssq, l1part, h, mu: float, lambda1: float, n: int, d: int):
+        obj = torch.empty((), dtype=torch.float64, device=ssq.device)
+        half_d, inv_n = 0.5 * d, 1 / n
+        stream = torch.cuda.current_stream(ssq.device).cuda_stream
+        h = h.contiguous()
+        with torch.cuda.device(ssq.device):
+            _lib.check(_lib.lib().midagma_mlp_objective(
+                C.c_void_p(ssq.data_ptr()), C.c_void_p(l1part.data_ptr()), l1part.numel(), C.c_void_p(h.data_ptr()),
+                float(mu), float(lambda1), half_d, inv_n, C.c_void_p(obj.data_ptr()),
+                C.c_void_p(stream) if stream else None), None, "mlp_objective")
+        ctx.save_for_backward(ssq)
+        ctx.consts = (float(mu), float(lambda1), half_d, inv_n, l1part.numel())
+        return obj
+
+    @staticmethod
+    def backward(ctx, g):
+        (ssq,) = ctx.saved_tensors
+        mu, lambda1, half_d, inv_n, np_ = ctx.consts
+        g = g.contiguous()
+        gssq = torch.empty((), dtype=torch.float64, device=ssq.device)
+        gl1 = torch.empty(np_, dtype=torch.float64, device=ssq.device)
+        gh = torch.empty((), dtype=torch.float64, device=ssq.device)
+        stream = torch.cuda.current_stream(ssq.device).cuda_stream
+        with torch.cuda.device(ssq.device):
+            _lib.check(_lib.lib().midagma_mlp_objective_bwd(
+                C.c_void_p(g.data_ptr()), C.c_void_p(ssq.data_ptr()), np_, mu, lambda1, half_d, inv_n,
+                C.c_void_p(gssq.data_ptr()), C.c_void_p(gl1.data_ptr()), C.c_void_p(gh.data_ptr()),
+                C.c_void_p(stream) if stream else None), None, "mlp_objective_bwd")
+        return gssq, gl1, gh, None, None, None, None
 
 
 def logdet_h(A: torch.Tensor, s: float = 1.0) -> torch.Tensor:
@@ -224,6 +297,22 @@ class DagmaNonlinear:
         n, d = target.shape
         return 0.5 * d * torch.log(1 / n * torch.sum((output - target) ** 2))
 
+    def _h_and_objective(self, mu: float, lambda1: float, s: float):
+        """(h, mu * (score + lambda1 * |fc1|_1) + h) (nonlinear.py:198-204): for a [d, m1, 1] MLP
+        on the GPU through the fused kernels (fc1 terms, log-det, tail, scalar objective),
+        otherwise the reference's expressions."""
+        m = self.model
+        if getattr(m, "fused_tail", lambda: False)():
+            n, d = self.X.shape
+            m1 = m.dims[1]
+            fc = m.fc2[0]
+            A, l1part = _Fc1Terms.apply(m.fc1.weight, d, m1)
+            h_val = logdet_h(A, s)
+            ssq = _MLPTail.apply(m.fc1(self.X), fc.weight, fc.bias, self.X, m1)
+            return h_val, _Objective.apply(ssq, l1part, h_val, mu, lambda1, n, d)
+        h_val = m.h_func(s)
+        return h_val, mu * (self._score() + lambda1 * m.fc1_l1_reg()) + h_val
+
     def _score(self) -> torch.Tensor:
         """log_mse_loss(model(X), X); the squared residual sum through the model's fused tail
         when it has one (same expression around it: 0.5 d log(1/n ssq))."""
@@ -258,10 +347,7 @@ class DagmaNonlinear:
         for i in range(max_iter):
             for p in params:
                 p.grad = None
-            h_val = self.model.h_func(s)
-            score = self._score()
-            l1_reg = lambda1 * self.model.fc1_l1_reg()
-            obj = mu * (score + l1_reg) + h_val
+            h_val, obj = self._h_and_objective(mu, lambda1, s)
             obj.backward()
             step = i + 1
             bc1 = 1 - beta1 ** step
@@ -317,8 +403,7 @@ class DagmaNonlinear:
         def body(gate):
             for p in params:
                 p.grad = None
-            h_val = self.model.h_func(s)
-            obj = mu * (self._score() + lambda1 * self.model.fc1_l1_reg()) + h_val
+            h_val, obj = self._h_and_objective(mu, lambda1, s)
             obj.backward()
             stream = torch.cuda.current_stream(dev).cuda_stream
             st = C.c_void_p(stream) if stream else None

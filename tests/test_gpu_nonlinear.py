@@ -85,3 +85,31 @@ def test_fused_tail_matches_torch(d, m1, n):
     assert abs(v1 - v0) <= 1e-12 * abs(v0)
     for k in g0:
         assert torch.max(torch.abs(g1[k] - g0[k])).item() <= 1e-11 * max(1e-300, torch.max(torch.abs(g0[k])).item()), k
+
+
+def test_fused_objective_matches_torch(monkeypatch):
+    """mu * (log-MSE score + lambda1 |fc1|_1) + h through the fused kernels (fc1 terms, log-det,
+    tail, scalar objective) against the reference's PyTorch expressions: value, h and every
+    parameter gradient."""
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    d, m1, n = 30, 10, 500
+    torch.manual_seed(3)
+    model = DagmaMLP(dims=[d, m1, 1]).to("cuda:0")
+    with torch.no_grad():
+        model.fc1.weight.normal_(0, 0.05)
+        model.fc1.bias.normal_(0, 0.1)
+    dn = DagmaNonlinear(model, device=0)
+    dn.X = torch.randn(n, d, dtype=torch.float64, device="cuda:0")
+    res = {}
+    for fused in (True, False):
+        if not fused:
+            monkeypatch.setenv("MIDAGMA_NO_MLP_TAIL", "1")
+        assert model.fused_tail() == fused
+        model.zero_grad()
+        h, obj = dn._h_and_objective(0.1, 0.02, 1.0)
+        obj.backward()
+        res[fused] = (h.item(), obj.item(), {k: p.grad.detach().clone() for k, p in model.named_parameters()})
+    (h1, o1, g1), (h0, o0, g0) = res[True], res[False]
+    assert abs(h1 - h0) <= 1e-12 * max(1.0, abs(h0)) and abs(o1 - o0) <= 1e-12 * abs(o0)
+    for k in g0:
+        assert torch.max(torch.abs(g1[k] - g0[k])).item() <= 1e-10 * max(1e-300, torch.max(torch.abs(g0[k])).item()), k
