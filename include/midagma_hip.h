@@ -183,6 +183,12 @@ int midagma_adam_step_table(double* p, const double* g, double* m, double* v, in
                             const int64_t* counter, double w1, double beta2, double c2, double eps, double wd,
                             const double* gate, void* stream);
 int midagma_counter_advance(int64_t* counter, void* stream);
+/* midagma_adam_step_table over k <= 8 tensors (host arrays of their device pointers and
+ * sizes) in one launch. */
+int midagma_adam_step_table_multi(int64_t k, double* const* p, const double* const* g, double* const* m,
+                                  double* const* v, const int64_t* n, const double* table, const int64_t* counter,
+                                  double w1, double beta2, double c2, double eps, double wd, const double* gate,
+                                  void* stream);
 
 /* The DagmaMLP tail of dims [d, m1, 1] (d * m1 <= 7936), fused on torch's device memory and
  * stream (replaces sigmoid -> LocallyConnected(d, m1, 1) -> squared residual sum in

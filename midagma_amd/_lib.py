@@ -90,6 +90,7 @@ EXPORTED = {
     "midagma_adam_step": (_int, [_vp, _vp, _vp, _vp, _i64, _d, _d, _d, _d, _d, _d, _d, _vp, _vp]),
     "midagma_adam_step_table": (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _d, _d, _d, _d, _d, _vp, _vp]),
     "midagma_counter_advance": (_int, [_vp, _vp]),
+    "midagma_adam_step_table_multi": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _d, _d, _d, _d, _vp, _vp]),
     "midagma_mlp_tail_scratch": (_i64, [_i64, _i64, _i64]),
     "midagma_fc1_terms_parts": (_i64, [_i64]),
     "midagma_fc1_terms": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),

@@ -155,6 +155,18 @@ void launch_adam_gated(double* p, const double* g, double* m, double* v, int64_t
 void launch_adam_gated_table(double* p, const double* g, double* m, double* v, int64_t n, const AdamCoef& c,
                              const double* table, const int64_t* counter, const double* gate, hipStream_t stream);
 void launch_counter_advance(int64_t* counter, hipStream_t stream);
+// the table step over k <= ADAM_MULTI tensors in one launch (off: prefix sums of the sizes)
+constexpr int ADAM_MULTI = 8;
+struct AdamSet {
+  double* p[ADAM_MULTI];
+  const double* g[ADAM_MULTI];
+  double* m[ADAM_MULTI];
+  double* v[ADAM_MULTI];
+  int64_t off[ADAM_MULTI + 1];
+  int k;
+};
+void launch_adam_gated_table_multi(const AdamSet& set, const AdamCoef& c, const double* table, const int64_t* counter,
+                                   const double* gate, hipStream_t stream);
 
 // --- sem.hip ----------------------------------------------------------------
 // Parents (CSR over columns of W, ascending) and topological levels of a weighted DAG.

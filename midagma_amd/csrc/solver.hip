@@ -1511,6 +1511,32 @@ extern "C" int midagma_adam_step_table(double* p, const double* g, double* m, do
   });
 }
 
+extern "C" int midagma_adam_step_table_multi(int64_t k, double* const* p, const double* const* g, double* const* m,
+                                             double* const* v, const int64_t* n, const double* table,
+                                             const int64_t* counter, double w1, double beta2, double c2, double eps,
+                                             double wd, const double* gate, void* stream) {
+  if (k < 1 || k > ADAM_MULTI || !p || !g || !m || !v || !n || !table || !counter)
+    return fail(nullptr, MIDAGMA_E_ARG, "adam_step_table_multi: bad arguments");
+  AdamSet set{};
+  set.k = (int)k;
+  set.off[0] = 0;
+  for (int64_t q = 0; q < k; ++q) {
+    if (!p[q] || !g[q] || !m[q] || !v[q] || n[q] < 0)
+      return fail(nullptr, MIDAGMA_E_ARG, "adam_step_table_multi: bad tensor");
+    set.p[q] = p[q];
+    set.g[q] = g[q];
+    set.m[q] = m[q];
+    set.v[q] = v[q];
+    set.off[q + 1] = set.off[q] + n[q];
+  }
+  if (set.off[k] == 0) return MIDAGMA_OK;
+  return guarded(nullptr, [&] {
+    launch_adam_gated_table_multi(set, AdamCoef{0.0, w1, beta2, c2, 1.0, eps, wd}, table, counter, gate,
+                                  reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
 extern "C" int midagma_counter_advance(int64_t* counter, void* stream) {
   if (!counter) return fail(nullptr, MIDAGMA_E_ARG, "counter_advance: null counter");
   return guarded(nullptr, [&] {

@@ -408,13 +408,22 @@ class DagmaNonlinear:
             stream = torch.cuda.current_stream(dev).cuda_stream
             st = C.c_void_p(stream) if stream else None
             g_ptr = C.c_void_p((h_val if gate is None else gate).data_ptr())
-            for p, m, v in zip(params, exp_avg, exp_avg_sq):
-                g = p.grad.contiguous()
-                _lib.check(L.midagma_adam_step_table(C.c_void_p(p.data_ptr()), C.c_void_p(g.data_ptr()),
-                                                     C.c_void_p(m.data_ptr()), C.c_void_p(v.data_ptr()), p.numel(),
-                                                     C.c_void_p(table_d.data_ptr()),
-                                                     C.c_void_p(counter.data_ptr()), 1 - beta1, beta2, 1 - beta2,
-                                                     eps, wd, g_ptr, st), None, "adam_step_table")
+            grads = [p.grad.contiguous() for p in params]
+            if len(params) <= 8:  # every parameter tensor in one launch
+                k = len(params)
+                arr = lambda ts: (C.c_void_p * k)(*[C.c_void_p(t.data_ptr()) for t in ts])  # noqa: E731
+                _lib.check(L.midagma_adam_step_table_multi(
+                    k, arr(params), arr(grads), arr(exp_avg), arr(exp_avg_sq),
+                    (C.c_int64 * k)(*[p.numel() for p in params]), C.c_void_p(table_d.data_ptr()),
+                    C.c_void_p(counter.data_ptr()), 1 - beta1, beta2, 1 - beta2, eps, wd, g_ptr, st), None,
+                    "adam_step_table_multi")
+            else:
+                for p, g, m, v in zip(params, grads, exp_avg, exp_avg_sq):
+                    _lib.check(L.midagma_adam_step_table(C.c_void_p(p.data_ptr()), C.c_void_p(g.data_ptr()),
+                                                         C.c_void_p(m.data_ptr()), C.c_void_p(v.data_ptr()),
+                                                         p.numel(), C.c_void_p(table_d.data_ptr()),
+                                                         C.c_void_p(counter.data_ptr()), 1 - beta1, beta2,
+                                                         1 - beta2, eps, wd, g_ptr, st), None, "adam_step_table")
             _lib.check(L.midagma_counter_advance(C.c_void_p(counter.data_ptr()), st), None, "counter_advance")
             return h_val, obj
 
