@@ -206,8 +206,13 @@ int midagma_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, co
  * backward from *g: *gssq, gl1part[*], *gh.  All device pointers, on `stream`. */
 int64_t midagma_fc1_terms_parts(int64_t d);
 int midagma_fc1_terms(const double* W1, int64_t d, int64_t m1, double* A, double* l1part, void* stream);
-int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gl1part,
-                          double* dW1, void* stream);
+int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gscale,
+                          const double* gl1part, double* dW1, void* stream);
+/* h = -log|det(sI - A)| + d log s (DagmaMLP.h_func, nonlinear.py:68-86) into *h_dev and, when
+ * Mt_dev is given, (sI - A)^-T (d x d, ldm) -- its gradient -- in four launches (build, GJ,
+ * epilogue; the GJ on the 32-padded problem). */
+int midagma_logdet_h_dev(const double* A, int64_t d, int64_t lda, double s, double* h_dev, double* Mt_dev, int64_t ldm,
+                         void* stream);
 int midagma_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
                           double lambda1, double half_d, double inv_n, double* obj, void* stream);
 int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,

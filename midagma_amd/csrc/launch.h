@@ -136,8 +136,11 @@ void launch_mlp_tail_bwd(const double* Z, const double* w2, const double* R, con
 // (fc1_terms_parts(d) of them); backward dW1 = 2 W1 gA^T + gl1part sign(W1)
 int64_t fc1_terms_parts(int64_t d);
 void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1part, hipStream_t stream);
-void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gl1part, double* dW1,
-                          hipStream_t stream);
+void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gscale,
+                          const double* gl1part, double* dW1, hipStream_t stream);
+// Mt (d x d, ldm; nullable) from the D x D log-det workspace Ws and h = -sum(piv[0:d]) + dls
+void launch_logdet_post(const double* piv, int64_t d, double dls, double* h, const double* Ws, int64_t D, double* Mt,
+                        int64_t ldm, hipStream_t stream);
 // obj = mu (half_d log(inv_n ssq) + lambda1 sum(l1part)) + h and its backward
 void launch_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
                           double lambda1, double half_d, double inv_n, double* out, hipStream_t stream);

@@ -172,21 +172,47 @@ __global__ __launch_bounds__(NTHREADS) void fc1_terms_kernel(const double* __res
   if (threadIdx.x == 0) l1part[blockIdx.x] = red[0];
 }
 
-// dW1[j m1 + m, i] = 2 W1 gA[i, j] + gl1[wg(j, i)] sign(W1)
+// dW1[j m1 + m, i] = 2 W1 gA[i, j] + gl1[wg(j, i)] sign(W1);  gA = (*gscale) gA when gscale is
+// given (the log-det's backward, grad_out * (sI - A)^-T, folded in)
 __global__ __launch_bounds__(NTHREADS) void fc1_terms_bwd_kernel(const double* __restrict__ W1, int64_t d, int m1,
                                                                  const double* __restrict__ gA,
+                                                                 const double* __restrict__ gscale,
                                                                  const double* __restrict__ gl1,
                                                                  double* __restrict__ dW1) {
   const int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   if (t >= d * d) return;
   const int64_t j = t / d, i = t % d;
-  const double ga = gA[i * d + j], gl = gl1[blockIdx.x];
+  const double ga = gscale ? gscale[0] * gA[i * d + j] : gA[i * d + j], gl = gl1[blockIdx.x];
   for (int m = 0; m < m1; ++m) {
     const int64_t e = (j * m1 + m) * d + i;
     const double w = W1[e];
     const double sg = w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : 0.0);
     dW1[e] = ga * (2.0 * w) + gl * sg;
   }
+}
+
+// the log-det's epilogue in one launch: Mt (d x d, ldm) from the D x D workspace, and
+// workgroup 0: h = -(sum of the pivot logs) + d log s (the reference's h_func, nonlinear.py:85-86)
+__global__ __launch_bounds__(NTHREADS) void logdet_post_kernel(const double* __restrict__ piv, int64_t d, double dls,
+                                                               double* __restrict__ h,
+                                                               const double* __restrict__ Ws, int64_t D,
+                                                               double* __restrict__ Mt, int64_t ldm) {
+  const int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  if (Mt && t < d * d) {
+    const int64_t i = t / d, j = t % d;
+    Mt[i * ldm + j] = Ws[i * D + j];
+  }
+  if (blockIdx.x != 0) return;
+  __shared__ double red[NTHREADS];
+  double acc = 0.0;
+  for (int64_t k = threadIdx.x; k < d; k += NTHREADS) acc += piv[k];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = NTHREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) h[0] = -red[0] + dls;
 }
 
 // one workgroup: obj = mu (0.5 d log(1/n ssq) + lambda1 sum(l1part)) + h, the reference's
@@ -237,10 +263,18 @@ void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1
   HIP_TRY(hipGetLastError());
 }
 
-void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gl1part, double* dW1,
-                          hipStream_t stream) {
+void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gscale,
+                          const double* gl1part, double* dW1, hipStream_t stream) {
   hipLaunchKernelGGL(fc1_terms_bwd_kernel, dim3((unsigned)fc1_terms_parts(d)), dim3(NTHREADS), 0, stream, W1, d, m1,
-                     gA, gl1part, dW1);
+                     gA, gscale, gl1part, dW1);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_logdet_post(const double* piv, int64_t d, double dls, double* h, const double* Ws, int64_t D, double* Mt,
+                        int64_t ldm, hipStream_t stream) {
+  const int64_t blocks = std::max<int64_t>(1, (d * d + NTHREADS - 1) / NTHREADS);
+  hipLaunchKernelGGL(logdet_post_kernel, dim3((unsigned)blocks), dim3(NTHREADS), 0, stream, piv, d, dls, h, Ws, D, Mt,
+                     ldm);
   HIP_TRY(hipGetLastError());
 }
 

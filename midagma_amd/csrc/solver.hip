@@ -1324,6 +1324,38 @@ std::mutex g_ws_mu;
 std::vector<LogdetWorkspace*> g_ws;
 }  // namespace
 
+extern "C" int midagma_logdet_h_dev(const double* A, int64_t d, int64_t lda, double s, double* h_dev, double* Mt_dev,
+                                    int64_t ldm, void* stream) {
+  if (!A || !h_dev || d < 1 || lda < d || !(s > 0.0) || (Mt_dev && ldm < d))
+    return fail(nullptr, MIDAGMA_E_ARG, "logdet_h_dev: bad arguments");
+  return guarded(nullptr, [&] {
+    setup_attributes_once();
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    const int64_t D = (d + 31) / 32 * 32;  // the 32-block Gauss-Jordan's own granularity
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    LogdetWorkspace* ws = nullptr;
+    for (auto* w : g_ws)
+      if (w->device == dev && w->D == D) ws = w;
+    if (!ws) {
+      ws = new LogdetWorkspace();
+      ws->device = dev;
+      ws->D = D;
+      ws->A.alloc((size_t)D * D);
+      ws->P.alloc(64 * 64);
+      ws->R.alloc((size_t)64 * D);
+      ws->C.alloc((size_t)D * 64);
+      ws->piv.alloc(D);
+      g_ws.push_back(ws);
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    launch_build_at(A, lda, false, ws->A.p, D, d, s, nullptr, nullptr, st);
+    launch_gj_inverse(ws->A.p, D, D, GJWork{ws->P.p, ws->R.p, ws->C.p, ws->piv.p}, nullptr, st);
+    launch_logdet_post(ws->piv.p, d, (double)d * std::log(s), h_dev, ws->A.p, D, Mt_dev, ldm, st);
+    return MIDAGMA_OK;
+  });
+}
+
 extern "C" int midagma_logdet_inv_dev(const double* A, int64_t d, int64_t lda, double s_dom, double* logdet_dev,
                                       double* Mt_dev, int64_t ldm, void* stream) {
   if (!A || d < 1 || lda < d || (Mt_dev && ldm < d))
@@ -1456,12 +1488,12 @@ extern "C" int midagma_fc1_terms(const double* W1, int64_t d, int64_t m1, double
   });
 }
 
-extern "C" int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gl1part,
-                                     double* dW1, void* stream) {
+extern "C" int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gscale,
+                                     const double* gl1part, double* dW1, void* stream) {
   if (!W1 || !gA || !gl1part || !dW1 || d < 1 || m1 < 1)
     return fail(nullptr, MIDAGMA_E_ARG, "fc1_terms_bwd: bad arguments");
   return guarded(nullptr, [&] {
-    launch_fc1_terms_bwd(W1, d, (int)m1, gA, gl1part, dW1, reinterpret_cast<hipStream_t>(stream));
+    launch_fc1_terms_bwd(W1, d, (int)m1, gA, gscale, gl1part, dW1, reinterpret_cast<hipStream_t>(stream));
     return MIDAGMA_OK;
   });
 }

@@ -130,10 +130,56 @@ class _Fc1Terms(torch.autograd.Function):
         stream = torch.cuda.current_stream(W1.device).cuda_stream
         with torch.cuda.device(W1.device):
             _lib.check(_lib.lib().midagma_fc1_terms_bwd(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(gA.data_ptr()),
-                                                        C.c_void_p(gl1part.data_ptr()), C.c_void_p(dW1.data_ptr()),
+                                                        None, C.c_void_p(gl1part.data_ptr()),
+                                                        C.c_void_p(dW1.data_ptr()),
                                                         C.c_void_p(stream) if stream else None), None,
                        "fc1_terms_bwd")
         return dW1, None, None
+
+
+class _Fc1H(torch.autograd.Function):
+    """(h, |fc1| partial sums) from fc1's weight in one autograd node: the fc1 terms, the
+    log-det with its epilogue (h = -log|det(sI - A)| + d log s and (sI - A)^-T in one launch),
+    and a backward that folds h's gradient (grad_h * (sI - A)^-T) into the fc1 terms' one."""
+
+    @staticmethod
+    def forward(ctx, W1: torch.Tensor, d: int, m1: int, s: float):
+        W1 = W1.contiguous()
+        dev = W1.device
+        A = torch.empty((d, d), dtype=torch.float64, device=dev)
+        l1part = torch.empty(int(_lib.lib().midagma_fc1_terms_parts(d)), dtype=torch.float64, device=dev)
+        Mt = torch.empty((d, d), dtype=torch.float64, device=dev)
+        h = torch.empty((), dtype=torch.float64, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        st = C.c_void_p(stream) if stream else None
+        L = _lib.lib()
+        with torch.cuda.device(dev):
+            _lib.check(L.midagma_fc1_terms(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(A.data_ptr()),
+                                           C.c_void_p(l1part.data_ptr()), st), None, "fc1_terms")
+            _lib.check(L.midagma_logdet_h_dev(C.c_void_p(A.data_ptr()), d, d, float(s), C.c_void_p(h.data_ptr()),
+                                              C.c_void_p(Mt.data_ptr()), d, st), None, "logdet_h_dev")
+        ctx.save_for_backward(W1, Mt)
+        ctx.dims = (d, m1)
+        return h, l1part
+
+    @staticmethod
+    def backward(ctx, gh, gl1part):
+        W1, Mt = ctx.saved_tensors
+        d, m1 = ctx.dims
+        dev = W1.device
+        gh = torch.zeros((), dtype=torch.float64, device=dev) if gh is None else gh.contiguous()
+        if gl1part is None:
+            gl1part = torch.zeros(int(_lib.lib().midagma_fc1_terms_parts(d)), dtype=torch.float64, device=dev)
+        gl1part = gl1part.contiguous()
+        dW1 = torch.empty_like(W1)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().midagma_fc1_terms_bwd(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(Mt.data_ptr()),
+                                                        C.c_void_p(gh.data_ptr()), C.c_void_p(gl1part.data_ptr()),
+                                                        C.c_void_p(dW1.data_ptr()),
+                                                        C.c_void_p(stream) if stream else None), None,
+                       "fc1_terms_bwd")
+        return dW1, None, None, None
 
 
 class _Objective(torch.autograd.Function):
@@ -330,8 +376,7 @@ class DagmaNonlinear:
             n, d = self.X.shape
             m1 = m.dims[1]
             fc = m.fc2[0]
-            A, l1part = _Fc1Terms.apply(m.fc1.weight, d, m1)
-            h_val = logdet_h(A, s)
+            h_val, l1part = _Fc1H.apply(m.fc1.weight, d, m1, s)
             ssq = _MLPTail.apply(_Fc1Linear.apply(self.X, m.fc1.weight, m.fc1.bias), fc.weight, fc.bias, self.X, m1)
             return h_val, _Objective.apply(ssq, l1part, h_val, mu, lambda1, n, d)
         h_val = m.h_func(s)
