@@ -15,7 +15,7 @@
 namespace midagma {
 namespace {
 
-constexpr int TAIL_ROWS = 16;  // rows per workgroup of the backward (partials per row chunk)
+constexpr int TAIL_ROWS = 32;  // rows per workgroup of the backward (partials per row chunk)
 
 __device__ __forceinline__ double sigmoid(double z) { return 1.0 / (1.0 + exp(-z)); }
 
@@ -99,16 +99,27 @@ __global__ __launch_bounds__(NTHREADS) void mlp_tail_dw_kernel(const double* __r
                                                                double* __restrict__ db2) {
   const int64_t dm = d * m1;
   const int64_t c = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  // four independent chains (loads in flight), combined in a fixed order
+  const double* src;
+  int64_t stride;
+  double* dst;
   if (c < dm) {
-    double a = 0.0;
-    for (int64_t k = 0; k < nchunk; ++k) a += pw[k * dm + c];
-    dw2[c] = a;
+    src = pw + c, stride = dm, dst = dw2 + c;
   } else if (c < dm + d) {
-    const int64_t j = c - dm;
-    double a = 0.0;
-    for (int64_t k = 0; k < nchunk; ++k) a += pb[k * d + j];
-    db2[j] = a;
+    src = pb + (c - dm), stride = d, dst = db2 + (c - dm);
+  } else {
+    return;
   }
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int64_t k = 0;
+  for (; k + 4 <= nchunk; k += 4) {
+    a0 += src[k * stride];
+    a1 += src[(k + 1) * stride];
+    a2 += src[(k + 2) * stride];
+    a3 += src[(k + 3) * stride];
+  }
+  for (; k < nchunk; ++k) a0 += src[k * stride];
+  *dst = (a0 + a1) + (a2 + a3);
 }
 
 }  // namespace
