@@ -194,11 +194,13 @@ int midagma_adam_step_table_multi(int64_t k, double* const* p, const double* con
  * stream (replaces sigmoid -> LocallyConnected(d, m1, 1) -> squared residual sum in
  * nonlinear.py:99-104, 139-159 and their autograd backward; dagma/locally_connected.py:55-85).
  * scratch: midagma_mlp_tail_scratch(n, d, m1) doubles of device memory.
- * fwd: Z (n x d*m1 row-major) -> R = Xhat - X (n x d), *ssq = sum R^2 (device).
- * bwd: *g = d loss / d ssq (device) -> dZ (n x d*m1), dw2 (d x m1), db2 (d). */
+ * fwd: Z (n x d*m1 row-major, plus b1 per column when b1 is given) -> R = Xhat - X (n x d),
+ * *ssq = sum R^2 (device).
+ * bwd: *g = d loss / d ssq (device) -> dZ (n x d*m1), dw2 (d x m1), db2 (d) and, when db1 is
+ * given, db1 = column sums of dZ (d*m1). */
 int64_t midagma_mlp_tail_scratch(int64_t n, int64_t d, int64_t m1);
-int midagma_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n, int64_t d,
-                         int64_t m1, double* R, double* scratch, double* ssq, void* stream);
+int midagma_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, const double* b2, const double* X,
+                         int64_t n, int64_t d, int64_t m1, double* R, double* scratch, double* ssq, void* stream);
 /* The rest of the [d, m1, 1] DagmaMLP objective (nonlinear.py:68-86, 139-159, 198-206):
  * fc1_terms: A[i, j] = sum_m W1[j m1 + m, i]^2 (d x d, the log-det operand) and the |W1| partial
  * sums l1part (midagma_fc1_terms_parts(d) doubles); its backward dW1 = 2 W1 gA^T + gl1 sign(W1).
@@ -207,7 +209,7 @@ int midagma_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, co
 int64_t midagma_fc1_terms_parts(int64_t d);
 int midagma_fc1_terms(const double* W1, int64_t d, int64_t m1, double* A, double* l1part, void* stream);
 int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gscale,
-                          const double* gl1part, double* dW1, void* stream);
+                          const double* gl1part, const double* lin, int64_t nlin, double* dW1, void* stream);
 /* h = -log|det(sI - A)| + d log s (DagmaMLP.h_func, nonlinear.py:68-86) into *h_dev and, when
  * Mt_dev is given, (sI - A)^-T (d x d, ldm) -- its gradient -- in four launches (build, GJ,
  * epilogue; the GJ on the 32-padded problem). */
@@ -217,8 +219,9 @@ int midagma_mlp_objective(const double* ssq, const double* l1part, int64_t np, c
                           double lambda1, double half_d, double inv_n, double* obj, void* stream);
 int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,
                               double inv_n, double* gssq, double* gl1part, double* gh, void* stream);
-int midagma_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n, int64_t d,
-                         int64_t m1, double* dZ, double* dw2, double* db2, double* scratch, void* stream);
+int midagma_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R, const double* g,
+                         int64_t n, int64_t d, int64_t m1, double* dZ, double* dw2, double* db2, double* db1,
+                         double* scratch, void* stream);
 
 #ifdef __cplusplus
 }

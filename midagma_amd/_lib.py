@@ -94,12 +94,12 @@ EXPORTED = {
     "midagma_mlp_tail_scratch": (_i64, [_i64, _i64, _i64]),
     "midagma_fc1_terms_parts": (_i64, [_i64]),
     "midagma_fc1_terms": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
-    "midagma_fc1_terms_bwd": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "midagma_fc1_terms_bwd": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "midagma_logdet_h_dev": (_int, [_vp, _i64, _i64, _d, _vp, _vp, _i64, _vp]),
     "midagma_mlp_objective": (_int, [_vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp, _vp]),
     "midagma_mlp_objective_bwd": (_int, [_vp, _vp, _i64, _d, _d, _d, _d, _vp, _vp, _vp, _vp]),
-    "midagma_mlp_tail_fwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
-    "midagma_mlp_tail_bwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "midagma_mlp_tail_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "midagma_mlp_tail_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _lock = threading.Lock()

@@ -126,18 +126,22 @@ constexpr int64_t MLP_TAIL_MAX_DM = 7936;  // d * m1 the fused DagmaMLP tail sta
 // doubles of scratch the tail needs (both directions)
 int64_t mlp_tail_scratch(int64_t n, int64_t d, int64_t m1);
 // Z (n x d*m1) -> R = Xhat - X (n x d), *ssq = sum R^2
-void launch_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n, int64_t d,
-                         int m1, double* R, double* scratch, double* ssq, hipStream_t stream);
+// (b1 nullable: Z is then the pre-activation itself, else Z + b1 per column)
+void launch_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, const double* b2, const double* X,
+                         int64_t n, int64_t d, int m1, double* R, double* scratch, double* ssq, hipStream_t stream);
 // g (device scalar) = d loss / d ssq -> dZ (n x d*m1), dw2 (d x m1), db2 (d)
-void launch_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n, int64_t d,
-                         int m1, double* dZ, double* dw2, double* db2, double* scratch, hipStream_t stream);
+// (db1 nullable: also the column sums of dZ, the fc1 bias gradient)
+void launch_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R, const double* g,
+                         int64_t n, int64_t d, int m1, double* dZ, double* dw2, double* db2, double* db1,
+                         double* scratch, hipStream_t stream);
 
 // fc1 terms of the [d, m1, 1] DagmaMLP: A[i, j] = sum_m W1[j m1 + m, i]^2, |W1| partial sums
 // (fc1_terms_parts(d) of them); backward dW1 = 2 W1 gA^T + gl1part sign(W1)
 int64_t fc1_terms_parts(int64_t d);
 void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1part, hipStream_t stream);
+// (lin, nlin: nlin split-K chunks of another dW1 contribution to add; nullable / 0)
 void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gscale,
-                          const double* gl1part, double* dW1, hipStream_t stream);
+                          const double* gl1part, const double* lin, int nlin, double* dW1, hipStream_t stream);
 // Mt (d x d, ldm; nullable) from the D x D log-det workspace Ws and h = -sum(piv[0:d]) + dls
 void launch_logdet_post(const double* piv, int64_t d, double dls, double* h, const double* Ws, int64_t D, double* Mt,
                         int64_t ldm, hipStream_t stream);

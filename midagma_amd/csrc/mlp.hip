@@ -34,6 +34,7 @@ __device__ __forceinline__ double block_sum256(double v, double* red) {
 // workgroup per row: S w2 staged in LDS (coalesced over the row's d m1 columns), then thread
 // j < d sums its m1 terms: R[row, j] = Xhat - X, part[row] = sum_j R^2
 __global__ __launch_bounds__(NTHREADS) void mlp_tail_fwd_kernel(const double* __restrict__ Z,
+                                                                const double* __restrict__ b1,
                                                                 const double* __restrict__ w2,
                                                                 const double* __restrict__ b2,
                                                                 const double* __restrict__ X, int64_t d, int m1,
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(NTHREADS) void mlp_tail_fwd_kernel(const double* __
   extern __shared__ double sw[];  // d m1 products, then the reduction scratch
   const int64_t row = blockIdx.x, dm = d * m1;
   const double* z = Z + row * dm;
-  for (int64_t c = threadIdx.x; c < dm; c += NTHREADS) sw[c] = sigmoid(z[c]) * w2[c];
+  for (int64_t c = threadIdx.x; c < dm; c += NTHREADS) sw[c] = sigmoid(b1 ? z[c] + b1[c] : z[c]) * w2[c];
   __syncthreads();
   double r2 = 0.0;
   for (int64_t j = threadIdx.x; j < d; j += NTHREADS) {
@@ -68,35 +69,41 @@ __global__ __launch_bounds__(NTHREADS) void mlp_sum_kernel(const double* __restr
 // grid (column tiles of 256, row chunks of TAIL_ROWS): thread per column c = j m1 + m over
 // the chunk's rows: dZ, and the chunk's partials of dw2 (pw[chunk][c]) and db2 (pb[chunk][j])
 __global__ __launch_bounds__(NTHREADS) void mlp_tail_bwd_kernel(const double* __restrict__ Z,
+                                                                const double* __restrict__ b1,
                                                                 const double* __restrict__ w2,
                                                                 const double* __restrict__ R,
                                                                 const double* __restrict__ g, int64_t n, int64_t d,
                                                                 int m1, double* __restrict__ dZ,
-                                                                double* __restrict__ pw, double* __restrict__ pb) {
+                                                                double* __restrict__ pw, double* __restrict__ pb,
+                                                                double* __restrict__ pz) {
   const int64_t dm = d * m1;
   const int64_t c = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   if (c >= dm) return;
   const int64_t j = c / m1;
   const int m = (int)(c % m1);
-  const double w = w2[c], g2 = 2.0 * g[0];
+  const double w = w2[c], g2 = 2.0 * g[0], bias = b1 ? b1[c] : 0.0;
   const int64_t r0 = (int64_t)blockIdx.y * TAIL_ROWS, r1 = r0 + TAIL_ROWS < n ? r0 + TAIL_ROWS : n;
-  double aw = 0.0, ab = 0.0;
+  double aw = 0.0, ab = 0.0, az = 0.0;
   for (int64_t row = r0; row < r1; ++row) {
     const double dxh = g2 * R[row * d + j];
-    const double s = sigmoid(Z[row * dm + c]);
-    dZ[row * dm + c] = dxh * w * (s * (1.0 - s));
+    const double s = sigmoid(b1 ? Z[row * dm + c] + bias : Z[row * dm + c]);
+    const double dz = dxh * w * (s * (1.0 - s));
+    dZ[row * dm + c] = dz;
     aw += dxh * s;
     ab += dxh;
+    az += dz;
   }
   pw[(int64_t)blockIdx.y * dm + c] = aw;
   if (m == 0) pb[(int64_t)blockIdx.y * d + j] = ab;
+  if (pz) pz[(int64_t)blockIdx.y * dm + c] = az;
 }
 
 // dw2[c] = sum over chunks of pw[.][c], db2[j] likewise (fixed order)
 __global__ __launch_bounds__(NTHREADS) void mlp_tail_dw_kernel(const double* __restrict__ pw,
-                                                               const double* __restrict__ pb, int64_t nchunk,
+                                                               const double* __restrict__ pb,
+                                                               const double* __restrict__ pz, int64_t nchunk,
                                                                int64_t d, int m1, double* __restrict__ dw2,
-                                                               double* __restrict__ db2) {
+                                                               double* __restrict__ db2, double* __restrict__ db1) {
   const int64_t dm = d * m1;
   const int64_t c = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   // four independent chains (loads in flight), combined in a fixed order
@@ -107,6 +114,8 @@ __global__ __launch_bounds__(NTHREADS) void mlp_tail_dw_kernel(const double* __r
     src = pw + c, stride = dm, dst = dw2 + c;
   } else if (c < dm + d) {
     src = pb + (c - dm), stride = d, dst = db2 + (c - dm);
+  } else if (db1 && c < 2 * dm + d) {
+    src = pz + (c - dm - d), stride = dm, dst = db1 + (c - dm - d);
   } else {
     return;
   }
@@ -126,28 +135,31 @@ __global__ __launch_bounds__(NTHREADS) void mlp_tail_dw_kernel(const double* __r
 
 int64_t mlp_tail_scratch(int64_t n, int64_t d, int64_t m1) {
   const int64_t chunks = (n + TAIL_ROWS - 1) / TAIL_ROWS;
-  return std::max<int64_t>(n, chunks * (d * m1 + d));
+  return std::max<int64_t>(n, chunks * (2 * d * m1 + d));
 }
 
-void launch_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n, int64_t d,
-                         int m1, double* R, double* part, double* ssq, hipStream_t stream) {
+void launch_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, const double* b2, const double* X,
+                         int64_t n, int64_t d, int m1, double* R, double* part, double* ssq, hipStream_t stream) {
   if (d * m1 > MLP_TAIL_MAX_DM) throw std::invalid_argument("mlp tail: d * m1 above the LDS row stage");
   const size_t lds = (size_t)(d * m1 + NTHREADS) * sizeof(double);
-  hipLaunchKernelGGL(mlp_tail_fwd_kernel, dim3((unsigned)n), dim3(NTHREADS), lds, stream, Z, w2, b2, X, d, m1, R,
+  hipLaunchKernelGGL(mlp_tail_fwd_kernel, dim3((unsigned)n), dim3(NTHREADS), lds, stream, Z, b1, w2, b2, X, d, m1, R,
                      part);
   hipLaunchKernelGGL(mlp_sum_kernel, dim3(1), dim3(NTHREADS), 0, stream, part, n, ssq);
   HIP_TRY(hipGetLastError());
 }
 
-void launch_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n, int64_t d,
-                         int m1, double* dZ, double* dw2, double* db2, double* scratch, hipStream_t stream) {
+void launch_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R, const double* g,
+                         int64_t n, int64_t d, int m1, double* dZ, double* dw2, double* db2, double* db1,
+                         double* scratch, hipStream_t stream) {
   const int64_t dm = d * m1, chunks = (n + TAIL_ROWS - 1) / TAIL_ROWS;
   double* pw = scratch;
   double* pb = scratch + chunks * dm;
+  double* pz = db1 ? pb + chunks * d : nullptr;
   hipLaunchKernelGGL(mlp_tail_bwd_kernel, dim3((unsigned)((dm + NTHREADS - 1) / NTHREADS), (unsigned)chunks),
-                     dim3(NTHREADS), 0, stream, Z, w2, R, g, n, d, m1, dZ, pw, pb);
-  hipLaunchKernelGGL(mlp_tail_dw_kernel, dim3((unsigned)((dm + d + NTHREADS - 1) / NTHREADS)), dim3(NTHREADS), 0,
-                     stream, pw, pb, chunks, d, m1, dw2, db2);
+                     dim3(NTHREADS), 0, stream, Z, b1, w2, R, g, n, d, m1, dZ, pw, pb, pz);
+  const int64_t cols = dm + d + (db1 ? dm : 0);
+  hipLaunchKernelGGL(mlp_tail_dw_kernel, dim3((unsigned)((cols + NTHREADS - 1) / NTHREADS)), dim3(NTHREADS), 0,
+                     stream, pw, pb, pz, chunks, d, m1, dw2, db2, db1);
   HIP_TRY(hipGetLastError());
 }
 
@@ -189,16 +201,23 @@ __global__ __launch_bounds__(NTHREADS) void fc1_terms_bwd_kernel(const double* _
                                                                  const double* __restrict__ gA,
                                                                  const double* __restrict__ gscale,
                                                                  const double* __restrict__ gl1,
+                                                                 const double* __restrict__ lin, int nlin,
                                                                  double* __restrict__ dW1) {
   const int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   if (t >= d * d) return;
-  const int64_t j = t / d, i = t % d;
+  const int64_t j = t / d, i = t % d, dd = d * m1 * d;
   const double ga = gscale ? gscale[0] * gA[i * d + j] : gA[i * d + j], gl = gl1[blockIdx.x];
   for (int m = 0; m < m1; ++m) {
     const int64_t e = (j * m1 + m) * d + i;
     const double w = W1[e];
     const double sg = w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : 0.0);
-    dW1[e] = ga * (2.0 * w) + gl * sg;
+    double v = ga * (2.0 * w) + gl * sg;
+    if (nlin > 0) {  // + the linear layer's weight gradient, summed over its split-K chunks
+      double a = lin[e];
+      for (int c = 1; c < nlin; ++c) a += lin[c * dd + e];
+      v = a + v;
+    }
+    dW1[e] = v;
   }
 }
 
@@ -275,9 +294,9 @@ void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1
 }
 
 void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gscale,
-                          const double* gl1part, double* dW1, hipStream_t stream) {
+                          const double* gl1part, const double* lin, int nlin, double* dW1, hipStream_t stream) {
   hipLaunchKernelGGL(fc1_terms_bwd_kernel, dim3((unsigned)fc1_terms_parts(d)), dim3(NTHREADS), 0, stream, W1, d, m1,
-                     gA, gscale, gl1part, dW1);
+                     gA, gscale, gl1part, lin, nlin, dW1);
   HIP_TRY(hipGetLastError());
 }
 

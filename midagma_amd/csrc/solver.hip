@@ -1456,24 +1456,26 @@ extern "C" int64_t midagma_mlp_tail_scratch(int64_t n, int64_t d, int64_t m1) {
   return mlp_tail_scratch(n, d, m1);
 }
 
-extern "C" int midagma_mlp_tail_fwd(const double* Z, const double* w2, const double* b2, const double* X, int64_t n,
-                                    int64_t d, int64_t m1, double* R, double* scratch, double* ssq, void* stream) {
+extern "C" int midagma_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, const double* b2,
+                                    const double* X, int64_t n, int64_t d, int64_t m1, double* R, double* scratch,
+                                    double* ssq, void* stream) {
   if (!Z || !w2 || !b2 || !X || !R || !scratch || !ssq || n < 1 || d < 1 || m1 < 1 || d * m1 > MLP_TAIL_MAX_DM)
     return fail(nullptr, MIDAGMA_E_ARG, "mlp_tail_fwd: bad arguments");
   return guarded(nullptr, [&] {
-    launch_mlp_tail_fwd(Z, w2, b2, X, n, d, (int)m1, R, scratch, ssq, reinterpret_cast<hipStream_t>(stream));
+    launch_mlp_tail_fwd(Z, b1, w2, b2, X, n, d, (int)m1, R, scratch, ssq, reinterpret_cast<hipStream_t>(stream));
     return MIDAGMA_OK;
   });
 }
 
-extern "C" int midagma_mlp_tail_bwd(const double* Z, const double* w2, const double* R, const double* g, int64_t n,
-                                    int64_t d, int64_t m1, double* dZ, double* dw2, double* db2, double* scratch,
-                                    void* stream) {
+extern "C" int midagma_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R,
+                                    const double* g, int64_t n, int64_t d, int64_t m1, double* dZ, double* dw2,
+                                    double* db2, double* db1, double* scratch, void* stream) {
   if (!Z || !w2 || !R || !g || !dZ || !dw2 || !db2 || !scratch || n < 1 || d < 1 || m1 < 1 ||
       d * m1 > MLP_TAIL_MAX_DM)
     return fail(nullptr, MIDAGMA_E_ARG, "mlp_tail_bwd: bad arguments");
   return guarded(nullptr, [&] {
-    launch_mlp_tail_bwd(Z, w2, R, g, n, d, (int)m1, dZ, dw2, db2, scratch, reinterpret_cast<hipStream_t>(stream));
+    launch_mlp_tail_bwd(Z, b1, w2, R, g, n, d, (int)m1, dZ, dw2, db2, db1, scratch,
+                        reinterpret_cast<hipStream_t>(stream));
     return MIDAGMA_OK;
   });
 }
@@ -1489,11 +1491,13 @@ extern "C" int midagma_fc1_terms(const double* W1, int64_t d, int64_t m1, double
 }
 
 extern "C" int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gscale,
-                                     const double* gl1part, double* dW1, void* stream) {
-  if (!W1 || !gA || !gl1part || !dW1 || d < 1 || m1 < 1)
+                                     const double* gl1part, const double* lin, int64_t nlin, double* dW1,
+                                     void* stream) {
+  if (!W1 || !gA || !gl1part || !dW1 || d < 1 || m1 < 1 || nlin < 0 || (nlin > 0 && !lin))
     return fail(nullptr, MIDAGMA_E_ARG, "fc1_terms_bwd: bad arguments");
   return guarded(nullptr, [&] {
-    launch_fc1_terms_bwd(W1, d, (int)m1, gA, gscale, gl1part, dW1, reinterpret_cast<hipStream_t>(stream));
+    launch_fc1_terms_bwd(W1, d, (int)m1, gA, gscale, gl1part, lin, (int)nlin, dW1,
+                         reinterpret_cast<hipStream_t>(stream));
     return MIDAGMA_OK;
   });
 }

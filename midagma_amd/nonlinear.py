@@ -74,7 +74,7 @@ class _MLPTail(torch.autograd.Function):
         stream = torch.cuda.current_stream(X.device).cuda_stream
         with torch.cuda.device(X.device):
             _lib.check(_lib.lib().midagma_mlp_tail_fwd(
-                C.c_void_p(Z.data_ptr()), C.c_void_p(w2.data_ptr()), C.c_void_p(b2.data_ptr()),
+                C.c_void_p(Z.data_ptr()), None, C.c_void_p(w2.data_ptr()), C.c_void_p(b2.data_ptr()),
                 C.c_void_p(X.data_ptr()), n, d, m1, C.c_void_p(R.data_ptr()), C.c_void_p(part.data_ptr()),
                 C.c_void_p(ssq.data_ptr()), C.c_void_p(stream) if stream else None), None, "mlp_tail_fwd")
         ctx.save_for_backward(Z, w2, R, part)
@@ -93,153 +93,88 @@ class _MLPTail(torch.autograd.Function):
         stream = torch.cuda.current_stream(Z.device).cuda_stream
         with torch.cuda.device(Z.device):
             _lib.check(_lib.lib().midagma_mlp_tail_bwd(
-                C.c_void_p(Z.data_ptr()), C.c_void_p(w2.data_ptr()), C.c_void_p(R.data_ptr()),
+                C.c_void_p(Z.data_ptr()), None, C.c_void_p(w2.data_ptr()), C.c_void_p(R.data_ptr()),
                 C.c_void_p(g.data_ptr()), n, d, ctx.m1, C.c_void_p(dZ.data_ptr()), C.c_void_p(dw2.data_ptr()),
-                C.c_void_p(db2.data_ptr()), C.c_void_p(scratch.data_ptr()), C.c_void_p(stream) if stream else None),
+                C.c_void_p(db2.data_ptr()), None, C.c_void_p(scratch.data_ptr()),
+                C.c_void_p(stream) if stream else None),
                 None, "mlp_tail_bwd")
         return dZ, dw2, db2, None, None
 
 
-class _Fc1Terms(torch.autograd.Function):
-    """(A, l1 partial sums) of fc1's weight for a [d, m1, 1] DagmaMLP in one launch:
-    A[i, j] = sum_m W1[j m1 + m, i]^2 (nonlinear.py:83-84), |W1| summed per workgroup."""
+def _vp(t):
+    return C.c_void_p(t.data_ptr())
+
+
+class _MLPObjective(torch.autograd.Function):
+    """(h, mu * (0.5 d log(1/n sum (model(X) - X)^2) + lambda1 |fc1|_1) + h) of a [d, m1, 1]
+    DagmaMLP as one autograd node (nonlinear.py:68-86, 139-159, 198-204), so that no gradient is
+    accumulated or reduced by PyTorch: fc1's pre-activation X W1^T without the bias (the tail
+    kernels add b1), the fc1 terms and the log-det, the tail and the scalar objective forward;
+    backward the objective, the tail (dZ with the bias gradient's column sums, dw2, db2), the
+    weight gradient dZ^T X as a 4-way split-K batched GEMM whose chunks the fc1 terms' backward
+    sums together with the log-det and L1 gradients."""
 
     @staticmethod
-    def forward(ctx, W1: torch.Tensor, d: int, m1: int):
-        W1 = W1.contiguous()
-        A = torch.empty((d, d), dtype=torch.float64, device=W1.device)
-        l1part = torch.empty(int(_lib.lib().midagma_fc1_terms_parts(d)), dtype=torch.float64, device=W1.device)
-        stream = torch.cuda.current_stream(W1.device).cuda_stream
-        with torch.cuda.device(W1.device):
-            _lib.check(_lib.lib().midagma_fc1_terms(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(A.data_ptr()),
-                                                    C.c_void_p(l1part.data_ptr()),
-                                                    C.c_void_p(stream) if stream else None), None, "fc1_terms")
-        ctx.save_for_backward(W1)
-        ctx.dims = (d, m1)
-        return A, l1part
-
-    @staticmethod
-    def backward(ctx, gA, gl1part):
-        (W1,) = ctx.saved_tensors
-        d, m1 = ctx.dims
-        gA = torch.zeros((d, d), dtype=torch.float64, device=W1.device) if gA is None else gA.contiguous()
-        if gl1part is None:
-            gl1part = torch.zeros(int(_lib.lib().midagma_fc1_terms_parts(d)), dtype=torch.float64, device=W1.device)
-        gl1part = gl1part.contiguous()
-        dW1 = torch.empty_like(W1)
-        stream = torch.cuda.current_stream(W1.device).cuda_stream
-        with torch.cuda.device(W1.device):
-            _lib.check(_lib.lib().midagma_fc1_terms_bwd(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(gA.data_ptr()),
-                                                        None, C.c_void_p(gl1part.data_ptr()),
-                                                        C.c_void_p(dW1.data_ptr()),
-                                                        C.c_void_p(stream) if stream else None), None,
-                       "fc1_terms_bwd")
-        return dW1, None, None
-
-
-class _Fc1H(torch.autograd.Function):
-    """(h, |fc1| partial sums) from fc1's weight in one autograd node: the fc1 terms, the
-    log-det with its epilogue (h = -log|det(sI - A)| + d log s and (sI - A)^-T in one launch),
-    and a backward that folds h's gradient (grad_h * (sI - A)^-T) into the fc1 terms' one."""
-
-    @staticmethod
-    def forward(ctx, W1: torch.Tensor, d: int, m1: int, s: float):
-        W1 = W1.contiguous()
-        dev = W1.device
-        A = torch.empty((d, d), dtype=torch.float64, device=dev)
-        l1part = torch.empty(int(_lib.lib().midagma_fc1_terms_parts(d)), dtype=torch.float64, device=dev)
-        Mt = torch.empty((d, d), dtype=torch.float64, device=dev)
-        h = torch.empty((), dtype=torch.float64, device=dev)
+    def forward(ctx, X, W1, b1, w2, b2, d: int, m1: int, s: float, mu: float, lambda1: float):
+        L = _lib.lib()
+        dev = X.device
+        X, W1, b1, w2, b2 = X.contiguous(), W1.contiguous(), b1.contiguous(), w2.contiguous(), b2.contiguous()
+        n = X.shape[0]
         stream = torch.cuda.current_stream(dev).cuda_stream
         st = C.c_void_p(stream) if stream else None
+        f64 = dict(dtype=torch.float64, device=dev)
+        Z = X @ W1.t()
+        A = torch.empty((d, d), **f64)
+        l1part = torch.empty(int(L.midagma_fc1_terms_parts(d)), **f64)
+        Mt = torch.empty((d, d), **f64)
+        h = torch.empty((), **f64)
+        R = torch.empty_like(X)
+        scratch = torch.empty(int(L.midagma_mlp_tail_scratch(n, d, m1)), **f64)
+        ssq = torch.empty((), **f64)
+        obj = torch.empty((), **f64)
+        with torch.cuda.device(dev):
+            _lib.check(L.midagma_fc1_terms(_vp(W1), d, m1, _vp(A), _vp(l1part), st), None, "fc1_terms")
+            _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None, "logdet_h_dev")
+            _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
+                                              _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
+            _lib.check(L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(h), float(mu),
+                                               float(lambda1), 0.5 * d, 1 / n, _vp(obj), st), None, "mlp_objective")
+        ctx.save_for_backward(X, W1, b1, w2, Z, R, Mt, ssq, scratch)
+        ctx.consts = (n, d, m1, float(mu), float(lambda1), l1part.numel())
+        ctx.set_materialize_grads(False)  # h's own gradient stays None (no zero fill and add)
+        return h, obj
+
+    @staticmethod
+    def backward(ctx, gh_out, g):
+        X, W1, b1, w2, Z, R, Mt, ssq, scratch = ctx.saved_tensors
+        n, d, m1, mu, lambda1, np_ = ctx.consts
         L = _lib.lib()
-        with torch.cuda.device(dev):
-            _lib.check(L.midagma_fc1_terms(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(A.data_ptr()),
-                                           C.c_void_p(l1part.data_ptr()), st), None, "fc1_terms")
-            _lib.check(L.midagma_logdet_h_dev(C.c_void_p(A.data_ptr()), d, d, float(s), C.c_void_p(h.data_ptr()),
-                                              C.c_void_p(Mt.data_ptr()), d, st), None, "logdet_h_dev")
-        ctx.save_for_backward(W1, Mt)
-        ctx.dims = (d, m1)
-        return h, l1part
-
-    @staticmethod
-    def backward(ctx, gh, gl1part):
-        W1, Mt = ctx.saved_tensors
-        d, m1 = ctx.dims
-        dev = W1.device
-        gh = torch.zeros((), dtype=torch.float64, device=dev) if gh is None else gh.contiguous()
-        if gl1part is None:
-            gl1part = torch.zeros(int(_lib.lib().midagma_fc1_terms_parts(d)), dtype=torch.float64, device=dev)
-        gl1part = gl1part.contiguous()
-        dW1 = torch.empty_like(W1)
+        dev = X.device
         stream = torch.cuda.current_stream(dev).cuda_stream
+        st = C.c_void_p(stream) if stream else None
+        f64 = dict(dtype=torch.float64, device=dev)
+        g = torch.zeros((), **f64) if g is None else g.contiguous()
+        gssq, gl1, gh = torch.empty((), **f64), torch.empty(np_, **f64), torch.empty((), **f64)
+        dZ = torch.empty_like(Z)
+        dw2, db2, db1 = torch.empty_like(w2), torch.empty((d, 1), **f64), torch.empty(d * m1, **f64)
+        dW1 = torch.empty_like(W1)
         with torch.cuda.device(dev):
-            _lib.check(_lib.lib().midagma_fc1_terms_bwd(C.c_void_p(W1.data_ptr()), d, m1, C.c_void_p(Mt.data_ptr()),
-                                                        C.c_void_p(gh.data_ptr()), C.c_void_p(gl1part.data_ptr()),
-                                                        C.c_void_p(dW1.data_ptr()),
-                                                        C.c_void_p(stream) if stream else None), None,
-                       "fc1_terms_bwd")
-        return dW1, None, None, None
-
-
-class _Objective(torch.autograd.Function):
-    """mu * (0.5 d log(1/n ssq) + lambda1 * sum(l1part)) + h in one launch, and its backward in
-    one (nonlinear.py:158, 203-204): replaces a dozen scalar PyTorch kernels per direction."""
-
-    @staticmethod
-    def forward(ctx, ssq, l1part, h, mu: float, lambda1: float, n: int, d: int):
-        obj = torch.empty((), dtype=torch.float64, device=ssq.device)
-        half_d, inv_n = 0.5 * d, 1 / n
-        stream = torch.cuda.current_stream(ssq.device).cuda_stream
-        h = h.contiguous()
-        with torch.cuda.device(ssq.device):
-            _lib.check(_lib.lib().midagma_mlp_objective(
-                C.c_void_p(ssq.data_ptr()), C.c_void_p(l1part.data_ptr()), l1part.numel(), C.c_void_p(h.data_ptr()),
-                float(mu), float(lambda1), half_d, inv_n, C.c_void_p(obj.data_ptr()),
-                C.c_void_p(stream) if stream else None), None, "mlp_objective")
-        ctx.save_for_backward(ssq)
-        ctx.consts = (float(mu), float(lambda1), half_d, inv_n, l1part.numel())
-        return obj
-
-    @staticmethod
-    def backward(ctx, g):
-        (ssq,) = ctx.saved_tensors
-        mu, lambda1, half_d, inv_n, np_ = ctx.consts
-        g = g.contiguous()
-        gssq = torch.empty((), dtype=torch.float64, device=ssq.device)
-        gl1 = torch.empty(np_, dtype=torch.float64, device=ssq.device)
-        gh = torch.empty((), dtype=torch.float64, device=ssq.device)
-        stream = torch.cuda.current_stream(ssq.device).cuda_stream
-        with torch.cuda.device(ssq.device):
-            _lib.check(_lib.lib().midagma_mlp_objective_bwd(
-                C.c_void_p(g.data_ptr()), C.c_void_p(ssq.data_ptr()), np_, mu, lambda1, half_d, inv_n,
-                C.c_void_p(gssq.data_ptr()), C.c_void_p(gl1.data_ptr()), C.c_void_p(gh.data_ptr()),
-                C.c_void_p(stream) if stream else None), None, "mlp_objective_bwd")
-        return gssq, gl1, gh, None, None, None, None
-
-
-class _Fc1Linear(torch.autograd.Function):
-    """fc1 (nn.Linear) whose weight gradient dZ^T X runs as a 4-way split-K batched GEMM plus a
-    fixed-order sum: the plain 2000 x 200 x 1000 product at config 5 has only 64 output tiles
-    (60 us on MI355X), the split 27 us (tools/blas_probe.py)."""
-
-    @staticmethod
-    def forward(ctx, X: torch.Tensor, W: torch.Tensor, b: torch.Tensor):
-        ctx.save_for_backward(X, W)
-        return torch.nn.functional.linear(X, W, b)
-
-    @staticmethod
-    def backward(ctx, dZ):
-        X, W = ctx.saved_tensors
-        n = X.shape[0]
-        dZ = dZ.contiguous()
-        if n % 4 == 0 and n >= 64:
-            r = n // 4
-            dW = torch.bmm(dZ.view(4, r, -1).transpose(1, 2), X.contiguous().view(4, r, -1)).sum(0)
-        else:
-            dW = dZ.t() @ X
-        dX = dZ @ W if ctx.needs_input_grad[0] else None
-        return dX, dW, dZ.sum(0)
+            _lib.check(L.midagma_mlp_objective_bwd(_vp(g), _vp(ssq), np_, mu, lambda1, 0.5 * d, 1 / n, _vp(gssq),
+                                                   _vp(gl1), _vp(gh), st), None, "mlp_objective_bwd")
+            if gh_out is not None:  # h is also an output (the Adam gate): its own gradient adds in
+                gh = gh + gh_out
+            _lib.check(L.midagma_mlp_tail_bwd(_vp(Z), _vp(b1), _vp(w2), _vp(R), _vp(gssq), n, d, m1, _vp(dZ),
+                                              _vp(dw2), _vp(db2), _vp(db1), _vp(scratch), st), None, "mlp_tail_bwd")
+            if n % 4 == 0 and n >= 64:
+                r = n // 4
+                lin = torch.bmm(dZ.view(4, r, -1).transpose(1, 2), X.view(4, r, -1))  # (4, d m1, d)
+                nlin = 4
+            else:
+                lin = (dZ.t() @ X).contiguous()
+                nlin = 1
+            _lib.check(L.midagma_fc1_terms_bwd(_vp(W1), d, m1, _vp(Mt), _vp(gh), _vp(gl1), _vp(lin), nlin,
+                                               _vp(dW1), st), None, "fc1_terms_bwd")
+        return None, dW1, db1, dw2, db2, None, None, None, None, None
 
 
 def logdet_h(A: torch.Tensor, s: float = 1.0) -> torch.Tensor:
@@ -376,9 +311,7 @@ class DagmaNonlinear:
             n, d = self.X.shape
             m1 = m.dims[1]
             fc = m.fc2[0]
-            h_val, l1part = _Fc1H.apply(m.fc1.weight, d, m1, s)
-            ssq = _MLPTail.apply(_Fc1Linear.apply(self.X, m.fc1.weight, m.fc1.bias), fc.weight, fc.bias, self.X, m1)
-            return h_val, _Objective.apply(ssq, l1part, h_val, mu, lambda1, n, d)
+            return _MLPObjective.apply(self.X, m.fc1.weight, m.fc1.bias, fc.weight, fc.bias, d, m1, s, mu, lambda1)
         h_val = m.h_func(s)
         return h_val, mu * (self._score() + lambda1 * m.fc1_l1_reg()) + h_val
 
