@@ -252,7 +252,8 @@ def bench_mlp(args, device, with_cpu):
     dt = time.perf_counter() - t0
     out = dict(value=K / dt, unit="steps/s", ms_per_step=dt / K * 1e3, steps=K, verified=bool(ok),
                workload="config5: DagmaNonlinear.minimize, DagmaMLP dims [200, 10, 1], n=1000, 1 GPU "
-                        "(PyTorch-ROCm model + Adam, HIP log-det h_func)")
+                        "(the reference's loop; objective as fused HIP kernels: fc1 terms, log-det, MLP tail, "
+                        "scalar objective, multi-tensor Adam; fc1 GEMMs on rocBLAS; one step replayed as a hipGraph)")
     if with_cpu:
         best = None
         ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
