@@ -96,6 +96,8 @@ if __name__ == "__main__":
         cov_case(1000, 2000, 10, 2000)
     if which == "fit":
         fit_case(1000, 10000)
+    if which == "fit20":
+        fit_case(20, 1000)
     if which == "d2000":
         cov_case(2000, 4000, 5, 100)
     if which in ("all", "d5000"):
