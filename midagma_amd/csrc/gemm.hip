@@ -326,7 +326,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int per_slice = tiles_m * tiles_n;
   const int z = t / per_slice, rem = t % per_slice;
-  int bm = rem / tiles_n, bn = rem % tiles_n;
+  int bm, bn;
+  if (tiles_n > 8) {
+    // grouped order: the 64 consecutive tiles one XCD holds resident (32 CUs x 2) form an
+    // 8 x 8 block, so its L2 serves each A row panel and B column panel to 8 tiles (row-major
+    // order put 40 different B panels in flight per XCD at d = 5000)
+    const int gsz = 8 * tiles_n, g = rem / gsz, w_ = rem - g * gsz;
+    const int fm = g * 8, rows = tiles_m - fm < 8 ? tiles_m - fm : 8;
+    bm = fm + w_ % rows;
+    bn = w_ / rows;
+  } else {
+    bm = rem / tiles_n;
+    bn = rem % tiles_n;
+  }
   if (EPI == EPI_SUB_BAND) {
     // trailing update of the blocked inverse: the tile grid skips the pivot band
     // [m_valid, m_valid + n_valid) (in 128-tiles) in both rows and columns
