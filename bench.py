@@ -62,7 +62,24 @@ def parse():
     p.add_argument("--large-d", type=int, default=5000)
     p.add_argument("--large-n", type=int, default=50_000)
     p.add_argument("--large-steps", type=int, default=100)
+    p.add_argument("--no-logistic", action="store_true", help="skip the logistic data-mode leg (SURVEY 8f-1)")
+    p.add_argument("--logistic-steps", type=int, default=10)
     return p.parse_args()
+
+
+def relaunch_ranks(args):
+    """`python bench.py --gpus N` (N > 1) outside a launcher: start one rank per GPU under
+    torch.distributed.run as a child process (no exec; nothing here has touched the GPU),
+    relay its output (rank 0 prints the JSON line) and exit with its return code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching:", " ".join(cmd))
+    sys.exit(subprocess.run(cmd).returncode)
 
 
 def setup_dist(args):
@@ -87,7 +104,7 @@ def setup_dist(args):
     return world, rank, local
 
 
-def make_shard(d, n, world, rank, seed, device):
+def make_shard(d, n, world, rank, seed, device, sem="gauss"):
     """This rank's rows of an ER(s0=d) linear-Gaussian SEM, generated on the GPU by the
     library's SEM generator (csrc/sem.hip, counter-based noise: the shard is exactly the
     rank's rows of the unsharded X).  Returns (X, n_k, generation seconds)."""
@@ -102,11 +119,11 @@ def make_shard(d, n, world, rank, seed, device):
     dev_index = device.index if hasattr(device, "index") else device
     # one tiny call first: the process's first launch of the library's kernels loads its code
     # object, a one-time cost that is not the generator's
-    simulate_linear_sem_gpu(W_true, n, "gauss", seed=seed * 1000003 + 17, device=dev_index, row0=row0,
+    simulate_linear_sem_gpu(W_true, n, sem, seed=seed * 1000003 + 17, device=dev_index, row0=row0,
                             n_rows=min(n_k, 256))
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    X = simulate_linear_sem_gpu(W_true, n, "gauss", seed=seed * 1000003 + 17, device=device.index
+    X = simulate_linear_sem_gpu(W_true, n, sem, seed=seed * 1000003 + 17, device=device.index
                                 if hasattr(device, "index") else device, row0=row0, n_rows=n_k)
     torch.cuda.synchronize(device)
     return X, n_k, time.perf_counter() - t0
@@ -256,28 +273,69 @@ def bench_mlp(args, device, with_cpu):
                         "scalar objective, multi-tensor Adam; fc1 GEMMs on rocBLAS; one step replayed as a hipGraph)")
     if with_cpu:
         best = None
-        ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-        share = min(ncpu, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+        phys = host_cpus()["physical_cores"]
+        sweep = {}
         with tempfile.TemporaryDirectory() as td:
             path = os.path.join(td, "mlp.npz")
             np.savez(path, X=X, **params)
-            for th in sorted({1, 4, 8, share} & set(range(1, share + 1))):
+            for th in thread_sweep(phys):
                 env = dict(os.environ, OMP_NUM_THREADS=str(th), HIP_VISIBLE_DEVICES="")
                 try:
                     r = subprocess.run([sys.executable, "-c", _MLP_CPU_CHILD, REPO, str(th), str(d), str(n), path],
                                        capture_output=True, text=True, timeout=600, env=env)
                     t = json.loads(r.stdout.strip().splitlines()[-1])["t"]
                     log(f"cpu oracle MLP d={d}: {1 / t:.1f} steps/s at {th} threads")
+                    sweep[str(th)] = 1.0 / t
                     if best is None or t < best[0]:
                         best = (t, th)
                 except Exception as e:  # noqa: BLE001
                     log(f"cpu oracle MLP at {th} threads failed: {e!r}")
         if best is not None:
             out["cpu_baseline"] = dict(value=1.0 / best[0], unit="steps/s", cores=best[1], kind="port",
+                                       physical_cores=phys, sweep=sweep,
                                        sample="oracle DagmaNonlinear.minimize (torch CPU, slogdet h_func as "
-                                              "nonlinear.py:84), 20 steps per thread count, best shown")
+                                              f"nonlinear.py:84), 20 steps per thread count, threads "
+                                              f"{thread_sweep(phys)}, best shown")
             out["vs_cpu"] = out["value"] * best[0]
     return out
+
+
+def bench_logistic(args, device, n, steps):
+    """the logistic loss in data mode at full speed (linear.py:245-246):
+    per step expit(X W) in the epilogue of the X W GEMM (EPI_SIGMOID), then X^T S, on 1 GPU.
+    X: a logistic SEM (Bernoulli rows) from the GPU generator; cov = X^T X / n from the device
+    Gram (linear.py:428; logistic does not centre X)."""
+    import torch
+    from midagma_amd.solver import HipSolver
+    d = args.d
+    dev = torch.device("cuda", device)
+    X, n_k, _ = make_shard(d, n, 1, 0, args.seed + 7, dev, sem="logistic")
+    s = HipSolver(d, "logistic", "data", device=device)
+    s.set_data(X, n_global=n)
+    del X
+    torch.cuda.empty_cache()
+    s.data_gram()
+    s.cov_from_zbuf(float(n))
+    s.begin(np.zeros((d, d)), 1.0, steps + 64, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
+    s.run_slots(3)
+    s.sync()
+    t0 = time.perf_counter()
+    s.run_slots(steps)
+    s.sync()
+    t1 = time.perf_counter()
+    r = s.poll()
+    prof = s.profile_parts(3)
+    s.close()
+    flops = 2.0 * n * d * d
+    t_sig = prof["gemm_xw"] * 1e-3
+    return dict(value=steps / (t1 - t0), unit="steps/s", ms_per_step=(t1 - t0) / steps * 1e3, steps=steps,
+                verified=(r.status == 0 and r.iters == steps + 3),
+                workload=f"logistic: d={d}, n={n}, data mode (X W GEMM with the sigmoid epilogue, X^T S), 1 GPU",
+                kernel_ms={k: round(v, 4) for k, v in prof.items()},
+                sigmoid_gemm={"kernel": "gemm_pipe_kernel<1, 0, 1> (EPI_SIGMOID)", "ms": prof["gemm_xw"],
+                              "achieved_tflops": flops / t_sig / 1e12 if t_sig > 0 else None,
+                              "frac_fp64_peak": flops / t_sig / 1e12 / FP64_MFMA_PEAK_TF if t_sig > 0 else None,
+                              "algorithmic": f"2*n*d^2 = {flops:.3e} flop + n*d sigmoids"})
 
 
 def bench_cov_large(args, device):
@@ -321,57 +379,105 @@ import numpy as np
 sys.path.insert(0, sys.argv[1])
 from threadpoolctl import threadpool_limits
 from oracle.dagma_oracle import LinearOracle
-mode, th, d = sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
-rng = np.random.default_rng(0)
+mode, d, extra = sys.argv[2], int(sys.argv[3]), sys.argv[4]
+threads = [int(t) for t in sys.argv[5].split(",")]
+steps = int(sys.argv[6])
+warm = sys.argv[7] == "1"
 
 
-def per_step(o, a, b):
-    # difference of two runs cancels the fixed cost of the final checkpoint (linear.py:279)
-    t0 = time.perf_counter()
-    o.minimize(np.zeros((d, d)), 1.0, a, 1.0, 3e-4, tol=-1.0)
-    t1 = time.perf_counter()
-    o.minimize(np.zeros((d, d)), 1.0, b, 1.0, 3e-4, tol=-1.0)
-    t2 = time.perf_counter()
-    return max(1e-9, (t2 - t1) - (t1 - t0)) / (b - a)
+def gauss(n, d, seed):
+    # N(0,1) n x d in parallel chunks (independent streams; numpy releases the GIL)
+    from concurrent.futures import ThreadPoolExecutor
+    X = np.empty((n, d))
+    ch = max(1, -(-n // 32))
+    def fill(k):
+        np.random.default_rng([seed, k]).standard_normal(out=X[k * ch:(k + 1) * ch])
+    with ThreadPoolExecutor(16) as ex:
+        list(ex.map(fill, range(-(-n // ch))))
+    return X
 
 
-with threadpool_limits(limits=th):
-    if mode == "cov":
-        cov = np.load(sys.argv[5])
-        o = LinearOracle("l2")
-        o.cov, o.d, o.n, o.eye, o.lambda1, o.checkpoint = cov, d, 10000, np.eye(d), 0.03, 10 ** 9
-        o.inc = o.exc = None
-        o.X = None
-        if d >= 3000:  # config 3: a few seconds per step -- 1 and 2 steps (3 CPU steps)
-            print(json.dumps({"t": per_step(o, 1, 2)}))
-        else:
-            print(json.dumps({"t": per_step(o, 1, 3) if th == 1 else per_step(o, 2, 5)}))
-    else:
-        ts = []
-        for n in (int(sys.argv[5]), 4 * int(sys.argv[5])):
-            X = rng.standard_normal((n, d))
-            o = LinearOracle("l2", score_mode="data")
-            o.X, o.d, o.n, o.eye, o.lambda1, o.checkpoint = X, d, n, np.eye(d), 0.03, 10 ** 9
-            o.cov = None
-            o.inc = o.exc = None
-            ts.append((n, float(np.median([per_step(o, 1, 3) for _ in range(3)]))))
-            del X, o
-        print(json.dumps({"t": ts}))
+if mode == "cov":                       # the reference algorithm: cov precomputed once
+    o = LinearOracle("l2")
+    o.cov, o.X, o.n = np.load(extra), None, 10000
+elif mode == "data":                    # the workload's math: -(mu/n) X^T (X (I - W)) per step
+    n = int(extra)
+    o = LinearOracle("l2", score_mode="data")
+    o.X, o.n, o.cov = gauss(n, d, 0), n, None
+else:                                   # logistic: (mu/n) X^T expit(X W) - mu cov per step
+    n = int(extra)
+    o = LinearOracle("logistic")
+    X = (gauss(n, d, 1) > 0).astype(np.float64)
+    o.X, o.n, o.cov = X, n, X.T @ X / float(n)
+o.d, o.eye, o.lambda1, o.checkpoint, o.inc, o.exc = d, np.eye(d), 0.03, 10 ** 9, None, None
+# the objective is evaluated once per `checkpoint` (1000) steps in a fit; the timed window is
+# the Adam step itself, so the final-iteration objective is not evaluated here
+o._objective = lambda W, mu, s: (0.0, 0.0, 0.0)
+out = {}
+for th in threads:
+    with threadpool_limits(limits=th):
+        if warm:
+            o.minimize(np.zeros((d, d)), 1.0, 1, 1.0, 3e-4, tol=-1.0)   # warm: pools, pages
+        t0 = time.perf_counter()
+        W, tr = o.minimize(np.zeros((d, d)), 1.0, steps, 1.0, 3e-4, tol=-1.0)
+        out[th] = (time.perf_counter() - t0) / steps
+        assert tr.iters == steps
+    print(json.dumps({"partial": out}), flush=True)
+print(json.dumps({"t": out}), flush=True)
 """
 
 
-def _cpu_runs(mode, d, extra, cands, env_base):
-    import subprocess
-    out = {}
-    for th in cands:
-        env = dict(env_base, OMP_NUM_THREADS=str(th), OPENBLAS_NUM_THREADS=str(th), HIP_VISIBLE_DEVICES="")
+def host_cpus():
+    """Host CPU facts for the baseline's `cores` statement: logical CPUs, physical cores
+    (unique (package, core) pairs from sysfs), this process's affinity and cgroup quota."""
+    import glob
+    logical = os.cpu_count() or 1
+    pairs = set()
+    for c in glob.glob("/sys/devices/system/cpu/cpu[0-9]*/topology"):
         try:
-            r = subprocess.run([sys.executable, "-c", _CPU_CHILD, REPO, mode, str(th), str(d), str(extra)],
-                               capture_output=True, text=True, timeout=600, env=env)
-            out[th] = json.loads(r.stdout.strip().splitlines()[-1])["t"]
-        except Exception as e:  # noqa: BLE001
-            log(f"cpu oracle ({mode}) at {th} threads failed: {e!r}")
-    return out
+            pairs.add((open(c + "/physical_package_id").read().strip(), open(c + "/core_id").read().strip()))
+        except OSError:
+            pass
+    physical = len(pairs) or logical
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else logical
+    return {"logical_cpus": logical, "physical_cores": physical, "affinity_cpus": aff, "cgroup_cpu_quota": quota}
+
+
+def thread_sweep(phys, base=(1, 4, 8, 16)):
+    """BASELINE.md's plan: threads in {1, 4, 8, 16, physical/2, physical}."""
+    return sorted({t for t in base} | {max(1, phys // 2), phys})
+
+
+def _cpu_runs(mode, d, extra, threads, steps, timeout=900, warm=True):
+    """One child process (no GPU) times `steps` oracle Adam steps per thread count; all three
+    BLAS/OpenMP pools pinned by threadpoolctl.  Returns {threads: seconds per step}."""
+    import subprocess
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS=str(max(threads)),
+               OPENBLAS_NUM_THREADS=str(max(threads)))
+    try:
+        r = subprocess.run([sys.executable, "-c", _CPU_CHILD, REPO, mode, str(d), str(extra),
+                            ",".join(str(t) for t in threads), str(steps), "1" if warm else "0"],
+                           capture_output=True, text=True, timeout=timeout, env=env)
+        lines = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
+        if r.returncode != 0:
+            log(f"cpu oracle ({mode}) exited {r.returncode}: {r.stderr[-400:]}")
+        got = lines[-1].get("t") or lines[-1].get("partial") if lines else {}
+        return {int(k): float(v) for k, v in (got or {}).items()}
+    except subprocess.TimeoutExpired as e:
+        lines = [json.loads(x) for x in (e.stdout or b"").decode(errors="ignore").splitlines() if x.startswith("{")]
+        log(f"cpu oracle ({mode}) timed out after {timeout}s")
+        return {int(k): float(v) for k, v in (lines[-1].get("partial", {}) if lines else {}).items()}
+
+
+def _best(runs, unit_per_step=1.0):
+    th = min(runs, key=runs.get)
+    return th, unit_per_step / runs[th]
 
 
 def bench_fit(args, device):
@@ -393,49 +499,46 @@ def bench_fit(args, device):
 
 def cpu_baseline(args, cov):
     """CPU oracle (numpy/scipy restatement of the reference, bit-identical at 1 thread) on the
-    host cores, each thread count in an isolated child process (no GPU):
-      * 'port' of THIS workload (data mode): per-step time (median of 3) at n_s and 4 n_s rows,
-        extrapolated linearly in n to the workload's n;
-      * the reference algorithm (cov precomputed, O(d^3) per step, n-independent)."""
+    host cores, in child processes with no GPU:
+      * 'port' of THIS workload (data mode, n = args.n rows, measured at that n);
+      * the reference algorithm (cov precomputed, O(d^3) per step, n-independent).
+    Threads swept over {1, 4, 8, 16, physical/2, physical}; the n=1e6 data-mode
+    step (two 2-TFLOP host GEMMs) is timed at the counts that can win, {8, 16, physical/2,
+    physical}: 1 and 4 threads would take minutes per step."""
     import tempfile
     d = cov.shape[0]
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    share = min(ncpu, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
-    env = dict(os.environ)
-    res = {}
+    hc = host_cpus()
+    phys = hc["physical_cores"]
+    res = {"host": hc}
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "cov.npy")
         np.save(path, cov)
-        cands = sorted({1, 4, 8, share} & set(range(1, share + 1)))
-        ref = _cpu_runs("cov", d, path, cands, env)
-    for th, t in ref.items():
+        sweep = thread_sweep(phys)
+        ref = _cpu_runs("cov", d, path, sweep, steps=20)
+    for th, t in sorted(ref.items()):
         log(f"cpu reference algorithm d={d}: {1 / t:.2f} steps/s at {th} threads")
     if ref:
-        th = min(ref, key=ref.get)
-        res["reference_algorithm"] = dict(value=1.0 / ref[th], unit="steps/s", cores=th, kind="port",
-                                          sample=f"oracle cov-mode Adam steps at d={d} (linear.py:244 with cov "
-                                                 f"precomputed once, as fit() does); threads {cands}, best shown")
+        th, v = _best(ref)
+        res["reference_algorithm"] = dict(
+            value=v, unit="steps/s", cores=th, kind="port", physical_cores=phys,
+            sweep={str(k): 1.0 / t for k, t in sorted(ref.items())},
+            sample=f"oracle cov-mode Adam steps at d={d} (linear.py:244 with cov precomputed once, as fit() "
+                   f"does), 20 steps per thread count, threads {sorted(ref)} (host: {phys} physical cores, "
+                   f"{hc['logical_cpus']} logical, cgroup quota {hc['cgroup_cpu_quota']}), best shown")
     if args.workload == "data":
-        n_s = 25_000
-        dat = _cpu_runs("data", d, n_s, sorted({8, share}), env)
-        best = None
-        for th, pts in dat.items():
-            (n1, t1), (n2, t2) = pts
-            slope = (t2 - t1) / (n2 - n1)
-            # linear in n (the two n x d x d GEMMs) plus the n-independent inverse; a noisy host
-            # can invert the two points, then the larger one is scaled proportionally (an upper
-            # bound on the CPU time, i.e. a conservative GPU/CPU ratio)
-            t_full = t1 + slope * (args.n - n1) if slope > 0 else t2 * args.n / n2
-            log(f"cpu data-mode port d={d}: {t1:.3f}s@n={n1}, {t2:.3f}s@n={n2} -> {t_full:.2f}s/step at n={args.n} "
-                f"({th} threads)")
-            if best is None or t_full < best[0]:
-                best = (t_full, th, pts)
-        if best is not None:
-            res["workload"] = dict(value=1.0 / best[0], unit="steps/s", cores=best[1], kind="port",
-                                   sample=f"oracle data-mode Adam step (G = -(mu/n) X^T (X (I-W)), the workload's "
-                                          f"math) timed at n={best[2][0][0]} and {best[2][1][0]} rows (median of 3), d={d}, "
-                                          f"linear fit in n extrapolated to n={args.n}; threads "
-                                          f"{sorted({8, share})} of {ncpu} host CPUs, best shown")
+        cands = sorted({8, 16, max(1, phys // 2), phys})
+        dat = _cpu_runs("data", d, args.n, cands, steps=2, timeout=1200, warm=False)
+        for th, t in sorted(dat.items()):
+            log(f"cpu data-mode port d={d} n={args.n}: {t:.2f} s/step at {th} threads")
+        if dat:
+            th, v = _best(dat)
+            res["workload"] = dict(
+                value=v, unit="steps/s", cores=th, kind="port", physical_cores=phys,
+                sweep={str(k): 1.0 / t for k, t in sorted(dat.items())},
+                sample=f"oracle data-mode Adam step (G = -(mu/n) X^T (X (I-W)), the workload's math) measured "
+                       f"at n={args.n}, d={d}: 2 steps per thread count, threads "
+                       f"{sorted(dat)} (1 and 4 not run: minutes per step); host {phys} physical cores, "
+                       f"{hc['logical_cpus']} logical, cgroup quota {hc['cgroup_cpu_quota']}; best shown")
     return res
 
 
@@ -471,6 +574,8 @@ def _pmc_traffic(kernel, d, n, world, n_k):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        relaunch_ranks(args)
     import torch
     world, rank, local = setup_dist(args)
     res = bench_data(args, world, rank, local) if args.workload == "data" and not args.no_data else None
@@ -486,9 +591,24 @@ def main():
     mlp_res = None
     if rank == 0 and world == 1 and not args.no_mlp and args.workload == "data":
         mlp_res = bench_mlp(args, local, with_cpu=not args.no_cpu)
+    logi = None
+    if rank == 0 and world == 1 and not args.no_logistic and args.workload == "data":
+        logi = [bench_logistic(args, local, nn, args.logistic_steps if nn > 100_000 else 200)
+                for nn in (10_000, args.n)]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and cov_res is not None:
         cpu = cpu_baseline(args, cov_res["cov"])
+        if logi:
+            hc = cpu["host"]
+            t = _cpu_runs("logistic", args.d, 10_000, thread_sweep(hc["physical_cores"]), steps=2)
+            if t:
+                th, v = _best(t)
+                logi[0]["cpu_baseline"] = dict(
+                    value=v, unit="steps/s", cores=th, kind="port", physical_cores=hc["physical_cores"],
+                    sweep={str(k): 1.0 / x for k, x in sorted(t.items())},
+                    sample=f"oracle logistic Adam step (linear.py:246) at d={args.d}, n=10000 binary X: 2 steps "
+                           f"per thread count after a warm step, threads {sorted(t)}, best shown")
+                logi[0]["vs_cpu"] = logi[0]["value"] / v
     if rank == 0 and res is None and cov_res is None:   # --no-data --no-cov: a profiling run of the other legs
         out = {k: v for k, v in (large_res or {}).items() if k != "cov"}
         print(json.dumps({"config3": out, "full_fit": fit_res, "config5": mlp_res}), flush=True)
@@ -564,21 +684,25 @@ def main():
             lr_ = {k: v for k, v in large_res.items() if k != "cov"}
             if cpu is not None and not args.no_cpu:
                 import tempfile
-                share = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+                phys = cpu["host"]["physical_cores"]
+                cands = sorted({16, max(1, phys // 2), phys})
                 with tempfile.TemporaryDirectory() as td:
                     path = os.path.join(td, "cov.npy")
                     np.save(path, large_res["cov"])
-                    t = _cpu_runs("cov", args.large_d, path, [share], dict(os.environ))
+                    t = _cpu_runs("cov", args.large_d, path, cands, steps=2, timeout=900)
                 if t:
-                    th, tt = next(iter(t.items()))
+                    th, v = _best(t)
                     lr_["cpu_reference_algorithm"] = dict(
-                        value=1.0 / tt, unit="steps/s", cores=th, kind="port",
-                        sample=f"oracle cov-mode Adam steps at d={args.large_d}: 1 and 2 steps, difference "
-                               f"(checkpoint cost cancelled), {th} threads")
-                    lr_["vs_cpu"] = lr_["value"] * tt
+                        value=v, unit="steps/s", cores=th, kind="port", physical_cores=phys,
+                        sweep={str(k): 1.0 / x for k, x in sorted(t.items())},
+                        sample=f"oracle cov-mode Adam steps at d={args.large_d}: 2 steps per thread count after a "
+                               f"warm step, threads {sorted(t)} (1-8 not run: tens of seconds per step), best shown")
+                    lr_["vs_cpu"] = lr_["value"] / v
             line["config3"] = lr_
         if mlp_res is not None:
             line["config5"] = mlp_res
+        if logi:
+            line["logistic"] = logi
         if fit_res is not None:
             fr = dict(fit_res)
             fr["workload"] = f"config2: DagmaLinear('l2').fit(X) defaults, d={d}, n={args.cov_n}, 1 GPU (cov mode)"

@@ -26,13 +26,13 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 4
+#define MIDAGMA_ABI_VERSION 5
 
 /* return codes */
 #define MIDAGMA_OK 0
 #define MIDAGMA_E_HIP (-1)      /* HIP runtime failure            -> RuntimeError        */
 #define MIDAGMA_E_SINGULAR (-2) /* non-finite inverse (scipy getrf info>0) -> LinAlgError */
-#define MIDAGMA_E_ARG (-3)      /* bad argument / shape            -> ValueError          */
+#define MIDAGMA_E_ARG (-3)      /* bad argument / shape, non-finite input (scipy check_finite) -> ValueError */
 #define MIDAGMA_E_STATE (-4)    /* call out of sequence            -> RuntimeError        */
 
 /* loss_type (linear.py:52-53) and score mode */
@@ -95,6 +95,9 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
 /* data mode: zbuf <- X_k^T X_k (all-reduce it, then midagma_cov_from_zbuf(n): cov = zbuf / n). */
 int midagma_data_gram(midagma_solver* s);
 int midagma_cov_from_zbuf(midagma_solver* s, double n);
+/* The solver's cov (d x d, ld) to the host: the `self.cov` attribute fit() keeps (linear.py:428)
+ * when cov was built on the device from the ranks' shards. */
+int midagma_get_cov(midagma_solver* s, double* out, int64_t ld);
 /* The d x d (+ tail) device buffer that carries the per-step score partial Z_k.
  * Bind an external buffer (e.g. a torch tensor that torch.distributed all-reduces). */
 int64_t midagma_zbuf_len(const midagma_solver* s);

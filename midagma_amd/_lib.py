@@ -66,6 +66,7 @@ EXPORTED = {
     "midagma_set_data": (_int, [_vp, _vp, _i64, _i64, _int]),
     "midagma_data_gram": (_int, [_vp]),
     "midagma_cov_from_zbuf": (_int, [_vp, _d]),
+    "midagma_get_cov": (_int, [_vp, _dp, _i64]),
     "midagma_zbuf_len": (_i64, [_vp]),
     "midagma_bind_zbuf": (_int, [_vp, _vp, _i64]),
     "midagma_minimize": (_int, [_vp, _dp, _d, _i64, _d, _d, _d, _d, _d, _d, _i64, C.POINTER(MidagmaResult)]),

@@ -235,6 +235,8 @@ void launch_control(const Params* pr, State* st, const double* partials, const d
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
                          const double* minc, const double* mexc, const double* trek, int64_t d, int64_t D,
                          double* npart, hipStream_t stream);
+// *flag (device int) <- 1 if any of x[0..n) is inf or nan, else 0
+void launch_any_nonfinite(const double* x, int64_t n, int* flag, hipStream_t stream);
 // y = a * x elementwise over n doubles
 void launch_scale(const double* x, double a, double* y, int64_t n, hipStream_t stream);
 // G = 2 * W * Mt on the logical block (linear.py:115)

@@ -24,6 +24,16 @@ using namespace midagma;
 namespace {
 thread_local std::string g_global_error;
 
+// scipy's check_finite (linear.py:226 -> sla.inv(..., check_finite=True)): a non-finite input
+// is a ValueError, not a singular matrix
+bool all_finite(const double* p, int64_t rows, int64_t cols, int64_t ld) {
+  for (int64_t i = 0; i < rows; ++i)
+    for (int64_t j = 0; j < cols; ++j)
+      if (!std::isfinite(p[i * ld + j])) return false;
+  return true;
+}
+constexpr const char* kNonFinite = "array must not contain infs or NaNs";
+
 struct DevBuf {
   double* p = nullptr;
   size_t n = 0;
@@ -759,6 +769,15 @@ void setup_attributes_once() {
   });
 }
 
+// A minimize that ended ST_SINGULAR: the reference's sla.inv raised at that step.  scipy
+// raises ValueError when sI - W*W has a non-finite entry (check_finite: W itself went
+// non-finite, e.g. from non-finite data) and LinAlgError when the finite matrix is singular.
+int singular_or_nonfinite(midagma_solver* s, int rc, const midagma_result* res, const double* W) {
+  if (rc != MIDAGMA_OK || !res || res->status != MIDAGMA_ST_SINGULAR) return rc;
+  if (!all_finite(W, s->d, s->d, s->d)) return fail(s, MIDAGMA_E_ARG, std::string("minimize: ") + kNonFinite);
+  return fail(s, MIDAGMA_E_SINGULAR, "singular matrix: inverse of sI - W*W is not finite");
+}
+
 }  // namespace
 
 extern "C" {
@@ -817,6 +836,7 @@ int64_t midagma_padded_dim(const midagma_solver* s) { return s ? s->D : 0; }
 
 int midagma_set_cov(midagma_solver* s, const double* cov, int64_t ld) {
   if (!s || !cov || ld < s->d) return fail(s, MIDAGMA_E_ARG, "set_cov: bad arguments");
+  if (!all_finite(cov, s->d, s->d, ld)) return fail(s, MIDAGMA_E_ARG, std::string("set_cov: ") + kNonFinite);
   return guarded(s, [&] {
     s->upload_matrix(s->cov, cov, ld);
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -855,6 +875,8 @@ int midagma_set_masks(midagma_solver* s, const double* mask_inc, const double* m
 int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_t n_global, int on_device) {
   if (!s || !X || n_local < 1 || n_global < n_local || s->mode != MIDAGMA_MODE_DATA)
     return fail(s, MIDAGMA_E_ARG, "set_data: bad arguments (data mode only)");
+  if (!on_device && !all_finite(X, n_local, s->d, s->d))
+    return fail(s, MIDAGMA_E_ARG, std::string("set_data: ") + kNonFinite);
   return guarded(s, [&] {
     const int64_t D = s->D;
     s->n_local = n_local;
@@ -866,6 +888,14 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     HIP_TRY(hipMemsetAsync(s->X.p, 0, nx * sizeof(double), s->stream));
     HIP_TRY(hipMemcpy2DAsync(s->X.p, D * sizeof(double), X, s->d * sizeof(double), s->d * sizeof(double), n_local,
                              on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s->stream));
+    if (on_device) {  // the host path checked before the copy
+      int* flag = reinterpret_cast<int*>(s->partials.p);
+      launch_any_nonfinite(s->X.p, (int64_t)nx, flag, s->stream);
+      int bad = 0;
+      HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, s->stream));
+      HIP_TRY(hipStreamSynchronize(s->stream));
+      if (bad) throw std::invalid_argument(std::string("set_data: ") + kNonFinite);
+    }
     size_t mem_free = 0, mem_total = 0;
     HIP_TRY(hipMemGetInfo(&mem_free, &mem_total));
     // (the 128-tile GEMM only: D % 128 == 0; smaller problems are not worth the copy)
@@ -929,6 +959,17 @@ int midagma_cov_from_zbuf(midagma_solver* s, double n) {
   });
 }
 
+int midagma_get_cov(midagma_solver* s, double* out, int64_t ld) {
+  if (!s || !out || ld < s->d) return fail(s, MIDAGMA_E_ARG, "get_cov: bad arguments");
+  if (!s->has_cov) return fail(s, MIDAGMA_E_STATE, "get_cov: no cov (set_cov or cov_from_zbuf first)");
+  return guarded(s, [&] {
+    HIP_TRY(hipMemcpy2DAsync(out, ld * sizeof(double), s->cov.p, s->D * sizeof(double), s->d * sizeof(double), s->d,
+                             hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
+}
+
 int64_t midagma_zbuf_len(const midagma_solver* s) { return s ? s->D * s->D + 64 : 0; }
 
 int midagma_bind_zbuf(midagma_solver* s, void* dev_ptr, int64_t len) {
@@ -943,20 +984,20 @@ int midagma_bind_zbuf(midagma_solver* s, void* dev_ptr, int64_t len) {
 int midagma_minimize(midagma_solver* s, double* W, double mu, int64_t max_iter, double s_dom, double lr, double tol,
                      double beta1, double beta2, double lambda1, int64_t checkpoint, midagma_result* res) {
   if (!s || !W) return fail(s, MIDAGMA_E_ARG, "minimize: null argument");
+  if (!all_finite(W, s->d, s->d, s->d)) return fail(s, MIDAGMA_E_ARG, std::string("minimize: ") + kNonFinite);
   int rc = guarded(s, [&] {
     s->begin(W, mu, max_iter, s_dom, lr, tol, beta1, beta2, lambda1, checkpoint);
     s->run_loop(max_iter, checkpoint);
     s->finish(W, res);
     return MIDAGMA_OK;
   });
-  if (rc == MIDAGMA_OK && res && res->status == MIDAGMA_ST_SINGULAR)
-    return fail(s, MIDAGMA_E_SINGULAR, "singular matrix: inverse of sI - W*W is not finite");
-  return rc;
+  return singular_or_nonfinite(s, rc, res, W);
 }
 
 int midagma_begin(midagma_solver* s, const double* W, double mu, int64_t max_iter, double s_dom, double lr,
                   double tol, double beta1, double beta2, double lambda1, int64_t checkpoint) {
   if (!s || !W) return fail(s, MIDAGMA_E_ARG, "begin: null argument");
+  if (!all_finite(W, s->d, s->d, s->d)) return fail(s, MIDAGMA_E_ARG, std::string("begin: ") + kNonFinite);
   return guarded(s, [&] {
     s->begin(W, mu, max_iter, s_dom, lr, tol, beta1, beta2, lambda1, checkpoint);
     s->ensure_graphs();
@@ -1088,9 +1129,7 @@ int midagma_end(midagma_solver* s, double* W, midagma_result* res) {
     s->finish(W, res);
     return MIDAGMA_OK;
   });
-  if (rc == MIDAGMA_OK && res && res->status == MIDAGMA_ST_SINGULAR)
-    return fail(s, MIDAGMA_E_SINGULAR, "singular matrix: inverse of sI - W*W is not finite");
-  return rc;
+  return singular_or_nonfinite(s, rc, res, W);
 }
 
 // Diagnostics of the fast blocked inverse (not in the public header): per outer block g,
@@ -1195,6 +1234,7 @@ int midagma_trek(midagma_solver* s, const double* W, double* value, double* G) {
 
 int midagma_h(midagma_solver* s, const double* W, double s_dom, double* h, double* G) {
   if (!s || !W || !h) return fail(s, MIDAGMA_E_ARG, "h: null argument");
+  if (!all_finite(W, s->d, s->d, s->d)) return fail(s, MIDAGMA_E_ARG, std::string("h: ") + kNonFinite);
   return guarded(s, [&] {
     const int64_t D = s->D, d = s->d, DD = D * D;
     s->scratch.alloc(DD);

@@ -367,6 +367,21 @@ __global__ __launch_bounds__(NTHREADS) void trace_l1_kernel(const double* __rest
   }
 }
 
+__global__ void any_nonfinite_kernel(const double* __restrict__ x, int64_t n, int* __restrict__ flag) {
+  int f = 0;
+  for (int64_t i = (int64_t)blockIdx.x * NTHREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTHREADS)
+    f |= isfinite(x[i]) ? 0 : 1;
+  if (__any(f) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+void launch_any_nonfinite(const double* x, int64_t n, int* flag, hipStream_t stream) {
+  HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), stream));
+  int64_t blocks = (n + NTHREADS - 1) / NTHREADS;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  hipLaunchKernelGGL(any_nonfinite_kernel, dim3((unsigned)blocks), dim3(NTHREADS), 0, stream, x, n, flag);
+  HIP_TRY(hipGetLastError());
+}
+
 void launch_reduce_check(const double* Mt, const double* W, const double* Z, const Params*, State* st,
                          double* partials, int64_t d, int64_t D, hipStream_t stream) {
   hipLaunchKernelGGL(reduce_check_kernel, dim3(NRED), dim3(NTHREADS), 0, stream, Mt, W, Z, st, partials, d, D);

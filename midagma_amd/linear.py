@@ -12,6 +12,14 @@ the C ABI.  Extra keyword-only constructor arguments:
 * ``device``      HIP device ordinal (default: LOCAL_RANK or 0).
 * ``process_group``  a torch.distributed group: in data mode each rank keeps
   its row shard of X and the per-step score partial is all-reduced over it.
+* ``force_allreduce``  run the all-reduce path (torch-owned score buffer,
+  `dist.all_reduce` on the solver stream) even on one rank (tests, rehearsals).
+* ``solver_factory``  the backend class (default `HipSolver`; tests pass a CPU double).
+
+`fit(X, ..., n_global=N)` (keyword-only extra): X is this rank's row shard of an
+N-row data matrix.  Each rank then touches only its own rows: l2 centring uses
+the all-reduced column sums (linear.py:411), and cov = X^T X / n (linear.py:428)
+is the all-reduced sum of the ranks' device Gram matrices X_k^T X_k.
 
 Trek regularizers (`trek_reg`, linear.py:251-258): the PST family of
 `notreks.PSTRegularizer` (seq exp / inv / log / binom, agg mean / sum / max / lse,
@@ -59,7 +67,8 @@ class DagmaLinear:
 
     def __init__(self, loss_type: str, verbose: bool = False, dtype: type = np.float64, *,
                  trek_reg=None, logger=None, log_cfg=None, score_mode: str | None = None,
-                 device: int | None = None, process_group=None) -> None:
+                 device: int | None = None, process_group=None, force_allreduce: bool = False,
+                 solver_factory=None) -> None:
         losses = ["l2", "logistic"]
         assert loss_type in losses, f"loss_type should be one of {losses}"
         if dtype is not np.float64:
@@ -82,7 +91,10 @@ class DagmaLinear:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         self.device = device
         self.process_group = process_group
+        self.force_allreduce = bool(force_allreduce)
+        self._solver_factory = solver_factory or HipSolver
         self._solver: HipSolver | None = None
+        self._allreduce = None
         self.minimize_log: list = []
 
     # ------------------------------------------------------------------ helpers
@@ -97,28 +109,46 @@ class DagmaLinear:
             pass
         return 1, 0
 
-    def _setup_solver(self):
+    def _allreduce_host(self, v: np.ndarray) -> np.ndarray:
+        """Sum a small host vector over the ranks of the process group (fit-time only)."""
+        import torch
+        import torch.distributed as dist
+        on_gpu = dist.get_backend(self.process_group) == "nccl"
+        t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64))
+        t = t.to(torch.device("cuda", self.device)) if on_gpu else t.clone()
+        dist.all_reduce(t, group=self.process_group)
+        return t.cpu().numpy()
+
+    def _setup_solver(self, X_local=None, cov_on_device=False):
         world, rank = self._world()
-        s = HipSolver(self.d, self.loss_type, self.score_mode, device=self.device)
+        s = self._solver_factory(self.d, self.loss_type, self.score_mode, device=self.device)
+        self._allreduce = None
         if self.score_mode == "data":
-            lo, hi = _row_range(self.n, world, rank)
-            s.set_data(np.ascontiguousarray(self.X[lo:hi]), n_global=self.n)
-            if world > 1:
-                import torch
+            if X_local is None:
+                lo, hi = _row_range(self.n, world, rank)
+                X_local = self.X[lo:hi]
+            s.set_data(np.ascontiguousarray(X_local), n_global=self.n)
+            if world > 1 or self.force_allreduce:
                 import torch.distributed as dist
-                ext = torch.cuda.ExternalStream(s.stream, device=torch.device("cuda", self.device))
-                zt = torch.zeros(s.zbuf_len, dtype=torch.float64, device=torch.device("cuda", self.device))
-                s.bind_zbuf(zt.data_ptr(), zt.numel())
+                zt, on_stream = s.torch_zbuf()
                 pg = self.process_group
 
                 def _allreduce():
-                    with torch.cuda.stream(ext):
+                    with on_stream():
                         dist.all_reduce(zt, group=pg)
 
                 self._allreduce, self._zt = _allreduce, zt
+            if cov_on_device:
+                # cov = (sum_k X_k^T X_k) / n (linear.py:428) from the ranks' device Gram matrices
+                s.data_gram()
+                if self._allreduce is not None:
+                    self._allreduce()
+                s.cov_from_zbuf(float(self.n))
+                self.cov = s.get_cov()
             else:
-                self._allreduce = None
-        s.set_cov(self.cov)
+                s.set_cov(self.cov)
+        else:
+            s.set_cov(self.cov)
         tr = self.trek_reg
         if tr is not None and tr.enabled() and tr.cfg.get("I") is not None and len(tr.cfg["I"]) > 0:
             if str(tr.name).lower().strip() == "tcc":
@@ -138,7 +168,7 @@ class DagmaLinear:
         if self.score_mode == "cov":
             return self._solver.score_value(W)
         self._solver.score_partial(W)
-        if getattr(self, "_allreduce", None) is not None:
+        if self._allreduce is not None:
             self._allreduce()
         return self._solver.score_finish()
 
@@ -187,7 +217,7 @@ class DagmaLinear:
         mask_inc, mask_exc = self._masks(mu)
         self._solver.set_masks(mask_inc, mask_exc)
         logging_on = bool(self._log_cfg.enabled)
-        if self.score_mode == "data" and getattr(self, "_allreduce", None) is not None:
+        if self.score_mode == "data" and self._allreduce is not None:
             res = run_allreduce_minimize(self._solver, W, mu, max_iter, s, lr, tol, beta_1, beta_2,
                                          self.lambda1, self.checkpoint, allreduce=self._allreduce)
             ckpts = self._solver.checkpoints() if logging_on else ()
@@ -217,13 +247,25 @@ class DagmaLinear:
             warm_iter: int = 3e4, max_iter: int = 6e4, lr: float = 0.0003, checkpoint: int = 1000,
             beta_1: float = 0.99, beta_2: float = 0.999,
             exclude_edges: typing.Optional[typing.List[typing.Tuple[int, int]]] = None,
-            include_edges: typing.Optional[typing.List[typing.Tuple[int, int]]] = None) -> np.ndarray:
-        """Runs DAGMA and returns the thresholded weighted adjacency (linear.py:335-462)."""
+            include_edges: typing.Optional[typing.List[typing.Tuple[int, int]]] = None, *,
+            n_global: int | None = None) -> np.ndarray:
+        """Runs DAGMA and returns the thresholded weighted adjacency (linear.py:335-462).
+        n_global: X is this rank's row shard of an n_global-row matrix (data mode)."""
+        world, rank = self._world()
+        sharded = n_global is not None
+        if sharded and self.score_mode != "data":
+            raise ValueError("fit(X_shard, n_global=...) needs score_mode='data'")
         self.X, self.lambda1, self.checkpoint = X, lambda1, checkpoint
-        self.n, self.d = X.shape
+        self.n, self.d = (int(n_global), X.shape[1]) if sharded else X.shape
         self.Id = np.eye(self.d).astype(self.dtype)
         if self.loss_type == 'l2':
-            self.X -= X.mean(axis=0, keepdims=True)
+            if sharded:  # the global column mean from the ranks' column sums
+                colsum = X.sum(axis=0)
+                if world > 1:
+                    colsum = self._allreduce_host(colsum)
+                self.X -= (colsum / float(self.n))[None, :]
+            else:
+                self.X -= X.mean(axis=0, keepdims=True)
         self.exc_r, self.exc_c = None, None
         self.inc_r, self.inc_c = None, None
         if exclude_edges is not None:
@@ -238,9 +280,14 @@ class DagmaLinear:
                 self.inc_r, self.inc_c = zip(*include_edges)
             else:
                 ValueError("whitelist should be a tuple of edges, e.g., ((1,2), (2,3))")
-        self.cov = X.T @ X / float(self.n)
+        # data mode over several ranks (or a shard): cov from the device Gram matrices, no rank
+        # multiplies another rank's rows; one rank keeps the reference's host product
+        cov_on_device = self.score_mode == "data" and (sharded or world > 1)
+        X_local = X if sharded else None
+        if not cov_on_device:
+            self.cov = X.T @ X / float(self.n)
         self.W_est = np.zeros((self.d, self.d)).astype(self.dtype)
-        self._setup_solver()
+        self._setup_solver(X_local=X_local, cov_on_device=cov_on_device)
         mu = mu_init
         if type(s) == list:
             if len(s) < T:

@@ -153,6 +153,22 @@ class HipSolver:
     def cov_from_zbuf(self, n: float):
         check(self.L.midagma_cov_from_zbuf(self.h, float(n)), self.h, "cov_from_zbuf")
 
+    def get_cov(self) -> np.ndarray:
+        out = np.empty((self.d, self.d))
+        check(self.L.midagma_get_cov(self.h, dptr(out), self.d), self.h, "get_cov")
+        return out
+
+    def torch_zbuf(self):
+        """A torch CUDA tensor bound as this solver's score-partial buffer, and a context that
+        makes the solver's stream torch's current one: `with ctx: dist.all_reduce(zt)` sums the
+        partial over ranks in stream order with the slot kernels (RCCL on the solver stream)."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        zt = torch.zeros(self.zbuf_len, dtype=torch.float64, device=dev)
+        self.bind_zbuf(zt.data_ptr(), zt.numel())
+        ext = torch.cuda.ExternalStream(self.stream, device=dev)
+        return zt, (lambda: torch.cuda.stream(ext))
+
     @property
     def zbuf_len(self) -> int:
         return int(self.L.midagma_zbuf_len(self.h))

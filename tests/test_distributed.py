@@ -145,3 +145,115 @@ def test_data_parallel_matches_single_process(world, golden):
     W_ref, tr = o.minimize(np.zeros((20, 20)), 1.0, K, 1.0, 3e-4, tol=-1.0)
     assert tr.iters == K
     assert np.abs(W0 - W_ref).max() <= 1e-9
+
+
+class _ShardSolver(_ShardBackend):
+    """CPU double of HipSolver for DagmaLinear.fit in data mode: the calls fit() makes
+    (set_data / data_gram / torch_zbuf / cov_from_zbuf / get_cov / the step protocol / h / score),
+    each on this rank's rows only."""
+
+    def __init__(self, d, loss, mode, device=0):
+        assert loss == "l2" and mode == "data"
+        self.d = d
+        self.zfull = torch.zeros(d * d + 64, dtype=torch.float64)  # the bound score buffer (+ tail)
+        self.z = self.zfull[:d * d]
+        self.rows_seen = 0
+
+    def set_data(self, X, n_global=None):
+        from oracle.dagma_oracle import AdamState
+        self.X, self.n = np.array(X), int(n_global)
+        self.rows_seen = self.X.shape[0]
+        self._Adam = AdamState
+
+    def torch_zbuf(self):
+        import contextlib
+        return self.zfull, contextlib.nullcontext
+
+    def data_gram(self):
+        self.z.copy_(torch.from_numpy((self.X.T @ self.X).reshape(-1)))
+
+    def cov_from_zbuf(self, n):
+        self.cov = self.z.numpy().reshape(self.d, self.d) / n
+
+    def get_cov(self):
+        return self.cov.copy()
+
+    def set_masks(self, mask_inc, mask_exc):
+        assert mask_inc is None and mask_exc is None
+
+    def begin(self, W, mu, max_iter, s, lr, tol, b1, b2, lambda1, checkpoint):
+        self.l1 = lambda1
+        super().begin(W, mu, max_iter, s, lr, tol, b1, b2, lambda1, checkpoint)
+
+    def step_partial(self):
+        if self.status != _lib.ST_RUNNING:
+            return
+        Zk = self.X.T @ (self.X @ (np.eye(self.d) - self.W))
+        self.z.copy_(torch.from_numpy(Zk.reshape(-1)))
+
+    def end(self, W):
+        from midagma_amd.solver import MinimizeResult
+        W[...] = self.W
+        return MinimizeResult(iters=self.it, success=self.status != _lib.ST_FAILED, status=self.status,
+                              halvings=self.halvings, early_stop=False, lr_final=self.lr, slots=self.it,
+                              obj_last=0.0, score_last=0.0, h_last=0.0)
+
+    def h_value(self, W, s=1.0, grad=True):
+        from oracle.dagma_oracle import h_logdet
+        return h_logdet(W, s)
+
+    def score_partial(self, W):
+        self._diff = np.eye(self.d) - W
+        Zk = self.X.T @ (self.X @ self._diff)
+        self.z.copy_(torch.from_numpy(Zk.reshape(-1)))
+
+    def score_finish(self):
+        Z = self.z.numpy().reshape(self.d, self.d)
+        return 0.5 * (np.sum(self._diff * Z) / self.n), -(Z / self.n)
+
+
+def _fit_worker(rank, world, port, X_shard, n_global, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from midagma_amd import DagmaLinear
+        m = DagmaLinear("l2", score_mode="data", solver_factory=_ShardSolver)
+        Xs = X_shard.copy()
+        W = m.fit(Xs, lambda1=0.03, T=2, warm_iter=300, max_iter=400, n_global=n_global)
+        out_q.put((rank, W, m.cov, Xs, m._solver.rows_seen, m.h_final, m.score_final,
+                   [e["iters"] for e in m.minimize_log]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_fit_each_rank_ingests_only_its_rows(golden):
+    """fit(X_shard, n_global=n) over 2 gloo ranks: every rank receives only its rows; the
+    centring (all-reduced column sums) and cov (all-reduced Gram matrices) are the oracle's
+    to rounding, and the fit matches the oracle's fit of the full X to 1e-9."""
+    from oracle.dagma_oracle import LinearOracle
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    n, world = X.shape[0], 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    spans = [_row_range(n, world, r) for r in range(world)]
+    procs = [ctx.Process(target=_fit_worker, args=(r, world, port, X[lo:hi].copy(), n, q))
+             for r, (lo, hi) in enumerate(spans)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=150) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    o = LinearOracle("l2")
+    W_ref = o.fit(X.copy(), lambda1=0.03, T=2, warm_iter=300, max_iter=400)
+    for r, W, cov, Xs, rows_seen, h, sc, iters in outs:
+        lo, hi = spans[r]
+        assert rows_seen == hi - lo
+        assert np.abs(Xs - o.X[lo:hi]).max() <= 1e-13            # centred with the global mean
+        assert np.abs(cov - o.cov).max() <= 1e-12 * np.abs(o.cov).max()
+        assert iters == [300, 400]
+        assert np.abs(W - W_ref).max() <= 1e-9
+        assert np.array_equal(W != 0, W_ref != 0)
+        assert abs(h - o.h_final) <= 1e-9 and abs(sc - o.score_final) <= 1e-9
+    assert np.array_equal(outs[0][1], outs[1][1]), "replicas diverged"

@@ -76,3 +76,61 @@ def test_two_ranks_match_single_process(loss):
         # binary X: exactly-zero gradient entries take their L1 branch from rounding (see
         # test_gpu_parity.test_logistic_data_mode); the rank-split sum is another valid order
         assert dW.max() <= 1e-3 and (dW > 1e-9).mean() <= 0.05
+
+
+_NCCL_CHILD = r"""
+import json, os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+from midagma_amd import DagmaLinear
+from midagma_amd.simulate import make_dataset
+X, _, _ = make_dataset(64, 3000, seed=5)
+kw = dict(lambda1=0.03, T=2, warm_iter=600, max_iter=800)
+m0 = DagmaLinear("l2", score_mode="data", device=0)
+W0 = m0.fit(X.copy(), **kw)
+dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=0, world_size=1,
+                        device_id=torch.device("cuda", 0))
+m1 = DagmaLinear("l2", score_mode="data", device=0, force_allreduce=True)
+W1 = m1.fit(X.copy(), **kw)
+m2 = DagmaLinear("l2", score_mode="data", device=0, force_allreduce=True)
+W2 = m2.fit(X.copy(), n_global=X.shape[0], **kw)
+out = dict(it0=[e["iters"] for e in m0.minimize_log], it1=[e["iters"] for e in m1.minimize_log],
+           bit_identical=bool(np.array_equal(W1, W0)), h=[m0.h_final, m1.h_final], sc=[m0.score_final, m1.score_final],
+           allreduce_path=m1._allreduce is not None and m2._allreduce is not None,
+           cov_rel=float(np.abs(m2.cov - m0.cov).max() / np.abs(m0.cov).max()),
+           dW2=float(np.abs(W2 - W0).max()), support2=bool(np.array_equal(W2 != 0, W0 != 0)))
+print(json.dumps(out), flush=True)
+for m in (m0, m1, m2):
+    m._solver.close()
+torch.cuda.synchronize()
+dist.destroy_process_group()
+print("DESTROYED", flush=True)
+"""
+
+
+def test_nccl_one_rank_allreduce_path_bit_identical():
+    """The RCCL code path at world size 1: DagmaLinear(score_mode='data', force_allreduce=True)
+    under a one-rank 'nccl' process group runs every step as step_partial -> dist.all_reduce of
+    the torch-owned score buffer on the solver's stream (ExternalStream) -> step_finish.  A
+    one-rank sum is the identity, so W must equal the single-process run bit for bit.  The
+    sharded form fit(X, n_global=n) (device Gram + all-reduce for cov) must agree to 1e-9.
+    Runs in a child process (its own HIP/RCCL state), which also destroys the process group."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NCCL_DEBUG="WARN")
+    r = subprocess.run([sys.executable, "-c", _NCCL_CHILD, repo, str(_free_port())], capture_output=True,
+                       text=True, timeout=240, env=env)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert lines, f"child rc={r.returncode}: {r.stderr[-3000:]}"
+    out = json.loads(lines[-1])
+    assert out["allreduce_path"]
+    assert out["it1"] == out["it0"]
+    assert out["bit_identical"]
+    assert out["h"][0] == out["h"][1] and out["sc"][0] == out["sc"][1]
+    assert out["cov_rel"] <= 1e-12
+    assert out["dW2"] <= 1e-9 and out["support2"]
+    assert "DESTROYED" in r.stdout and r.returncode == 0, f"destroy_process_group: rc={r.returncode} {r.stderr[-3000:]}"

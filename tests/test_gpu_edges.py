@@ -67,3 +67,56 @@ def test_dagma_linear_fit_tiny():
     X = _case(2, 200)
     W = DagmaLinear("l2").fit(X, lambda1=0.02, T=2, warm_iter=500, max_iter=800)
     assert W.shape == (2, 2) and np.isfinite(W).all() and W[0, 0] == 0 and W[1, 1] == 0
+
+
+def test_nonfinite_inputs_raise_value_error():
+    """scipy's check_finite (linear.py:226): non-finite W / cov / X -> ValueError."""
+    from midagma_amd.solver import HipSolver
+    X = _case(6, 80)
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 10)
+    s = HipSolver(6, "l2", "cov", device=0)
+    bad = o.cov.copy()
+    bad[1, 2] = np.inf
+    with pytest.raises(ValueError):
+        s.set_cov(bad)
+    s.set_cov(o.cov)
+    W = np.zeros((6, 6))
+    W[0, 4] = np.nan
+    with pytest.raises(ValueError):
+        s.minimize(W, 1.0, 5, 1.0, 3e-4, lambda1=0.03)
+    with pytest.raises(ValueError):
+        s.h_value(W, 1.0)
+    s.close()
+    sd = HipSolver(6, "l2", "data", device=0)
+    Xb = X - X.mean(axis=0, keepdims=True)
+    Xb[7, 3] = np.nan
+    with pytest.raises(ValueError):
+        sd.set_data(Xb, n_global=80)
+    with pytest.raises(ValueError):
+        sd.set_data(torch.from_numpy(Xb).cuda(), n_global=80)   # device-pointer path
+    sd.close()
+
+
+def test_singular_vs_nonfinite_during_minimize():
+    """A finite singular sI - W o W -> LinAlgError (LAPACK getrf info > 0); W that turns
+    non-finite inside the loop (non-finite data) -> ValueError, as sla.inv's check_finite."""
+    from midagma_amd.solver import HipSolver
+    X = _case(2, 60)
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 10)
+    s = HipSolver(2, "l2", "cov", device=0)
+    s.set_cov(o.cov)
+    W = np.array([[0.0, 1.0], [1.0, 0.0]])
+    with pytest.raises(np.linalg.LinAlgError):
+        s.minimize(W, 1.0, 5, 1.0, 3e-4, lambda1=0.03)
+    s.close()
+    # data mode with a huge entry: G overflows to inf, Adam makes W nan after step 1
+    Xh = X - X.mean(axis=0, keepdims=True)
+    Xh[3, 0] = 1e200
+    sd = HipSolver(2, "l2", "data", device=0)
+    sd.set_data(Xh, n_global=60)
+    W = np.zeros((2, 2))
+    with pytest.raises(ValueError):
+        sd.minimize(W, 1.0, 5, 1.0, 3e-4, lambda1=0.03)
+    sd.close()

@@ -1,0 +1,82 @@
+#!/bin/bash
+# The one GPU-box driver (run under gpurun from the repo root):
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- 'bash tools/gpu.sh TASK [ARGS...]'
+# Every GPU step runs under its own `timeout -k 10`; the first failure ends the call.
+#
+# TASK
+#   tests [PATHS/ARGS]    pytest -m gpu (default path: tests) (one process, as the driver runs it) -> gpurun_out/gpu_tests.log
+#   smoke                 __graft_entry__.smoke()
+#   bench [BENCH ARGS]    python bench.py -> gpurun_out/bench.json (+ .err)
+#   prof LEG              rocprofv3 --kernel-trace --stats of one bench leg -> gpurun_out/prof_LEG/
+#                         LEG: data | cov | large | small | logistic | mlp
+#   pmc LEG               FETCH_SIZE and WRITE_SIZE passes (each its own run) of one leg,
+#                         summarised per kernel -> gpurun_out/pmc_LEG.json (tools/pmc_summary.py)
+#   probe NAME [ARGS]     python tools/NAME.py ARGS (probe_perf, peak_probe, blocked_debug, ...)
+# Several tasks may be chained in one call: `bash tools/gpu.sh tests -- bench -- prof cov`.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+
+leg_args() {
+  case "$1" in
+    data)     echo "--steps 5 --warmup 1 --no-cpu --no-cov --no-fit --no-large --no-mlp --no-logistic" ;;
+    cov)      echo "--workload cov --cov-steps 2000 --no-cpu --no-fit --no-large" ;;
+    large)    echo "--no-data --no-cov --no-fit --no-cpu --no-mlp --no-logistic --large-steps 200" ;;
+    mlp)      echo "--no-data --no-cov --no-fit --no-cpu --no-large --no-logistic" ;;
+    logistic) echo "--no-data --no-cov --no-fit --no-cpu --no-large --no-mlp" ;;
+    *) return 1 ;;
+  esac
+}
+
+run_task() {
+  local task=$1; shift
+  case "$task" in
+    tests)
+      [ $# -eq 0 ] && set -- tests
+      timeout -k 10 1500 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
+        > gpurun_out/gpu_tests.log 2>&1; local rc=$?
+      grep -E "passed|failed|error" gpurun_out/gpu_tests.log | tail -3; return $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; local rc=$?
+      tail -3 gpurun_out/smoke.log; return $rc ;;
+    bench)
+      timeout -k 10 1100 python bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err; local rc=$?
+      echo "bench rc=$rc"; cat gpurun_out/bench.json; grep -v amdgpu.ids gpurun_out/bench.err | tail -8; return $rc ;;
+    prof)
+      local leg=$1 a
+      if [ "$leg" = small ]; then a="$R/tools/probe_perf.py small"; else a="$R/bench.py $(leg_args "$leg")" || return 2; fi
+      (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$leg" -o "$leg" \
+        --output-format csv -- python3 $a > "$R/gpurun_out/prof_$leg.log" 2>&1); local rc=$?
+      echo "prof $leg rc=$rc"; return $rc ;;
+    pmc)
+      local leg=$1 a c
+      if [ "$leg" = small ]; then a="$R/tools/probe_perf.py small"; else a="$R/bench.py $(leg_args "$leg") --profile-reps 1" || return 2; fi
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && timeout -s KILL 600 rocprofv3 --pmc $c --kernel-trace -d "$R/gpurun_out/pmc_${leg}_$c" -o p \
+          --output-format csv -- python3 $a > "$R/gpurun_out/pmc_${leg}_$c.log" 2>&1) || { echo "pmc $leg $c failed"; return 1; }
+      done
+      python3 tools/pmc_summary.py "gpurun_out/pmc_${leg}_FETCH_SIZE" "gpurun_out/pmc_${leg}_WRITE_SIZE" \
+        "gpurun_out/pmc_$leg.json"; return $? ;;
+    probe)
+      local name=$1; shift
+      timeout -k 10 900 python "tools/$name.py" "$@" > "gpurun_out/probe_$name.log" 2>&1; local rc=$?
+      tail -30 "gpurun_out/probe_$name.log"; return $rc ;;
+    *) echo "unknown task $task"; return 2 ;;
+  esac
+}
+
+# split the argument list on "--" into tasks
+args=("$@")
+cur=()
+for a in "${args[@]}" "--"; do
+  if [ "$a" = "--" ]; then
+    if [ ${#cur[@]} -gt 0 ]; then
+      run_task "${cur[@]}" || exit $?
+    fi
+    cur=()
+  else
+    cur+=("$a")
+  fi
+done
+exit 0
