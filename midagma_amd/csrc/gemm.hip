@@ -261,21 +261,31 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
         }
     return;
   }
+  // (sigmoid: the accumulators pass through a per-lane LDS stage so that the transcendental
+  // loop can stay rolled without demoting acc to scratch; see gemm_pipe_kernel)
   const bool want_loss = loss_part != nullptr && (st == nullptr || st->ckpt_pending);
   double part = 0.0;
+  __syncthreads();
+  double* stg = smem + (tid >> 6) * 1024 + lane;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
+      for (int tt = 0; tt < 4; ++tt) stg[(4 * j + tt) * 64] = acc[i][j][tt];
+#pragma unroll 1
+    for (int jt = 0; jt < 16; ++jt) {
+      const int j = jt >> 2, tt = jt & 3;
+      {
         const int64_t row = m0 + mb + i * 16 + acc_row(lane, tt);
         const int64_t col = n0 + nbs + j * 16 + acc_col(lane);
-        const double v = acc[i][j][tt];
+        const double v = stg[jt * 64];
         if (want_loss && row < m_valid && col < n_valid)  // X[row][col]: A's (m, k) = (row, col)
           part += logaddexp0(v) - (ATRANS ? A[col * lda + row] : A[row * lda + col]) * v;
         Ct[row * ldc + col] = 1.0 / (1.0 + exp(-v));
       }
+    }
+  }
   if (!want_loss) return;
   __syncthreads();
   double* red = smem;
@@ -519,25 +529,38 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64
     return;
   }
   // EPI_SIGMOID: C = expit(acc); loss partial sum(logaddexp(0, acc) - X * acc) over the valid
-  // block, X = op(A) at (row, col)
+  // block, X = op(A) at (row, col).
+  // The 64 accumulators stay in registers only while every index into acc is a compile-time
+  // constant, and the f64 exp / log bodies are too large to unroll 64 times: hipcc then keeps
+  // acc in scratch for the whole kernel (544 B/lane, the GEMM 5x slower).  So each 16-row block
+  // is parked in a per-lane LDS stage with constant indices, and a rolled loop does the
+  // transcendental work.  A lane reads back only its own slots (no barrier inside).
   const bool want_loss = loss_part != nullptr && (st == nullptr || st->ckpt_pending);
   double part = 0.0;
+  __syncthreads();  // every wave is done with the A images the stage overlays
+  double* stg = smem + w * 512 + lane;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 8; ++i) {
 #pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      stg[(2 * tt) * 64] = acc[i][0][tt];
+      stg[(2 * tt + 1) * 64] = acc[i][1][tt];
+    }
+#pragma unroll 1
     for (int tt = 0; tt < 4; ++tt) {
       const int64_t row = m0 + 16 * i + acc_row(lane, tt);
       const int64_t col = nw + 2 * acc_col(lane);
       double2 o;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const double v = acc[i][j][tt];
+        const double v = stg[(2 * tt + j) * 64];
         if (want_loss && row < m_valid && col + j < n_valid)
           part += logaddexp0(v) - (AMODE ? A[(col + j) * lda + row] : A[row * lda + col + j]) * v;
         (j ? o.y : o.x) = 1.0 / (1.0 + exp(-v));
       }
       *reinterpret_cast<double2*>(Ct + row * ldc + col) = o;
     }
+  }
   if (!want_loss) return;
   __syncthreads();
   double* red = smem;

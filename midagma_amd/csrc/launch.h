@@ -67,6 +67,20 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
 void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes = NM_PASSES_RUN);
 
+// --- small.hip --------------------------------------------------------------
+// LDS/register block edge of the one-workgroup small-d inner loop (16, 32 or 64; 0: d > 64).
+int small_block(int64_t d);
+// Up to n_slots slots of the cov-mode l2 inner loop (linear.py:224-331) in one persistent
+// workgroup: W, m, v (leading dimension pr->D) are read at entry and written back at exit,
+// with the State.  Across launches: carry (NORM_FIELDS + 1 doubles) holds a pending
+// checkpoint step's norms and the warm-start count, pstore (2 x 32 x 32) the last two
+// inverses; zero carry before a call's first launch.  Slots after a terminal status are
+// not run.
+void launch_small_minimize(const Params* pr, State* st, double* W, double* m, double* v, const double* covs,
+                           const double* minc, const double* mexc, const double* bc_table, CkptRec* ckpt,
+                           int64_t ckpt_cap, double* carry, double* pstore, int64_t d, int64_t n_slots,
+                           hipStream_t stream);
+
 // --- trek.hip ---------------------------------------------------------------
 enum TrekSeq : int { TREK_EXP = 0, TREK_INV = 1, TREK_LOG = 2, TREK_BINOM = 3 };
 enum TrekAgg : int { TREK_MEAN = 0, TREK_SUM = 1, TREK_MAX = 2, TREK_LSE = 3 };

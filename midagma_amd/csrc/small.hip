@@ -1,0 +1,627 @@
+// Small-d cov-mode inner loop in ONE persistent workgroup (d <= 32, l2, no trek regularizer).
+//
+// At d = 20 a graph-replayed slot is 8 dependent launches of a 64 x 64 padded problem, each
+// 4-6 us (profiles/r01_rocprof_cov_small_kernel_stats.csv): the GPU ran the reference's loop
+// only 1.7x faster than its CPU.  Here the whole per-mu state lives in one CU for as many
+// Adam steps as the host asks for:
+//   registers : this lane's elements of W, m, v, the inverse and the score gradient, and the
+//               last two slots' inverses (the warm start)
+//   LDS       : (-mu) cov (the score GEMM's A operand, loaded once per launch), W and
+//               I - W images (the transposed build and the MFMA B operand), the product
+//               form's operand images, the Gauss-Jordan pivot row / column (double-buffered),
+//               pivots, reduction slots, the State and the controller's decision
+// One slot is exactly the reference's loop body (linear.py:224-331), in its order:
+//   build (sI - W o W)^T -> its inverse: the warm-started product form on
+//   v_mfma_f64_16x16x4f64 (3-4 dependent 32^3 products), or the unpivoted Gauss-Jordan
+//   (d steps, one barrier each; sI - W o W is an M-matrix in the domain) on
+//   checkpoint slots, which need the pivots for log|det| -> rhs = ((-mu) cov)(I - W) on the
+//   matrix cores -> domain test any(inv + 1e-16 < 0) / non-finite ->
+//   control (checkpoint objective + tolerance, line search, lr halving: the decisions of
+//   step.hip's control_kernel, by thread 0 on a State kept in LDS, broadcast through LDS) ->
+//   G_obj, Adam, W -= lr g, W *= mask (or the line-search revert / halving).
+// Element ownership follows the f64 16x16x4 MFMA accumulator map, so every product's output
+// lands in the registers of the lane that owns the element: wave w owns the 16 x 16 tile
+// (w / (DS/16), w % (DS/16)); lane l owns column 16 tc + (l & 15), rows 16 tr + (l >> 4) + 4 t
+// for t = 0..3.  DS = 16, 32 -> 1, 4 waves.
+// Arithmetic per element is step.hip's, in the same order (built with -ffp-contract=off).
+#include "launch.h"
+#include "mfma64.h"
+
+namespace midagma {
+namespace {
+
+__device__ __forceinline__ double sgn(double w) { return w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : w); }
+
+__device__ __forceinline__ double wave_sum(double x) {
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  return x;
+}
+__device__ __forceinline__ double wave_max(double x) {
+  for (int off = 32; off > 0; off >>= 1) x = fmax(x, __shfl_xor(x, off));
+  return x;
+}
+__device__ __forceinline__ double wave_min(double x) {
+  for (int off = 32; off > 0; off >>= 1) x = fmin(x, __shfl_xor(x, off));
+  return x;
+}
+
+// colb position of row i: the 4 rows a lane owns (16 tr + q + 4 t) are 4 consecutive slots
+__device__ __forceinline__ int cpos(int i) { return (i & ~15) + 4 * (i & 3) + ((i & 15) >> 2); }
+
+// acc += A[row0 .. row0+15][0 .. kd) * B[0 .. kd)[col0 .. col0+15] on the f64 16x16x4 MFMA;
+// A from an [m][k] image (stride SA_), B from a [k][n] image (stride SB_).  Terms with
+// k >= d are exact zeros in every product of this file (zero off-diagonal padding).
+template <int DS, int SA_, int SB_>
+__device__ __forceinline__ dbl4 tile_mma(const double* __restrict__ A, const double* __restrict__ B, int row0,
+                                         int col0, int q, int c, int kd, dbl4 acc) {
+#pragma unroll
+  for (int kk = 0; kk < DS / 4; ++kk)
+    if (4 * kk < kd)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(row0 + c) * SA_ + 4 * kk + q], B[(4 * kk + q) * SB_ + col0 + c],
+                                                 acc, 0, 0, 0);
+  return acc;
+}
+
+struct SmallCtl {
+  int32_t act, norms, run, pad_;
+  double lr_a, lr_b, bc1, bc2;
+};
+
+// The controller: step.hip's control_kernel decisions (linear.py:230-241, 279-331) on the
+// State in LDS, run by thread 0 once per slot.  Kept out of line: inlined into the slot loop,
+// its code raised the kernel to 230+ VGPRs (DS = 64 spilled inside the Gauss-Jordan loop).
+template <int NW>
+__device__ __noinline__ void small_control(const Params* __restrict__ pr, State& S, SmallCtl& ctl,
+                                           const double (*red)[NW], const double (*nred)[NW], const int* flw,
+                                           CkptRec* __restrict__ ckpt, int64_t ckpt_cap, double bc1n,
+                                           double bc2n) {
+    int flags = 0;
+#pragma unroll 1
+    for (int x = 0; x < NW; ++x) flags |= flw[x];
+    if (S.slots == 0) S.t0 = __builtin_amdgcn_s_memrealtime();
+    S.slots += 1;
+    S.warm_valid = 1;
+    S.warm_run = S.warm_run < 2 ? S.warm_run + 1 : 2;
+    S.flags = 0;
+    int act = ACT_NOOP;
+    bool running = true;
+    if (S.ckpt_pending) {
+      double sd = 0.0, l1 = 0.0, ld = 0.0;
+      double nf[NORM_FIELDS];
+#pragma unroll 1
+      for (int x = 0; x < NW; ++x) {
+        sd += red[0][x];
+        l1 += red[1][x];
+        ld += red[2][x];
+      }
+      for (int f = 0; f < NORM_FIELDS; ++f) {
+        double x = f == NF_WMIN ? INFINITY : 0.0;
+#pragma unroll 1
+        for (int y = 0; y < NW; ++y)
+          x = f == NF_WMAX ? fmax(x, nred[f][y]) : (f == NF_WMIN ? fmin(x, nred[f][y]) : x + nred[f][y]);
+        nf[f] = x;
+      }
+      S.ckpt_pending = 0;
+      const double h = -ld + pr->d_log_s;
+      const double score = pr->score_scale * sd;
+      const double obj = pr->mu * (score + pr->lambda1 * l1) + h;
+      if (S.n_ckpt < ckpt_cap) {
+        CkptRec& r = ckpt[S.n_ckpt];
+        r.iter = S.iter;
+        r.obj = obj;
+        r.score = score;
+        r.h = h;
+        r.lr = S.lr;
+        r.l1 = l1;
+        r.w_norm = sqrt(nf[NF_W2]);
+        r.max_abs_w = nf[NF_WMAX];
+        r.min_abs_w_nonzero = isfinite(nf[NF_WMIN]) ? nf[NF_WMIN] : 0.0;  // linear.py:311
+        r.grad_raw_norm = sqrt(nf[NF_GOBJ]);
+        r.grad_step_norm = sqrt(nf[NF_GSTEP]);
+        r.grad_score_norm = sqrt(nf[NF_GSCORE]);
+        r.grad_dag_norm = sqrt(nf[NF_GDAG]);
+        r.grad_l1_norm = sqrt(nf[NF_GL1]);
+        r.grad_inc_norm = sqrt(nf[NF_GINC]);
+        r.elapsed = (double)(__builtin_amdgcn_s_memrealtime() - S.t0) * 1e-8;
+        r.reg_trek_value = 0.0;
+        r.grad_trek_norm = 0.0;
+      }
+      S.n_ckpt += 1;
+      S.obj_last = obj;
+      S.score_last = score;
+      S.h_last = h;
+      S.l1_last = l1;
+      if (fabs((S.obj_prev - obj) / S.obj_prev) <= pr->tol) {
+        S.status = ST_DONE;
+        S.early_stop = 1;
+        running = false;
+      } else {
+        S.obj_prev = obj;
+        if (S.iter >= pr->max_iter) {
+          S.status = ST_DONE;
+          running = false;
+        }
+      }
+    }
+    if (running) {
+      if (flags & 2) {
+        S.status = ST_SINGULAR;
+      } else if (flags & 1) {  // sI - W o W left the M-matrix domain (linear.py:230-241)
+        if (S.iter == 0 || pr->s <= 0.9) {
+          S.status = ST_FAILED;
+        } else {
+          S.warm_run = 1;
+          const double lr_old = S.lr;
+          S.lr = lr_old * .5;
+          S.halvings += 1;
+          S.lr_a = lr_old;
+          S.lr_b = S.lr;
+          if (S.lr <= 1e-16) {
+            S.status = ST_LR_UNDERFLOW;
+            act = ACT_REVERT;
+          } else {
+            act = ACT_HALVE;
+          }
+        }
+      } else {
+        const int64_t it = S.iter + 1;
+        S.bc1 = bc1n;
+        S.bc2 = bc2n;
+        S.lr_a = S.lr;
+        act = ACT_STEP;
+        S.iter = it;
+        if (it % pr->checkpoint == 0 || it == pr->max_iter) S.ckpt_pending = 1;
+      }
+    }
+    S.action = act;
+    ctl.act = act;
+    ctl.norms = act == ACT_STEP && S.ckpt_pending;
+    ctl.run = S.status == ST_RUNNING;
+    ctl.lr_a = S.lr_a;
+    ctl.lr_b = S.lr_b;
+    ctl.bc1 = S.bc1;
+    ctl.bc2 = S.bc2;
+}
+
+template <int DS, int NW>
+__global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
+    const Params* __restrict__ pr, State* __restrict__ stg, double* __restrict__ Wg, double* __restrict__ mg,
+    double* __restrict__ vg, const double* __restrict__ covs, const double* __restrict__ minc,
+    const double* __restrict__ mexc, const double* __restrict__ bc_table, CkptRec* __restrict__ ckpt,
+    int64_t ckpt_cap, double* __restrict__ carry, double* __restrict__ pstore, int64_t n_slots) {
+  constexpr int NT = 64 * NW, TPR = DS / 16, TPW = TPR * TPR / NW, E = 4 * TPW;
+  static_assert(TPW * NW == TPR * TPR, "whole tiles per wave");
+  constexpr int SW = DS + 2;                         // W, cov images: 16 rows x 4 cols per read
+  constexpr int SI = ((DS + 15) / 32) * 32 + 16;     // I - W image: B operand rows, = 16 mod 32
+  __shared__ double Wimg[DS * SW];
+  __shared__ double Cimg[DS * SW];
+  __shared__ double IWimg[DS * SI];
+  __shared__ __attribute__((aligned(32))) double rowb[2][DS];
+  __shared__ __attribute__((aligned(32))) double colb[2][DS];
+  __shared__ double piv[DS];
+  // product-form inverse operands, two sets: [m][k] images (PA: the left factor, PR: R as a
+  // left factor) and [k][n] images (PB)
+  __shared__ double PA[2][DS * SW];
+  __shared__ double PR[2][DS * SW];
+  __shared__ double PB[2][DS * SI];
+  __shared__ double nrm[NW];
+  __shared__ double red[3][NW];               // checkpoint objective: (I - W) o Z, |W|, log|pivot|
+  __shared__ double nred[NORM_FIELDS][NW];    // the checkpoint step's norms, per wave
+  __shared__ int flw[NW];
+  __shared__ State S;                         // the controller's (thread 0's) state
+  __shared__ SmallCtl ctl;                    // its decision for the slot, read by every thread
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  int tr[TPW], cols[E], rows[E];
+#pragma unroll
+  for (int u = 0; u < TPW; ++u) {
+    const int tile = w * TPW + u;
+    tr[u] = tile / TPR;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      rows[4 * u + t] = 16 * tr[u] + q + 4 * t;
+      cols[4 * u + t] = 16 * (tile % TPR) + c;
+    }
+  }
+  const int64_t d = pr->d, D = pr->D;
+  const int di = (int)d;
+  const bool has_inc = pr->has_inc != 0, has_exc = pr->has_exc != 0;
+
+  if (tid == 0) {
+    S = *stg;
+    ctl.run = S.status == ST_RUNNING && n_slots > 0;
+    if (S.ckpt_pending)  // the pending checkpoint step's norms, reduced by the last launch
+      for (int f = 0; f < NORM_FIELDS; ++f) {
+        nred[f][0] = carry[f];
+        for (int y = 1; y < NW; ++y) nred[f][y] = f == NF_WMIN ? INFINITY : 0.0;
+      }
+  }
+  bool real[E];
+  double wv[E], mv[E], vv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    real[e] = rows[e] < di && cols[e] < di;
+    const int64_t idx = (int64_t)rows[e] * D + cols[e];
+    wv[e] = real[e] ? Wg[idx] : 0.0;
+    mv[e] = real[e] ? mg[idx] : 0.0;
+    vv[e] = real[e] ? vg[idx] : 0.0;
+  }
+  // MFMA A operand image: (-mu) cov, zero padding
+  for (int e = tid; e < DS * SW; e += NT) {
+    const int r = e / SW, k = e % SW;
+    Cimg[e] = (r < di && k < di) ? covs[(int64_t)r * D + k] : 0.0;
+  }
+  for (int e = tid; e < DS * SW; e += NT) Wimg[e] = 0.0;
+  for (int e = tid; e < DS * SI; e += NT) IWimg[e] = 0.0;
+  __syncthreads();
+  if (!ctl.run) return;
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (real[e]) {
+      Wimg[rows[e] * SW + cols[e]] = wv[e];
+      IWimg[rows[e] * SI + cols[e]] = ((rows[e] == cols[e]) ? 1.0 : 0.0) - wv[e];
+    }
+  const double s_dom = pr->s;
+  // the last two slots' inverses (warm start of the product form) and how many are valid;
+  // kept across launches (pstore, carry[NORM_FIELDS]) so that results do not depend on how
+  // the host batches slots
+  double p1[E], p2[E];
+  const int warm0 = (int)carry[NORM_FIELDS];
+  int warm = warm0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    p1[e] = warm0 > 0 ? pstore[rows[e] * DS + cols[e]] : 0.0;
+    p2[e] = warm0 > 1 ? pstore[DS * DS + rows[e] * DS + cols[e]] : 0.0;
+  }
+  __syncthreads();
+
+  for (int64_t slot = 0; slot < n_slots; ++slot) {
+    // 1 - beta^it for it = iter + 1 from the host table (read early: latency under the inverse)
+    double bc1n = 1.0, bc2n = 1.0;
+    if (tid == 0 && S.iter < pr->ld_table) {
+      bc1n = bc_table[2 * S.iter];
+      bc2n = bc_table[2 * S.iter + 1];
+    }
+
+    // ---- (sI - W o W)^T, identity padding (linear.py:226, 113)
+    double a[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = rows[e], j = cols[e];
+      if (real[e]) {
+        const double wji = Wimg[j * SW + i];
+        a[e] = ((i == j) ? s_dom : 0.0) - wji * wji;
+      } else {
+        a[e] = (i == j) ? 1.0 : 0.0;
+      }
+    }
+    // ---- a <- inv(A^T) = inv(A)^T.  Checkpoint slots (log|det| needs the pivots), the first
+    // slot of a launch and unconverged warm starts: Gauss-Jordan.  Otherwise the product form
+    // inv(S) = X0 (I + R)(I + R^2)[(I + R^4)], R = I - S X0, from the linear extrapolation
+    // X0 = 2 P1 - P2 of the last two inverses (P1 alone after a halving), on the matrix cores
+    // (blockinv.hip's fast path at one-workgroup scale; d ||R||max bounds ||R||inf).
+    bool gj = S.ckpt_pending != 0 || warm == 0;
+    if (!gj) {
+      double x0[E], r[E];
+      double mx = 0.0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = rows[e], j = cols[e];
+        x0[e] = real[e] ? (warm >= 2 ? 2.0 * p1[e] - p2[e] : p1[e]) : ((i == j) ? 1.0 : 0.0);
+        PA[1][i * SW + j] = a[e];
+        PB[1][i * SI + j] = x0[e];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < TPW; ++u) {
+        const dbl4 t4 = tile_mma<DS, SW, SI>(PA[1], PB[1], 16 * tr[u], cols[4 * u] - c, q, c, di,
+                                             dbl4{0.0, 0.0, 0.0, 0.0});
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int e = 4 * u + t;
+          r[e] = real[e] ? (((rows[e] == cols[e]) ? 1.0 : 0.0) - t4[t]) : 0.0;
+          const double ar = fabs(r[e]);
+          mx = ar != ar ? INFINITY : fmax(mx, ar);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        PA[0][rows[e] * SW + cols[e]] = x0[e];
+        PB[0][rows[e] * SI + cols[e]] = r[e];
+        PR[0][rows[e] * SW + cols[e]] = r[e];
+      }
+      mx = wave_max(mx);
+      if (lane == 0) nrm[w] = mx;
+      __syncthreads();
+      double nr = 0.0;
+#pragma unroll
+      for (int x = 0; x < NW; ++x) nr = fmax(nr, nrm[x]);
+      nr *= (double)di;
+      if (nr <= 1e-2) {
+        const bool three = !(nr <= 1e-4);  // ||R||^4 > 1e-16: one more factor
+        double y[E], r2[E];
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+          const int row0 = 16 * tr[u], col0 = cols[4 * u] - c;
+          const dbl4 yv = tile_mma<DS, SW, SI>(PA[0], PB[0], row0, col0, q, c, di,
+                                               dbl4{x0[4 * u], x0[4 * u + 1], x0[4 * u + 2], x0[4 * u + 3]});
+          const dbl4 rv = tile_mma<DS, SW, SI>(PR[0], PB[0], row0, col0, q, c, di, dbl4{0.0, 0.0, 0.0, 0.0});
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int e = 4 * u + t;
+            y[e] = real[e] ? yv[t] : ((rows[e] == cols[e]) ? 1.0 : 0.0);
+            r2[e] = real[e] ? rv[t] : 0.0;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          PA[1][rows[e] * SW + cols[e]] = y[e];
+          PB[1][rows[e] * SI + cols[e]] = r2[e];
+          if (three) PR[1][rows[e] * SW + cols[e]] = r2[e];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+          const int row0 = 16 * tr[u], col0 = cols[4 * u] - c;
+          const dbl4 yv = tile_mma<DS, SW, SI>(PA[1], PB[1], row0, col0, q, c, di,
+                                               dbl4{y[4 * u], y[4 * u + 1], y[4 * u + 2], y[4 * u + 3]});
+          dbl4 rv = dbl4{0.0, 0.0, 0.0, 0.0};
+          if (three) rv = tile_mma<DS, SW, SI>(PR[1], PB[1], row0, col0, q, c, di, rv);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int e = 4 * u + t;
+            y[e] = real[e] ? yv[t] : ((rows[e] == cols[e]) ? 1.0 : 0.0);
+            r2[e] = real[e] ? rv[t] : 0.0;
+          }
+        }
+        if (three) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            PA[0][rows[e] * SW + cols[e]] = y[e];
+            PB[0][rows[e] * SI + cols[e]] = r2[e];
+          }
+          __syncthreads();
+#pragma unroll
+          for (int u = 0; u < TPW; ++u) {
+            const dbl4 yv = tile_mma<DS, SW, SI>(PA[0], PB[0], 16 * tr[u], cols[4 * u] - c, q, c, di,
+                                                 dbl4{y[4 * u], y[4 * u + 1], y[4 * u + 2], y[4 * u + 3]});
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const int e = 4 * u + t;
+              y[e] = real[e] ? yv[t] : ((rows[e] == cols[e]) ? 1.0 : 0.0);
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) a[e] = y[e];
+      } else {
+        gj = true;
+      }
+    }
+    if (gj) {
+      // in-place Gauss-Jordan, no pivoting (the pivots give log|det| on checkpoint slots)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (rows[e] == 0) rowb[0][cols[e]] = a[e];
+        if (cols[e] == 0) colb[0][cpos(rows[e])] = a[e];
+      }
+      __syncthreads();
+      for (int k = 0; k < di; ++k) {
+        const int b = k & 1;
+        const double p = rowb[b][k];
+        const double pinv = 1.0 / p;
+        if (tid == 0) piv[k] = p;
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+          const int j = cols[4 * u];
+          const double rk = rowb[b][j] * pinv;
+          const double4 ck = *reinterpret_cast<const double4*>(&colb[b][16 * tr[u] + 4 * q]);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int e = 4 * u + t;
+            if (!real[e]) continue;
+            const int i = rows[e];
+            const double cki = t == 0 ? ck.x : (t == 1 ? ck.y : (t == 2 ? ck.z : ck.w));
+            if (i == k)
+              a[e] = (j == k) ? pinv : a[e] * pinv;
+            else if (j == k)
+              a[e] = -(a[e] * pinv);
+            else
+              a[e] = a[e] - cki * rk;
+          }
+        }
+        if (k + 1 < di) {
+          const int b1 = b ^ 1;
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            if (rows[e] == k + 1) rowb[b1][cols[e]] = a[e];
+            if (cols[e] == k + 1) colb[b1][cpos(rows[e])] = a[e];
+          }
+        }
+        __syncthreads();
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      p2[e] = p1[e];
+      p1[e] = a[e];
+    }
+    warm = warm < 2 ? warm + 1 : 2;
+
+    // ---- rhs = ((-mu) cov) @ (I - W)  (linear.py:244) on the matrix cores
+    double z[E];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < DS / 4; ++kk)
+        if (4 * kk < di)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Cimg[(16 * tr[u] + c) * SW + 4 * kk + q],
+                                                     IWimg[(4 * kk + q) * SI + cols[4 * u]], acc, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) z[4 * u + t] = acc[t];
+    }
+
+    // ---- domain test (linear.py:226-230) and, when due, the checkpoint objective's sums
+    int fl = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (real[e]) {
+        if (a[e] + 1e-16 < 0.0) fl |= 1;
+        if (!isfinite(a[e])) fl |= 2;
+      }
+    {
+      const unsigned long long b1 = __ballot(fl & 1), b2 = __ballot(fl & 2);
+      if (lane == 0) flw[w] = (b1 ? 1 : 0) | (b2 ? 2 : 0);
+    }
+    if (S.ckpt_pending) {
+      double sd = 0.0, l1 = 0.0;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (real[e]) {
+          sd += (((rows[e] == cols[e]) ? 1.0 : 0.0) - wv[e]) * z[e];
+          l1 += fabs(wv[e]);
+        }
+      const double ld = tid < di ? log(fabs(piv[tid])) : 0.0;
+      sd = wave_sum(sd);
+      l1 = wave_sum(l1);
+      const double lds = wave_sum(ld);
+      if (lane == 0) {
+        red[0][w] = sd;
+        red[1][w] = l1;
+        red[2][w] = lds;
+      }
+    }
+    __syncthreads();
+
+    // ---- control, thread 0 (step.hip control_kernel; linear.py:230-241, 279-331)
+    if (tid == 0) small_control<NW>(pr, S, ctl, red, nred, flw, ckpt, ckpt_cap, bc1n, bc2n);
+    __syncthreads();
+    const int act = ctl.act;
+    if (act == ACT_NOOP) break;  // terminal: nothing of this slot is applied
+    if (act == ACT_HALVE) warm = 1;  // W turns back: the last two inverses do not extrapolate
+    const bool norms = ctl.norms != 0;
+    const double lr_a = ctl.lr_a, lr_b = ctl.lr_b, bc1 = ctl.bc1, bc2 = ctl.bc2;
+
+    // ---- G_obj -> Adam -> update (linear.py:248, 138-163, 275-276), or the line search's
+    // revert / halving with the last step's direction recomputed from m, v (step.hip)
+    double qf[NORM_FIELDS];
+#pragma unroll
+    for (int f = 0; f < NORM_FIELDS; ++f) qf[f] = f == NF_WMIN ? INFINITY : 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (!real[e]) continue;
+      const double wo = wv[e];
+      if (act == ACT_STEP) {
+        const int64_t idx = (int64_t)rows[e] * D + cols[e];
+        const double mt = a[e] + 1e-16;
+        const double gs = pr->zscale * z[e];
+        const double sg = sgn(wo);
+        const double gl1 = pr->mu_l1 * sg;
+        const double gh = (2.0 * wo) * mt;
+        double gobj = gs + gl1;
+        gobj = gobj + gh;
+        double gi = 0.0;
+        if (has_inc) {
+          gi = minc[idx] * sg;
+          gobj = gobj + gi;
+        }
+        const double mm = mv[e] * pr->beta1 + pr->c1 * gobj;
+        const double vx = vv[e] * pr->beta2 + pr->c2 * (gobj * gobj);
+        const double mh = mm / bc1;
+        const double vh = vx / bc2;
+        const double gd = mh / (sqrt(vh) + 1e-8);
+        double wn = wo - lr_a * gd;
+        if (has_exc) wn = wn * mexc[idx];
+        mv[e] = mm;
+        vv[e] = vx;
+        wv[e] = wn;
+        if (norms) {
+          qf[NF_GOBJ] += gobj * gobj;
+          qf[NF_GSCORE] += gs * gs;
+          qf[NF_GDAG] += gh * gh;
+          qf[NF_GL1] += gl1 * gl1;
+          qf[NF_GINC] += gi * gi;
+          qf[NF_GSTEP] += gd * gd;
+          qf[NF_W2] += wn * wn;
+          qf[NF_WMAX] = fmax(qf[NF_WMAX], fabs(wn));
+          if (wn != 0.0) qf[NF_WMIN] = fmin(qf[NF_WMIN], fabs(wn));
+        }
+      } else {
+        const double gd = (mv[e] / bc1) / (sqrt(vv[e] / bc2) + 1e-8);
+        if (act == ACT_HALVE) {
+          const double wn = wo + lr_a * gd;
+          wv[e] = wn - lr_b * gd;
+        } else {
+          wv[e] = wo + lr_a * gd;
+        }
+      }
+      Wimg[rows[e] * SW + cols[e]] = wv[e];
+      IWimg[rows[e] * SI + cols[e]] = ((rows[e] == cols[e]) ? 1.0 : 0.0) - wv[e];
+    }
+    if (norms) {
+#pragma unroll
+      for (int f = 0; f < NORM_FIELDS; ++f) {
+        const double x = f == NF_WMAX ? wave_max(qf[f]) : (f == NF_WMIN ? wave_min(qf[f]) : wave_sum(qf[f]));
+        if (lane == 0) nred[f][w] = x;
+      }
+    }
+    const bool more = ctl.run != 0;
+    __syncthreads();
+    if (!more) break;
+  }
+
+  // write back: the state, this lane's elements, the pending checkpoint step's norms
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (real[e]) {
+      const int64_t idx = (int64_t)rows[e] * D + cols[e];
+      Wg[idx] = wv[e];
+      mg[idx] = mv[e];
+      vg[idx] = vv[e];
+    }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    pstore[rows[e] * DS + cols[e]] = p1[e];
+    pstore[DS * DS + rows[e] * DS + cols[e]] = p2[e];
+  }
+  if (tid == 0) {
+    carry[NORM_FIELDS] = (double)warm;
+    if (S.ckpt_pending)
+      for (int f = 0; f < NORM_FIELDS; ++f) {
+        double x = f == NF_WMIN ? INFINITY : 0.0;
+#pragma unroll 1
+        for (int y = 0; y < NW; ++y)
+          x = f == NF_WMAX ? fmax(x, nred[f][y]) : (f == NF_WMIN ? fmin(x, nred[f][y]) : x + nred[f][y]);
+        carry[f] = x;
+      }
+    *stg = S;
+  }
+}
+
+}  // namespace
+
+// d <= 32 (the operand images of the product form outgrow the LDS at DS = 64, and the
+// Gauss-Jordan-only kernel measured slower than the graph-replayed slots for 32 < d <= 64)
+int small_block(int64_t d) { return d <= 16 ? 16 : (d <= 32 ? 32 : 0); }
+
+void launch_small_minimize(const Params* pr, State* st, double* W, double* m, double* v, const double* covs,
+                           const double* minc, const double* mexc, const double* bc_table, CkptRec* ckpt,
+                           int64_t ckpt_cap, double* carry, double* pstore, int64_t d, int64_t n_slots,
+                           hipStream_t stream) {
+  const int ds = small_block(d);
+  if (ds == 0) throw std::invalid_argument("small_minimize: d > 32");
+#define MIDAGMA_SMALL(DS_, NW_)                                                                                  \
+  hipLaunchKernelGGL((small_minimize_kernel<DS_, NW_>), dim3(1), dim3(64 * NW_), 0, stream, pr, st, W, m, v, covs, \
+                     minc, mexc, bc_table, ckpt, ckpt_cap, carry, pstore, n_slots)
+  // one wave per 16 x 16 tile
+  if (ds == 16)
+    MIDAGMA_SMALL(16, 1);
+  else
+    MIDAGMA_SMALL(32, 4);
+#undef MIDAGMA_SMALL
+  HIP_TRY(hipGetLastError());
+}
+
+}  // namespace midagma

@@ -69,6 +69,12 @@ struct midagma_solver {
   bool cov_at = getenv("MIDAGMA_EXP_COV_AMODE0") == nullptr;  // experiment knob
   bool cov_iw = getenv("MIDAGMA_EXP_COV_IW") != nullptr;      // experiment knob
   DevBuf npart;  // checkpoint-step norm partials (fused_update -> control)
+  // cov mode, l2, d <= 64, no trek regularizer: the one-workgroup persistent loop (small.hip)
+  DevBuf scarry, sprev;  // between two small-loop launches: pending norms + warm count, last inverses
+  bool use_small = getenv("MIDAGMA_EXP_NO_SMALL") == nullptr;  // experiment knob
+  bool small_on() const {
+    return use_small && mode == MIDAGMA_MODE_COV && loss == MIDAGMA_LOSS_L2 && !trek_on && small_block(d) > 0;
+  }
   // PST trek regularizer (trek.hip)
   TrekCfg tcfg{};
   bool trek_on = false;
@@ -132,7 +138,7 @@ struct midagma_solver {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
-                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW})
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW, &scarry, &sprev})
       b->release();
     for (DevBuf& b : tbufs) b.release();
     for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices, &cA, &cMi, &cS, &cvec, &cpart, &cP, &cR, &cC}) b->release();
@@ -468,6 +474,9 @@ struct midagma_solver {
     partials.alloc(2 * NRED);
     npart.alloc((size_t)((d + NTHREADS - 1) / NTHREADS) * d * NORM_FIELDS);
     HIP_TRY(hipMemsetAsync(npart.p, 0, npart.n * sizeof(double), stream));
+    scarry.alloc(NORM_FIELDS + 1);
+    HIP_TRY(hipMemsetAsync(scarry.p, 0, scarry.n * sizeof(double), stream));
+    if (small_block(d) > 0) sprev.alloc(2 * 32 * 32);
     if (D % 128 == 0) {
       // split-K of the cov score GEMM: small grids get slices to fill the chip; large ones the
       // split that best rounds the last wave of 128-tiles (2 workgroups per CU resident:
@@ -609,6 +618,7 @@ struct midagma_solver {
     upload_matrix(W, Wh, d);
     const size_t DD = (size_t)D * D;
     for (DevBuf* b : {&m, &v}) HIP_TRY(hipMemsetAsync(b->p, 0, DD * sizeof(double), stream));
+    HIP_TRY(hipMemsetAsync(scarry.p, 0, scarry.n * sizeof(double), stream));  // no warm start yet
     HIP_TRY(hipStreamSynchronize(stream));  // h_state[0] reused as a snapshot slot below
     fast_ready = false;  // the first slot of a call runs the GJ path (warm starts are stale)
     three_pass_left = 0;
@@ -681,9 +691,36 @@ struct midagma_solver {
   int fast_group = getenv("MIDAGMA_EXP_FAST_GROUP") ? std::max(1, atoi(getenv("MIDAGMA_EXP_FAST_GROUP"))) : 4;
   int64_t fast_batch = 64;
 
+  // Small d: the whole inner loop in one persistent workgroup, kSmallBatch slots per launch
+  // (one host sync per launch).  n_slots < 0: until terminal.
+  static constexpr int64_t kSmallBatch = 4096;
+  void drive_small(int64_t n_slots) {
+    const int64_t max_iter = hp.max_iter, checkpoint = std::max<int64_t>(hp.checkpoint, 1);
+    const int64_t cap = max_iter + max_iter / checkpoint + 512;
+    int64_t launched = 0;
+    for (;;) {
+      const int64_t B = std::min<int64_t>(kSmallBatch, (n_slots < 0 ? cap : n_slots) - launched);
+      if (B <= 0) {
+        if (n_slots < 0) throw std::runtime_error("minimize: slot budget exceeded (controller stuck)");
+        break;
+      }
+      launch_small_minimize(d_params, d_state, W.p, m.p, v.p, covs.p, has_inc ? minc.p : nullptr,
+                            has_exc ? mexc.p : nullptr, bc_table.p, d_ckpt, ckpt_cap, scarry.p, sprev.p, d, B,
+                            stream);
+      launched += B;
+      HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (terminal(h_state[1])) break;
+    }
+  }
+
   void run_loop(int64_t max_iter, int64_t checkpoint) {
     if (blocked()) {
       drive_blocked(-1);
+      return;
+    }
+    if (small_on()) {
+      drive_small(-1);
       return;
     }
     ensure_graphs();
@@ -1010,6 +1047,10 @@ int midagma_run_slots(midagma_solver* s, int64_t n) {
   return guarded(s, [&] {
     if (s->blocked()) {
       s->drive_blocked(n);
+      return MIDAGMA_OK;
+    }
+    if (s->small_on()) {
+      s->drive_small(n);
       return MIDAGMA_OK;
     }
     for (int64_t i = 0; i < n; ++i) HIP_TRY(hipGraphLaunch(s->g_full, s->stream));

@@ -169,6 +169,15 @@ def gen_traj(X, tag, Ks, lr=3e-4, mu=1.0, s=1.0, loss="l2", lambda1=0.03):
     np.savez_compressed(os.path.join(HERE, f"traj_{tag}.npz"), **out)
 
 
+def gen_traj_logistic_d100():
+    """Logistic at d=100 (D=128: the 128-tile pipelined GEMM with the sigmoid epilogue on the
+    GPU side).  Binary X from the logistic SEM (seed 9, n=3000); the reference's minimize at
+    K = 1, 10, 100, 500 and the same run with 1e-16 noise in every inverse (the envelope)."""
+    Xl, _, _ = make_dataset(100, 3000, seed=9, sem_type="logistic")
+    np.savez_compressed(os.path.join(HERE, "data_logistic_d100.npz"), X=Xl)
+    gen_traj(Xl, "logistic_d100", [1, 10, 100, 500], loss="logistic", lambda1=0.05)
+
+
 def gen_branches(X):
     out = {}
     d = X.shape[1]
@@ -403,6 +412,6 @@ if __name__ == "__main__":
             X20 = np.load(os.path.join(HERE, "data_d20_n1000_seed0.npz"))["X"]
             for name in sys.argv[1:]:
                 fn = globals()[name]
-                fn(X20) if name in ("gen_tcc", "gen_mlp_traj") else fn()
+                fn(X20) if name in ("gen_tcc", "gen_mlp_traj") else fn()  # e.g. gen_traj_logistic_d100
     else:
         main()

@@ -1,0 +1,155 @@
+"""The one-workgroup small-d inner loop (csrc/small.hip: cov mode, l2, d <= 32) against the
+oracle (the numpy/scipy restatement of linear.py:165-333), against the graph-replayed slot
+path it replaces (MIDAGMA_EXP_NO_SMALL), and across launch boundaries (run_slots chunks that
+end right after a checkpoint step, so the pending checkpoint norms cross launches)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from midagma_amd.simulate import make_dataset  # noqa: E402
+from oracle.dagma_oracle import LinearOracle  # noqa: E402
+
+REC_FIELDS = ("obj", "score", "h", "lr", "w_norm", "max_abs_w", "min_abs_w_nonzero", "grad_raw_norm",
+              "grad_step_norm", "grad_score_norm", "grad_dag_norm", "grad_l1_norm", "grad_inc_norm")
+ORACLE_KEYS = dict(obj="obj_total", score="score_datafit", h="reg_dag_value")
+
+
+def _oracle(d, n=None, seed=11, exc=None, inc=None):
+    X, _, _ = make_dataset(d, n or max(200, 10 * d), seed=seed)
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 50, exc, inc)
+    return o
+
+
+def _solver(d, cov, masks=None):
+    from midagma_amd.solver import HipSolver
+    s = HipSolver(d, "l2", "cov", device=0)
+    s.set_cov(cov)
+    if masks is not None:
+        s.set_masks(*masks)
+    return s
+
+
+def _check_records(res, tr):
+    assert [c.iter for c in res.checkpoints] == [r["iter"] for r in tr.records]
+    for c, r in zip(res.checkpoints, tr.records):
+        for f in REC_FIELDS:
+            want = r[ORACLE_KEYS.get(f, f)]
+            got = getattr(c, f)
+            assert abs(got - want) <= 1e-9 * max(1.0, abs(want)), (c.iter, f, got, want)
+
+
+@pytest.mark.parametrize("d", [1, 4, 16, 17, 20, 31, 32, 33])
+def test_small_path_matches_oracle(d):
+    o = _oracle(d)
+    K = 300
+    s = _solver(d, o.cov)
+    W = np.zeros((d, d))
+    res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=50, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert res.success and res.iters == tr.iters == K and res.slots == K + 1  # + the last objective
+    assert np.abs(W - Wr).max() <= 1e-9
+    _check_records(res, tr)
+    s.close()
+
+
+def test_small_path_masks_and_early_stop():
+    d = 20
+    exc = ((0, 1), (3, 2), (5, 7))
+    inc = ((1, 0), (4, 9))
+    o = _oracle(d, exc=exc, inc=inc)
+    mi, me = o.masks(1.0)
+    s = _solver(d, o.cov, masks=(mi, me))
+    W = np.zeros((d, d))
+    # tol 1e-6: the checkpoint tolerance stops the loop (linear.py:328-331)
+    res = s.minimize(W, 1.0, 20000, 1.0, 3e-4, tol=1e-6, lambda1=0.03, checkpoint=50, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, 20000, 1.0, 3e-4, tol=1e-6)
+    assert tr.early_stop and res.early_stop and res.iters == tr.iters
+    assert np.abs(W - Wr).max() <= 1e-9
+    assert W[0, 1] == W[3, 2] == W[5, 7] == 0.0
+    _check_records(res, tr)
+    s.close()
+
+
+def test_small_path_line_search_branches(golden):
+    """lr halving at s = 1 and the out-of-domain failure at s <= 0.9 (linear.py:230-241), on
+    the reference's own fixture (branches.npz)."""
+    b = golden("branches.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    o = LinearOracle("l2")
+    o.prepare(X, 0.03, 1000)
+    for s_dom, key in ((1.0, "halve"), (0.9, "ood")):
+        s = _solver(20, o.cov)
+        W = np.zeros((20, 20))
+        res = s.minimize(W, 1.0, 60, s_dom, 0.3, tol=-1.0, lambda1=0.03)
+        assert res.success == bool(b[f"{key}_ok"])
+        assert np.abs(W - b[f"{key}_W"]).max() <= 1e-9
+        if key == "halve":
+            assert res.halvings == int(b["halve_nhalvings"])
+        s.close()
+
+
+@pytest.mark.parametrize("d", [20, 32])
+def test_small_path_launch_boundaries_bit_identical(d):
+    """run_slots in chunks of 50 with checkpoint = 50: every launch ends right after a
+    checkpoint step, so the step's norms cross to the next launch.  Same kernel arithmetic:
+    W and every checkpoint record field are bit-identical to one minimize call."""
+    o = _oracle(d)
+    K = 400
+    a = _solver(d, o.cov)
+    Wa = np.zeros((d, d))
+    ra = a.minimize(Wa, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=50, want_checkpoints=True)
+    b = _solver(d, o.cov)
+    b.begin(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=50)
+    for _ in range(K // 50 + 2):
+        b.run_slots(50)
+    Wb = np.zeros((d, d))
+    rb = b.end(Wb)
+    cb = b.checkpoints()
+    assert rb.iters == ra.iters == K
+    assert np.array_equal(Wa, Wb)
+    assert len(cb) == len(ra.checkpoints)
+    for x, y in zip(ra.checkpoints, cb):
+        for f in REC_FIELDS:
+            assert getattr(x, f) == getattr(y, f), (x.iter, f)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("d", [5, 20, 32])
+def test_small_path_vs_graph_path(d, monkeypatch):
+    """The persistent kernel and the graph-replayed slots (MIDAGMA_EXP_NO_SMALL) agree to
+    rounding: same iterations, W within 1e-11 after 500 steps (checkpoint every 100: Gauss-Jordan
+    slots between runs of product-form slots)."""
+    o = _oracle(d)
+    K = 500
+    a = _solver(d, o.cov)
+    Wa = np.zeros((d, d))
+    ra = a.minimize(Wa, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100)
+    monkeypatch.setenv("MIDAGMA_EXP_NO_SMALL", "1")
+    b = _solver(d, o.cov)
+    monkeypatch.delenv("MIDAGMA_EXP_NO_SMALL")
+    Wb = np.zeros((d, d))
+    rb = b.minimize(Wb, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100)
+    assert ra.iters == rb.iters == K and ra.slots == rb.slots
+    assert np.abs(Wa - Wb).max() <= 1e-11
+    a.close()
+    b.close()
+
+
+def test_small_path_long_trajectory_d20(golden):
+    """10000 steps at d=20 against the reference's own trajectory (traj_d20.npz): ~9990
+    product-form slots between the Gauss-Jordan checkpoint slots."""
+    t = golden("traj_d20.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    o = LinearOracle("l2")
+    o.prepare(X, 0.03, 1000)
+    s = _solver(20, o.cov)
+    W = np.zeros((20, 20))
+    res = s.minimize(W, 1.0, 10000, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
+    assert res.iters == 10000
+    assert np.abs(W - t["W_K10000"]).max() <= max(1e-9, 2 * float(t["env_K10000"]))
+    s.close()

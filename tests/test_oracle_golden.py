@@ -62,7 +62,8 @@ def test_adam_matches_reference(golden):
 
 @pytest.mark.parametrize("tag,K", [("d20", 1), ("d20", 10), ("d20", 100), ("d20", 1000),
                                    ("d20", 10000), ("d100", 1), ("d100", 10), ("d100", 100),
-                                   ("d100", 1000), ("logistic_d20", 100), ("logistic_d20", 1000)])
+                                   ("d100", 1000), ("logistic_d20", 100), ("logistic_d20", 1000),
+                                   ("logistic_d100", 10), ("logistic_d100", 500)])
 def test_minimize_trajectory_bit_exact(golden, tag, K):
     t = golden(f"traj_{tag}.npz")
     if tag == "d20":
@@ -70,6 +71,8 @@ def test_minimize_trajectory_bit_exact(golden, tag, K):
     elif tag == "d100":
         from midagma_amd.simulate import make_dataset
         X, loss, l1 = make_dataset(100, 2000, seed=1)[0], "l2", 0.03
+    elif tag == "logistic_d100":
+        X, loss, l1 = golden("data_logistic_d100.npz")["X"].copy(), "logistic", 0.05
     else:
         X, loss, l1 = golden("data_meta.npz")["logit_X"].copy(), "logistic", 0.05
     o = _oracle(X, loss, l1)

@@ -90,7 +90,10 @@ def fit_case(d, n):
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "small"):
-        cov_case(20, 1000, 50, 2000)
+        cov_case(20, 1000, 50, 20000)
+        for d in (10, 32, 48, 64):
+            cov_case(d, 1000, 50, 10000)
+        cov_case(65, 1000, 50, 5000)
         cov_case(200, 2000, 20, 500)
     if which in ("all", "d1000"):
         cov_case(1000, 2000, 10, 2000)
