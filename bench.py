@@ -58,6 +58,7 @@ def parse():
     p.add_argument("--no-data", action="store_true", help="skip the data-mode leg (profiling the other legs)")
     p.add_argument("--no-large", action="store_true", help="skip the config 3 leg (d=5000, n=5e4, cov mode)")
     p.add_argument("--no-mlp", action="store_true", help="skip the config 5 leg (DagmaNonlinear, dims [200,10,1])")
+    p.add_argument("--no-small", action="store_true", help="skip the config 1 leg (d=20, one persistent workgroup)")
     p.add_argument("--mlp-steps", type=int, default=300)
     p.add_argument("--large-d", type=int, default=5000)
     p.add_argument("--large-n", type=int, default=50_000)
@@ -338,6 +339,62 @@ def bench_logistic(args, device, n, steps):
                               "algorithmic": f"2*n*d^2 = {flops:.3e} flop + n*d sigmoids"})
 
 
+def bench_small(args, device, with_cpu):
+    """Config 1 (BASELINE): d=20, n=1000, l2, cov mode -- the one-workgroup persistent kernel
+    (csrc/small.hip).  Steps/s over a 20000-step window (stage 1: mu=1, s=1, lr=3e-4, tol=-1)
+    and the default fit() wall-clock; the CPU oracle (the reference's algorithm, bit-exact to
+    it at 1 BLAS thread) timed beside it on the same host."""
+    from midagma_amd import DagmaLinear
+    from midagma_amd.simulate import count_accuracy, make_dataset
+    from midagma_amd.solver import HipSolver
+    d, n, K = 20, 1000, 20000
+    X, W_true, B_true = make_dataset(d, n, seed=args.seed)
+    Xc = X - X.mean(0, keepdims=True)
+    cov = Xc.T @ Xc / float(n)
+    s = HipSolver(d, "l2", "cov", device=device)
+    s.set_cov(cov)
+    s.begin(np.zeros((d, d)), 1.0, K + 100, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
+    s.run_slots(20)
+    s.sync()
+    t0 = time.perf_counter()
+    s.run_slots(K)
+    s.sync()
+    t1 = time.perf_counter()
+    r = s.poll()
+    s.close()
+    DagmaLinear("l2", device=device).fit(X.copy(), lambda1=0.03)   # warm: code objects
+    m = DagmaLinear("l2", device=device)
+    f0 = time.perf_counter()
+    W = m.fit(X.copy(), lambda1=0.03)
+    wall = time.perf_counter() - f0
+    iters = [e["iters"] for e in m.minimize_log]
+    out = dict(value=K / (t1 - t0), unit="steps/s", ms_per_step=(t1 - t0) / K * 1e3, steps=K,
+               verified=(r.status == 0 and r.iters == K + 20),
+               workload="config1: d=20, n=1000, l2, cov mode, 1 GPU (one persistent workgroup, csrc/small.hip)",
+               fit={"wall_s": wall, "total_iters": int(sum(iters)), "stage_iters": iters,
+                    "accuracy": count_accuracy(B_true, W != 0)},
+               reference_survey={"steps_per_s": 16430, "fit_wall_s": 3.13,
+                                 "source": "BASELINE.md survey probe (the reference itself, 8-vCPU survey host)"})
+    if with_cpu:
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "cov.npy")
+            np.save(path, cov)
+            t = _cpu_runs("cov", d, path, [1, 4], steps=2000)
+        if t:
+            th, v = _best(t)
+            out["cpu_baseline"] = dict(value=v, unit="steps/s", cores=th, kind="port",
+                                       sweep={str(k): 1.0 / x for k, x in sorted(t.items())},
+                                       sample="oracle cov-mode Adam steps at d=20: 2000 steps per thread count, "
+                                              "threads [1, 4], best shown")
+            out["vs_cpu"] = out["value"] / v
+        tf = _cpu_runs("fit", d, n, [1], steps=1, timeout=300)
+        if tf:
+            out["fit"]["cpu_fit_wall_s"] = tf[1]
+            out["fit"]["vs_cpu"] = tf[1] / wall
+    return out
+
+
 def bench_cov_large(args, device):
     """Config 3: d=5000, n=5e4, l2, cov mode on one GPU -- the inverse-dominated
     size.  X is generated and reduced to cov = X^T X / n on the GPU (torch plumbing: a CPU
@@ -397,6 +454,20 @@ def gauss(n, d, seed):
     return X
 
 
+if mode == "fit":                       # config 1: the whole default fit() (linear.py:335-462)
+    from midagma_amd.simulate import make_dataset
+    X, _, _ = make_dataset(d, int(extra), seed=0)
+    out = {}
+    for th in threads:
+        with threadpool_limits(limits=th):
+            o = LinearOracle("l2")
+            t0 = time.perf_counter()
+            o.fit(X.copy(), lambda1=0.03)
+            out[th] = time.perf_counter() - t0
+            out_it = sum(st[4].iters for st in o.stages)
+        print(json.dumps({"partial": out}), flush=True)
+    print(json.dumps({"t": out, "iters": out_it}), flush=True)
+    sys.exit(0)
 if mode == "cov":                       # the reference algorithm: cov precomputed once
     o = LinearOracle("l2")
     o.cov, o.X, o.n = np.load(extra), None, 10000
@@ -591,6 +662,9 @@ def main():
     mlp_res = None
     if rank == 0 and world == 1 and not args.no_mlp and args.workload == "data":
         mlp_res = bench_mlp(args, local, with_cpu=not args.no_cpu)
+    small_res = None
+    if rank == 0 and world == 1 and not args.no_small and args.workload == "data":
+        small_res = bench_small(args, local, with_cpu=not args.no_cpu)
     logi = None
     if rank == 0 and world == 1 and not args.no_logistic and args.workload == "data":
         logi = [bench_logistic(args, local, nn, args.logistic_steps if nn > 100_000 else 200)
@@ -611,7 +685,8 @@ def main():
                 logi[0]["vs_cpu"] = logi[0]["value"] / v
     if rank == 0 and res is None and cov_res is None:   # --no-data --no-cov: a profiling run of the other legs
         out = {k: v for k, v in (large_res or {}).items() if k != "cov"}
-        print(json.dumps({"config3": out, "full_fit": fit_res, "config5": mlp_res}), flush=True)
+        print(json.dumps({"config3": out, "full_fit": fit_res, "config5": mlp_res, "config1": small_res,
+                          "logistic": logi}), flush=True)
         return
     if rank == 0:
         d = args.d
@@ -703,6 +778,8 @@ def main():
             line["config5"] = mlp_res
         if logi:
             line["logistic"] = logi
+        if small_res is not None:
+            line["config1"] = small_res
         if fit_res is not None:
             fr = dict(fit_res)
             fr["workload"] = f"config2: DagmaLinear('l2').fit(X) defaults, d={d}, n={args.cov_n}, 1 GPU (cov mode)"

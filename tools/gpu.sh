@@ -8,7 +8,7 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench [BENCH ARGS]    python bench.py -> gpurun_out/bench.json (+ .err)
 #   prof LEG              rocprofv3 --kernel-trace --stats of one bench leg -> gpurun_out/prof_LEG/
-#                         LEG: data | cov | large | small | logistic | mlp
+#                         LEG: data | cov | large | small | logistic | mlp (one bench leg each)
 #   pmc LEG               FETCH_SIZE and WRITE_SIZE passes (each its own run) of one leg,
 #                         summarised per kernel -> gpurun_out/pmc_LEG.json (tools/pmc_summary.py)
 #   probe NAME [ARGS]     python tools/NAME.py ARGS (probe_perf, peak_probe, blocked_debug, ...)
@@ -19,12 +19,14 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 
 leg_args() {
+  local skip="--no-cpu --no-fit --no-cov --no-large --no-mlp --no-logistic --no-small"
   case "$1" in
-    data)     echo "--steps 5 --warmup 1 --no-cpu --no-cov --no-fit --no-large --no-mlp --no-logistic" ;;
+    data)     echo "--steps 5 --warmup 1 ${skip}" ;;
     cov)      echo "--workload cov --cov-steps 2000 --no-cpu --no-fit --no-large" ;;
-    large)    echo "--no-data --no-cov --no-fit --no-cpu --no-mlp --no-logistic --large-steps 200" ;;
-    mlp)      echo "--no-data --no-cov --no-fit --no-cpu --no-large --no-logistic" ;;
-    logistic) echo "--no-data --no-cov --no-fit --no-cpu --no-large --no-mlp" ;;
+    large)    echo "--no-data ${skip/--no-large/} --large-steps 200" ;;
+    mlp)      echo "--no-data ${skip/--no-mlp/}" ;;
+    logistic) echo "--no-data ${skip/--no-logistic/}" ;;
+    small)    echo "--no-data ${skip/--no-small/}" ;;
     *) return 1 ;;
   esac
 }
@@ -45,13 +47,13 @@ run_task() {
       echo "bench rc=$rc"; cat gpurun_out/bench.json; grep -v amdgpu.ids gpurun_out/bench.err | tail -8; return $rc ;;
     prof)
       local leg=$1 a
-      if [ "$leg" = small ]; then a="$R/tools/probe_perf.py small"; else a="$R/bench.py $(leg_args "$leg")" || return 2; fi
+      a="$R/bench.py $(leg_args "$leg")" || return 2
       (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$leg" -o "$leg" \
         --output-format csv -- python3 $a > "$R/gpurun_out/prof_$leg.log" 2>&1); local rc=$?
       echo "prof $leg rc=$rc"; return $rc ;;
     pmc)
       local leg=$1 a c
-      if [ "$leg" = small ]; then a="$R/tools/probe_perf.py small"; else a="$R/bench.py $(leg_args "$leg") --profile-reps 1" || return 2; fi
+      a="$R/bench.py $(leg_args "$leg") --profile-reps 1" || return 2
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && timeout -s KILL 600 rocprofv3 --pmc $c --kernel-trace -d "$R/gpurun_out/pmc_${leg}_$c" -o p \
           --output-format csv -- python3 $a > "$R/gpurun_out/pmc_${leg}_$c.log" 2>&1) || { echo "pmc $leg $c failed"; return 1; }
