@@ -250,37 +250,75 @@ __global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restr
   store_row_partial(abs_or_inf(qq), part_next, m0, n0, nt);
 }
 
-// acc += A[0:32, 0:K] B[0:K, 0:32] (global operands), 32-deep chunks through double-
-// buffered LDS images with a register prefetch of the next chunk; one barrier per chunk.
-__device__ __forceinline__ void tile32_gemm(const double* __restrict__ A, int64_t lda,
-                                            const double* __restrict__ B, int64_t ldb, int K, dbl4& acc,
-                                            double* As0, double* As1, double* Bs0, double* Bs1) {
+// acc += A[0:32, 0:K] B[0:K, 0:32] (global operands, K <= 256), 32-deep chunks through double-
+// buffered LDS images; the register loads run PF chunks ahead of the MFMAs (the operands were
+// written by the previous launch on other XCDs: each chunk is a MALL round trip).  One barrier
+// per chunk.
+template <int PF, int NK>
+__device__ __forceinline__ void tile32_gemm_pf(const double* __restrict__ A, int64_t lda,
+                                               const double* __restrict__ B, int64_t ldb, dbl4& acc,
+                                               double* As0, double* As1, double* Bs0, double* Bs1) {
   const int tid = threadIdx.x;
   const int r0 = tid >> 4, c0 = (tid & 15) * 2;  // items tid and tid + 256: rows r0, r0 + 16
-  double2 a0, a1, b0, b1;
-#define T32_LOAD(kc)                                                                       \
+  double2 a0[PF], a1[PF], b0[PF], b1[PF];
+  constexpr int nk = NK;
+#define T32_LOAD(slot, kc)                                                                 \
   do {                                                                                     \
     const double* ap = A + (int64_t)r0 * lda + (kc) * 32 + c0;                             \
     const double* bp = B + ((int64_t)(kc) * 32 + r0) * ldb + c0;                           \
-    a0 = *reinterpret_cast<const double2*>(ap);                                            \
-    a1 = *reinterpret_cast<const double2*>(ap + 16 * lda);                                 \
-    b0 = *reinterpret_cast<const double2*>(bp);                                            \
-    b1 = *reinterpret_cast<const double2*>(bp + 16 * ldb);                                 \
+    a0[slot] = *reinterpret_cast<const double2*>(ap);                                      \
+    a1[slot] = *reinterpret_cast<const double2*>(ap + 16 * lda);                           \
+    b0[slot] = *reinterpret_cast<const double2*>(bp);                                      \
+    b1[slot] = *reinterpret_cast<const double2*>(bp + 16 * ldb);                           \
   } while (0)
-  T32_LOAD(0);
-  const int nk = K / 32;
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (p < nk) T32_LOAD(p, p);
+  // slot 0 holds chunk kc; the queue shifts by one each chunk (constant register indices:
+  // the loop need not be unrolled for the arrays to stay in registers)
   for (int kc = 0; kc < nk; ++kc) {
     double* As = (kc & 1) ? As1 : As0;
     double* Bs = (kc & 1) ? Bs1 : Bs0;
-    *reinterpret_cast<double2*>(As + r0 * ST + c0) = a0;
-    *reinterpret_cast<double2*>(As + (r0 + 16) * ST + c0) = a1;
-    *reinterpret_cast<double2*>(Bs + r0 * ST + c0) = b0;
-    *reinterpret_cast<double2*>(Bs + (r0 + 16) * ST + c0) = b1;
+    *reinterpret_cast<double2*>(As + r0 * ST + c0) = a0[0];
+    *reinterpret_cast<double2*>(As + (r0 + 16) * ST + c0) = a1[0];
+    *reinterpret_cast<double2*>(Bs + r0 * ST + c0) = b0[0];
+    *reinterpret_cast<double2*>(Bs + (r0 + 16) * ST + c0) = b1[0];
     __syncthreads();
-    if (kc + 1 < nk) T32_LOAD(kc + 1);
+#pragma unroll
+    for (int p = 0; p + 1 < PF; ++p) {
+      a0[p] = a0[p + 1];
+      a1[p] = a1[p + 1];
+      b0[p] = b0[p + 1];
+      b1[p] = b1[p + 1];
+    }
+    if (kc + PF < nk) T32_LOAD(PF - 1, kc + PF);
     mma32(As, Bs, acc);
   }
 #undef T32_LOAD
+}
+
+// prefetch depth of the panel / trailing tiles (experiment knob MIDAGMA_EXP_T32_PF: 1, 2, 3;
+// d=1000 fast slot: 4160 steps/s at 1, 4340 at 3, two runs each)
+static int t32_pf() {
+  static const int pf = getenv("MIDAGMA_EXP_T32_PF") ? atoi(getenv("MIDAGMA_EXP_T32_PF")) : 3;
+  return pf < 1 ? 1 : (pf > 3 ? 3 : pf);
+}
+
+__device__ __forceinline__ void tile32_gemm_any(int pf, const double* __restrict__ A, int64_t lda,
+                                                const double* __restrict__ B, int64_t ldb, int K, dbl4& acc,
+                                                double* As0, double* As1, double* Bs0, double* Bs1) {
+  if (K == 128) {
+    if (pf >= 2)
+      tile32_gemm_pf<2, 4>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
+    else
+      tile32_gemm_pf<1, 4>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
+  } else if (pf == 3) {
+    tile32_gemm_pf<3, 8>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
+  } else if (pf == 2) {
+    tile32_gemm_pf<2, 8>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
+  } else {
+    tile32_gemm_pf<1, 8>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
+  }
 }
 
 // Panels of outer step g (one 32 x 32 tile per workgroup):
@@ -293,7 +331,7 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
                                                               const double* __restrict__ P, int64_t ldp,
                                                               double* __restrict__ Pe, double* __restrict__ Po,
                                                               const int* __restrict__ done, int check,
-                                                              State* __restrict__ st) {
+                                                              State* __restrict__ st, int pf) {
   if (st && st->status != ST_RUNNING) return;
   if (done && *done == 0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
@@ -307,8 +345,8 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   if (job < nu) {
     const int a = job / mb, cq = job % mb, c = cq < g0 ? cq : cq + gb;
-    tile32_gemm(P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, img[0], img[1],
-                img[2], img[3]);
+    tile32_gemm_any(pf, P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, img[0], img[1],
+                    img[2], img[3]);
     double* out = Aout + (G0 + (int64_t)a * NB) * D + (int64_t)c * NB;
     int flag = 0;
     acc_foreach(acc, [&](int row, int col, double& v) {
@@ -318,8 +356,8 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
     if (check && flag) atomicOr(&st->flags, flag);
   } else if (job < 2 * nu) {
     const int j2 = job - nu, iq = j2 / gb, c = j2 % gb, i = iq < g0 ? iq : iq + gb;
-    tile32_gemm(Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, img[0], img[1], img[2],
-                img[3]);
+    tile32_gemm_any(pf, Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, img[0], img[1],
+                    img[2], img[3]);
     double* out = Aout + (int64_t)i * NB * D + G0 + (int64_t)c * NB;
     int flag = 0;
     acc_foreach(acc, [&](int row, int col, double& v) {
@@ -350,7 +388,7 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
 // outside G (Aout[G, j] = P Ain[G, j] from the panel launch).
 __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __restrict__ Ain,
                                                               double* __restrict__ Aout, int64_t D, int B2, int g,
-                                                              int check, State* __restrict__ st) {
+                                                              int check, State* __restrict__ st, int pf) {
   if (st && st->status != ST_RUNNING) return;
   __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
   const int nb = (int)(D / NB), gb = B2 / NB, g0 = g * gb, mb = nb - gb;
@@ -362,8 +400,8 @@ __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __re
   dbl4 c_old;
   acc_foreach(c_old, [&](int row, int col, double& v) { v = Ci[(int64_t)row * D + col]; });
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  tile32_gemm(Ain + (int64_t)i * NB * D + G0, D, Aout + G0 * D + (int64_t)j * NB, D, B2, acc, img[0], img[1],
-              img[2], img[3]);
+  tile32_gemm_any(pf, Ain + (int64_t)i * NB * D + G0, D, Aout + G0 * D + (int64_t)j * NB, D, B2, acc, img[0],
+                  img[1], img[2], img[3]);
   double* out = Aout + (int64_t)i * NB * D + (int64_t)j * NB;
   const int lane = threadIdx.x & 63, m0 = q_m0(), n0 = q_n0();
   int flag = 0;
@@ -448,14 +486,14 @@ void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     // the fast slot takes the domain flags from the last outer step's outputs (no reduce_check)
     const int check = fast && g == K2 - 1;
     hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2,
-                       g, P, ldp, Pe, Po, done, check, st);
+                       g, P, ldp, Pe, Po, done, check, st, t32_pf());
     if (mb > 0) {
       // large D: 128 x 128 tiles (operand reuse; enough tiles to fill the chip), else 32 x 32
       if (D - B2 >= TRAIL128_MIN)
         launch_trail128(Ain, Aout, D, B2, g, check, st, stream);
       else
         hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2, g, check,
-                           st);
+                           st, t32_pf());
     }
   }
   HIP_TRY(hipGetLastError());

@@ -97,6 +97,8 @@ if __name__ == "__main__":
         cov_case(200, 2000, 20, 500)
     if which in ("all", "d1000"):
         cov_case(1000, 2000, 10, 2000)
+    if which == "d1000short":  # PMC passes: few dispatches
+        cov_case(1000, 2000, 10, 40)
     if which == "fit":
         fit_case(1000, 10000)
     if which == "fit20":
