@@ -25,7 +25,7 @@
 #include <cstdlib>
 
 #include "launch.h"
-#include "tile32.h"
+#include "nm16.h"
 
 namespace midagma {
 
@@ -38,116 +38,30 @@ __device__ __forceinline__ int xcd_spread(int w, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
 }
 
-// This wave's quarter of K for a 16 x 16 output tile (m0, n0) of op = A B:
-//   lane (r, kq) runs k = kb + kq L + q, q < L, kb = w * 4L  (L = K / 16)
-// so each lane streams L contiguous values of its A row.  Two chains (q even / odd).
-template <int L>
-__device__ __forceinline__ void splitk_partial(const double* __restrict__ A, int64_t lda,
-                                               const double* __restrict__ B, int64_t ldb, int m0, int n0,
-                                               dbl4& acc) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, kq = lane >> 4;
-  const int kb = w * 4 * L + kq * L;
-  const double* a = A + (int64_t)(m0 + r) * lda + kb;
-  const double* b = B + (int64_t)kb * ldb + n0 + r;
-  dbl4 c1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int q = 0; q < L; q += 2) {
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[(int64_t)q * ldb], acc, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q + 1], b[(int64_t)(q + 1) * ldb], c1, 0, 0, 0);
-  }
-  acc = acc + c1;
-}
-
-// splitk_partial in two halves: the operand loads (issued before a dependent reduction so
-// their latency overlaps it) and the MFMA chains, in the same order (bit-identical)
 template <int L>
 __device__ __forceinline__ void splitk_load_a(const double* __restrict__ A, int64_t lda, int m0, double (&a)[L]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, kq = lane >> 4;
-  const double* ap = A + (int64_t)(m0 + r) * lda + w * 4 * L + kq * L;
+  const double* ap = A + (int64_t)(m0 + (threadIdx.x & 15)) * lda + splitk_k0<L>();
 #pragma unroll
   for (int q = 0; q < L; ++q) a[q] = ap[q];
 }
 template <int L>
 __device__ __forceinline__ void splitk_load_b(const double* __restrict__ B, int64_t ldb, int n0, double (&b)[L]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, kq = lane >> 4;
-  const double* bp = B + (int64_t)(w * 4 * L + kq * L) * ldb + n0 + r;
+  const double* bp = B + (int64_t)splitk_k0<L>() * ldb + n0 + (threadIdx.x & 15);
 #pragma unroll
   for (int q = 0; q < L; ++q) b[q] = bp[(int64_t)q * ldb];
 }
-template <int L>
-__device__ __forceinline__ void splitk_mfma(const double (&a)[L], const double (&b)[L], dbl4& acc) {
-  dbl4 c1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int q = 0; q < L; q += 2) {
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q + 1], b[q + 1], c1, 0, 0, 0);
-  }
-  acc = acc + c1;
-}
 
-// Sum the 4 waves' partials of one 16 x 16 tile in a fixed order: thread e of the workgroup
-// returns element e (t = e >> 6 register, lane e & 63 of the accumulator layout).
-__device__ __forceinline__ double splitk_sum(const dbl4& part, double* red) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) red[w * 256 + t * 64 + lane] = part[t];
-  __syncthreads();
-  return ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
-}
-
-__device__ __forceinline__ void tile_elem(int e, int& row, int& col) {
-  const int t = e >> 6, lane = e & 63;
-  row = acc_row(lane, t);
-  col = acc_col(lane);
-}
-
-// max over the workgroup of one non-negative float per thread -> red4 (4 floats), all threads
-__device__ __forceinline__ float block_max(float v, float* red4) {
-  v = wave_max(v);
-  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
-  __syncthreads();
-  return fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
-}
-
-__device__ __forceinline__ double abs_or_inf(double v) { return isfinite(v) ? fabs(v) : INFINITY; }
-
-// The domain flags of reduce_check (linear.py:226-230: any(inv + 1e-16 < 0); non-finite),
-// taken on the last outer step's outputs so the fast slot needs no extra pass over Mt.
-__device__ __forceinline__ int domain_flag(double v) { return (v + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v) ? 0 : 2); }
-
-template <int CTRL>
-__device__ __forceinline__ double dpp_add(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
-  return v + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Row sums of |Q| for the ||.||_inf bound: thread e holds tile element (row, col); the 16
-// threads of a row are one DPP row of a wave.  The row's partial over this tile's 16
-// columns goes to rowpart[(m0 + row) * NT + tile column].
+// Row partial of |Q| over this tile's 16 columns -> rowpart[(m0 + row) * NT + tile column]
 __device__ __forceinline__ void store_row_partial(double a, double* __restrict__ rowpart, int m0, int n0, int NT) {
-  a = dpp_add<0xB1>(a);   // quad_perm [1,0,3,2]
-  a = dpp_add<0x4E>(a);   // quad_perm [2,3,0,1]
-  a = dpp_add<0x141>(a);  // row_half_mirror
-  a = dpp_add<0x140>(a);  // row_mirror
+  a = row_sum16(a);
   int row, col;
   tile_elem(threadIdx.x, row, col);
   if (col == 0) rowpart[(int64_t)(m0 + row) * NT + n0 / 16] = a;
 }
 
-// ||Q||_inf = max over rows of the summed row partials (B2 <= NTHREADS rows, one per thread)
 template <int B2>
 __device__ __forceinline__ double inf_norm(const double* __restrict__ rowpart, float* red4) {
-  constexpr int NT = B2 / 16;
-  double r = 0.0;
-  if ((int)threadIdx.x < B2) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) r += rowpart[(int64_t)threadIdx.x * NT + t];
-  }
-  // non-finite propagates as inf/nan; widen by 1e-6 against the float max below
-  const float f = isfinite(r) ? (float)(r * (1.0 + 1e-6)) : INFINITY;
-  return (double)block_max(f, red4);
+  return inf_norm_rows<B2>([&](int i) { return rowpart[i]; }, red4);
 }
 
 // X0 = the warm start of this block: with two consecutive stored slots (st->warm_run >= 2)
@@ -200,7 +114,7 @@ __global__ __launch_bounds__(NTHREADS) void nm_resid_kernel(const double* __rest
 }
 
 // Pass p: rho = ||Q||_inf from the previous launch's row partials; converged -> P = Y + Y Q
-// (done = 1), else Y' = Y + Y Q, Q' = Q Q and the row partials of |Q'|.  Far or diverging
+// (done = p), else Y' = Y + Y Q, Q' = Q Q and the row partials of |Q'|.  Far or diverging
 // -> ST_NEED_GJ.
 template <int L>
 __global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restrict__ Y,
@@ -208,9 +122,12 @@ __global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restr
                                                            double* __restrict__ Qn, double* __restrict__ P,
                                                            const double* __restrict__ part_prev,
                                                            double* __restrict__ part_next, int* __restrict__ done,
-                                                           State* __restrict__ st) {
+                                                           int pass, State* __restrict__ st) {
   if (st->status != ST_RUNNING) return;
-  if (*done) return;
+  // an EARLIER pass converged (done holds its number; this pass's own workgroups may store
+  // theirs meanwhile, which must not make a sibling skip its tile of P)
+  const int dn = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (dn != 0 && dn < pass) return;
   constexpr int B2 = 16 * L;
   __shared__ double red[4 * 256];
   __shared__ float red4[4];
@@ -236,7 +153,7 @@ __global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restr
     splitk_mfma<L>(aY, bQ, ay);
     const double yq = splitk_sum(ay, red);
     st_wt(P + (int64_t)gi * B2 + gj, yold + yq);
-    if (wg == 0 && tid == 0) __hip_atomic_store(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wg == 0 && tid == 0) __hip_atomic_store(done, pass, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   dbl4 aq = {0.0, 0.0, 0.0, 0.0};
@@ -447,7 +364,7 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
     const double* Y = bw.Y[(p - 1) & 1];  // pass 1: X0 from nm_resid
     hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Y, bw.Q[(p - 1) & 1],
                        bw.Y[p & 1], bw.Q[p & 1], bw.P, part + (p - 1) * PART_STRIDE, part + p * PART_STRIDE,
-                       done, st);
+                       done, p, st);
   }
 }
 

@@ -67,6 +67,35 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
 void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes = NM_PASSES_RUN);
 
+// --- dfinv.hip --------------------------------------------------------------
+// The fast slot's blocked inverse as one dataflow launch (tile tasks, host-planned order).
+constexpr int DF_MAX_K2 = 8;  // outer blocks of 256
+// D the one-launch inverse takes (D % 256 == 0, 512 <= D <= MIDAGMA_EXP_DF_MAXD, default 1536)
+bool df_available(int64_t D);
+// ints of the control block (zeroed once at allocation; every launch leaves it zeroed, except
+// the timeout count at [2 * 32])
+int64_t df_ctl_ints(int64_t D);
+struct DfPlanHost {  // views into a process-wide cache
+  const std::vector<int>* tasks;  // 12 ints per task, grouped by workgroup
+  const std::vector<int>* woff;   // nwg + 1 offsets (in tasks)
+  int nctr;
+  double est_us;                  // the list scheduler's makespan under its cost model
+};
+DfPlanHost df_plan(int64_t D, int passes, int nwg);
+struct DfWork {
+  double* A[DF_MAX_K2];  // A^0 (build_at's target) .. A^{K2-1}; A^{K2} is Mt
+  double* Y;             // K2 x (NM_PASSES + 1) series iterates, B2 x B2 each
+  double* Q;
+  double* P;             // K2 converged diagonal-block inverses
+  int* ctl;
+  const int* tasks[2];   // device copies of df_plan(D, 2 / 3, nwg)
+  const int* woff[2];
+  int nwg;
+  unsigned long long* stamps = nullptr;  // diagnostics (MIDAGMA_DF_STAMPS): 3 per task of the last launch
+};
+void launch_df_inverse(double* Mt, int64_t D, const DfWork& w, const BInvWork& bw, int passes, State* st,
+                       hipStream_t stream);
+
 // --- small.hip --------------------------------------------------------------
 // LDS/register block edge of the one-workgroup small-d inner loop (16, 32 or 64; 0: d > 64).
 int small_block(int64_t d);

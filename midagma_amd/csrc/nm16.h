@@ -1,0 +1,99 @@
+// Compute pieces of the product-form diagonal-block inverse shared by the launch-per-phase
+// blocked inverse (blockinv.hip) and the one-launch dataflow inverse (dfinv.hip): the 16 x 16
+// split-K tile product over the 4 waves, its fixed-order wave sum, the row sums of |Q| and the
+// domain flags.  Both files run the same arithmetic in the same order, so their results are
+// bit-identical; they differ only in how operands reach the registers.
+#pragma once
+
+#include "tile32.h"
+
+namespace midagma {
+
+// This wave's quarter of K for a 16 x 16 output tile: lane (r, kq) runs k = kb + kq L + q,
+// q < L, kb = w * 4L (L = K / 16), so each lane streams L contiguous values of its A row.
+// The MFMA chains: q even / odd, summed at the end.
+template <int L>
+__device__ __forceinline__ void splitk_mfma(const double (&a)[L], const double (&b)[L], dbl4& acc) {
+  dbl4 c1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < L; q += 2) {
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q + 1], b[q + 1], c1, 0, 0, 0);
+  }
+  acc = acc + c1;
+}
+
+// first k of this lane's run (see splitk_mfma)
+template <int L>
+__device__ __forceinline__ int splitk_k0() {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  return w * 4 * L + (lane >> 4) * L;
+}
+
+// Sum the 4 waves' partials of one 16 x 16 tile in a fixed order: thread e of the workgroup
+// returns element e (t = e >> 6 register, lane e & 63 of the accumulator layout).
+__device__ __forceinline__ double splitk_sum(const dbl4& part, double* red) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) red[w * 256 + t * 64 + lane] = part[t];
+  __syncthreads();
+  return ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
+}
+
+__device__ __forceinline__ void tile_elem(int e, int& row, int& col) {
+  const int t = e >> 6, lane = e & 63;
+  row = acc_row(lane, t);
+  col = acc_col(lane);
+}
+
+// max over the workgroup of one non-negative float per thread -> red4 (4 floats), all threads
+__device__ __forceinline__ float block_max(float v, float* red4) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
+}
+
+__device__ __forceinline__ double abs_or_inf(double v) { return isfinite(v) ? fabs(v) : INFINITY; }
+
+// The domain flags of reduce_check (linear.py:226-230: any(inv + 1e-16 < 0); non-finite),
+// taken on the last outer step's outputs so the fast slot needs no extra pass over Mt.
+__device__ __forceinline__ int domain_flag(double v) { return (v + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v) ? 0 : 2); }
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_add(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return v + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Row sum over a tile's 16 columns: thread e holds tile element (row, col); the 16 threads of
+// a row are one DPP row of a wave.  Every thread of the row returns the sum.
+__device__ __forceinline__ double row_sum16(double a) {
+  a = dpp_add<0xB1>(a);   // quad_perm [1,0,3,2]
+  a = dpp_add<0x4E>(a);   // quad_perm [2,3,0,1]
+  a = dpp_add<0x141>(a);  // row_half_mirror
+  a = dpp_add<0x140>(a);  // row_mirror
+  return a;
+}
+
+// ||Q||_inf from the row partials (row r's NT = B2 / 16 tile partials at rowpart[r NT + t]),
+// B2 <= NTHREADS rows, one per thread; load(i) returns rowpart[i].  Non-finite propagates as
+// inf/nan; widened by 1e-6 against the float max.
+template <int B2, class Load>
+__device__ __forceinline__ double inf_norm_rows(Load&& load, float* red4) {
+  constexpr int NT = B2 / 16;
+  double r = 0.0;
+  if ((int)threadIdx.x < B2) {
+    double v[NT];  // all loads in flight before the (ordered) sum
+#pragma unroll
+    for (int t = 0; t < NT; ++t) v[t] = load((int)threadIdx.x * NT + t);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) r += v[t];
+  }
+  const float f = isfinite(r) ? (float)(r * (1.0 + 1e-6)) : INFINITY;
+  return (double)block_max(f, red4);
+}
+
+}  // namespace midagma

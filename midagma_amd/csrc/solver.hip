@@ -92,6 +92,11 @@ struct midagma_solver {
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
   DevBuf Malt, Pst2, Pst2b, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone;
+  // the fast slot's inverse as one dataflow launch (dfinv.hip; MIDAGMA_EXP_DF=1 enables: measured
+  // slower than the launch-per-phase inverse at d = 500 and 1000)
+  bool df_on = false;
+  DevBuf dfA, dfY, dfQ, dfP, dfCtl, dfTasks[2], dfWoff[2], dfStamps;
+  DfWork dfw{};
   bool fast_ready = false;  // Pst2 holds the previous slot's outer-block inverses
   double* zbuf = nullptr;  // d x d (+64 tail) score partial; internal or bound
   int64_t zbuf_cap = 0;
@@ -138,7 +143,8 @@ struct midagma_solver {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
-                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW, &scarry, &sprev})
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW, &scarry, &sprev, &dfA, &dfY,
+                      &dfQ, &dfP, &dfCtl, &dfTasks[0], &dfTasks[1], &dfWoff[0], &dfWoff[1], &dfStamps})
       b->release();
     for (DevBuf& b : tbufs) b.release();
     for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices, &cA, &cMi, &cS, &cvec, &cpart, &cP, &cR, &cC}) b->release();
@@ -190,9 +196,7 @@ struct midagma_solver {
   // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
   void enqueue_part1(bool fast = false, int passes = NM_PASSES_RUN) {
     if (blocked()) {
-      launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
-                      stream, IW.p);
-      launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes);
+      enqueue_build_inverse(fast, passes);
     } else if (forked_inverse()) {
       // fork: the inverse (latency-bound, a few % of the chip) on the side stream, the n x d
       // GEMMs on the main one; joined before anything reads Mt.  With the blocked layout the
@@ -229,6 +233,19 @@ struct midagma_solver {
         launch_trek_tcc(W.p, d, D, ccfg, cw, d_state, Gtrek.p, stream);
       else
         launch_trek_pst(W.p, d, D, tcfg, tw, d_state, Gtrek.p, stream);
+    }
+  }
+
+  // blocked layout: build_at and the two-level inverse (fast: warm-started diagonal blocks, as
+  // one dataflow launch when df_on)
+  void enqueue_build_inverse(bool fast, int passes) {
+    if (fast && df_on) {
+      launch_build_at(W.p, D, /*square=*/true, dfw.A[0], D, d, 0.0, d_params, d_state, stream, IW.p);
+      launch_df_inverse(Mt.p, D, dfw, binv(), passes <= 2 ? 2 : 3, d_state, stream);
+    } else {
+      launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
+                      stream, IW.p);
+      launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes);
     }
   }
 
@@ -506,6 +523,8 @@ struct midagma_solver {
       nmPart.alloc((size_t)(D / b2) * (NM_PASSES + 1) * PART_STRIDE);
       nmDone.alloc(D / b2);
     }
+    const char* dfe = getenv("MIDAGMA_EXP_DF");
+    if (blocked() && mode == MIDAGMA_MODE_COV && df_available(D) && dfe && atoi(dfe) != 0) setup_df();
     zown.alloc(DD + 64);
     HIP_TRY(hipMemsetAsync(zown.p, 0, (DD + 64) * sizeof(double), stream));
     zbuf = zown.p;
@@ -521,6 +540,51 @@ struct midagma_solver {
       HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     }
+  }
+
+  // buffers and the two task plans (2 and 3 product-form passes) of the one-launch inverse
+  void setup_df() {
+    const int64_t K2 = D / 256, BB = 256 * 256, DD = D * D;
+    int ncu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+    // workgroups per CU (the kernel's registers admit 2; every one must be resident)
+    static const int per_cu = getenv("MIDAGMA_EXP_DF_PER_CU") ? std::max(1, std::min(2, atoi(getenv("MIDAGMA_EXP_DF_PER_CU")))) : 2;
+    ncu *= per_cu;
+    dfA.alloc((size_t)K2 * DD);
+    dfY.alloc((size_t)K2 * (NM_PASSES + 1) * BB);
+    dfQ.alloc((size_t)K2 * (NM_PASSES + 1) * BB);
+    dfP.alloc((size_t)K2 * BB);
+    const int64_t nctl = df_ctl_ints(D);
+    dfCtl.alloc((size_t)(nctl + 1) / 2);
+    HIP_TRY(hipMemset(dfCtl.p, 0, (size_t)nctl * sizeof(int)));
+    for (int k = 0; k < 2; ++k) {
+      const DfPlanHost pl = df_plan(D, k == 0 ? 2 : 3, ncu);
+      dfTasks[k].alloc((pl.tasks->size() + 1) / 2);
+      dfWoff[k].alloc((pl.woff->size() + 1) / 2);
+      HIP_TRY(hipMemcpy(dfTasks[k].p, pl.tasks->data(), pl.tasks->size() * sizeof(int), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(dfWoff[k].p, pl.woff->data(), pl.woff->size() * sizeof(int), hipMemcpyHostToDevice));
+      dfw.tasks[k] = reinterpret_cast<const int*>(dfTasks[k].p);
+      dfw.woff[k] = reinterpret_cast<const int*>(dfWoff[k].p);
+    }
+    for (int64_t g = 0; g < K2; ++g) dfw.A[g] = dfA.p + g * DD;
+    dfw.Y = dfY.p;
+    dfw.Q = dfQ.p;
+    dfw.P = dfP.p;
+    dfw.ctl = reinterpret_cast<int*>(dfCtl.p);
+    dfw.nwg = ncu;
+    if (getenv("MIDAGMA_DF_STAMPS")) {  // diagnostics: per-task timestamps of the last launch
+      dfStamps.alloc((size_t)3 * std::max(df_plan(D, 3, ncu).tasks->size(), df_plan(D, 2, ncu).tasks->size()) / 12);
+      HIP_TRY(hipMemset(dfStamps.p, 0, dfStamps.n * sizeof(double)));
+      dfw.stamps = reinterpret_cast<unsigned long long*>(dfStamps.p);
+    }
+    df_on = true;
+  }
+  // wait timeouts of the one-launch inverse so far (a planning bug; the solver raises on it)
+  int df_timeouts() {
+    if (!df_on) return 0;
+    int t = 0;
+    HIP_TRY(hipMemcpy(&t, dfw.ctl + 2 * 32, sizeof(int), hipMemcpyDeviceToHost));
+    return t;
   }
 
   void upload_matrix(DevBuf& dst, const double* src, int64_t ld_src) {
@@ -684,6 +748,7 @@ struct midagma_solver {
     }
     handback_count += handbacks;
     fast_batch = bmax;
+    if (const int to = df_timeouts()) throw std::runtime_error("one-launch inverse: " + std::to_string(to) + " wait timeouts");
     static const bool dbg = getenv("MIDAGMA_DEBUG_HANDBACKS") != nullptr;  // diagnostics
     if (dbg) fprintf(stderr, "drive_blocked: %lld slots, %lld hand-backs\n", (long long)launched, (long long)handbacks);
   }
@@ -1117,11 +1182,7 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
       // [6] build + fast blocked inverse, less [0]   [7] whole fast slot (graph).  Both need a
       // warm start and no pending checkpoint: one slow slot first.
       HIP_TRY(hipGraphLaunch(s->g_full, s->stream));
-      ms_out[6] = timed([&] {
-        launch_build_at(s->W.p, D, true, binv_build_target(s->Mt.p, D, s->binv()), D, s->d, 0.0, s->d_params,
-                        s->d_state, s->stream);
-        launch_blocked_inverse(s->Mt.p, D, s->binv(), true, s->gj(), s->d_state, s->stream);
-      }) - ms_out[0];
+      ms_out[6] = timed([&] { s->enqueue_build_inverse(/*fast=*/true, 2); }) - ms_out[0];
       ms_out[7] = timed([&] { HIP_TRY(hipGraphLaunch(s->g_fast, s->stream)); });
       State st{};
       HIP_TRY(hipMemcpy(&st, s->d_state, sizeof(State), hipMemcpyDeviceToHost));
@@ -1660,4 +1721,35 @@ extern "C" int midagma_counter_advance(int64_t* counter, void* stream) {
     launch_counter_advance(counter, reinterpret_cast<hipStream_t>(stream));
     return MIDAGMA_OK;
   });
+}
+
+// Diagnostics (not part of the ABI header): the one-launch inverse's task plan for D, passes
+// and nwg workgroups, as planned on the host (no GPU needed).  tasks (12 ints per task, grouped
+// by workgroup) and woff (nwg + 1) may be null to query the sizes.  Returns 0, or -1.
+extern "C" int midagma_debug_df_plan(int64_t D, int passes, int nwg, double* est_us, int64_t* ntasks, int* tasks,
+                                     int* woff, int* nctr) {
+  try {
+    if (!df_available(D) || (passes != 2 && passes != 3) || nwg < 1) return -1;
+    const DfPlanHost p = df_plan(D, passes, nwg);
+    if (est_us) *est_us = p.est_us;
+    if (ntasks) *ntasks = (int64_t)(p.tasks->size() / 12);
+    if (nctr) *nctr = p.nctr;
+    if (tasks) std::memcpy(tasks, p.tasks->data(), p.tasks->size() * sizeof(int));
+    if (woff) std::memcpy(woff, p.woff->data(), p.woff->size() * sizeof(int));
+    return 0;
+  } catch (const std::exception& e) {
+    fprintf(stderr, "midagma_debug_df_plan: %s\n", e.what());
+    return -1;
+  }
+}
+
+// Diagnostics: the one-launch inverse's per-task timestamps of the last launch (3 per task in
+// plan order: wait start, go, done; 100 MHz ticks), with MIDAGMA_DF_STAMPS set at create.
+// Returns the number of values copied, or -1.
+extern "C" int64_t midagma_debug_df_stamps(midagma_solver* s, unsigned long long* out, int64_t cap) {
+  if (!s || !s->dfw.stamps) return -1;
+  const int64_t n = std::min<int64_t>(cap, (int64_t)s->dfStamps.n);
+  if (hipStreamSynchronize(s->stream) != hipSuccess) return -1;
+  if (hipMemcpy(out, s->dfStamps.p, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return n;
 }

@@ -97,6 +97,13 @@ if __name__ == "__main__":
         cov_case(200, 2000, 20, 500)
     if which in ("all", "d1000"):
         cov_case(1000, 2000, 10, 2000)
+    if which == "dfcmp":  # the one-launch fast-slot inverse against the launch-per-phase one
+        for d, K in ((1000, 2000), (500, 2000), (1400, 1000)):
+            for df in ("1", "0"):
+                os.environ["MIDAGMA_EXP_DF"] = df
+                print(f"MIDAGMA_EXP_DF={df}", end=" ")
+                cov_case(d, 2 * d, 10, K)
+        os.environ.pop("MIDAGMA_EXP_DF")
     if which == "d1000short":  # PMC passes: few dispatches
         cov_case(1000, 2000, 10, 40)
     if which == "fit":
