@@ -115,7 +115,8 @@ class _MLPObjective(torch.autograd.Function):
     sums together with the log-det and L1 gradients."""
 
     @staticmethod
-    def forward(ctx, X, W1, b1, w2, b2, d: int, m1: int, s: float, mu: float, lambda1: float):
+    def forward(ctx, X, W1, b1, w2, b2, d: int, m1: int, s: float, mu: float, lambda1: float,
+                overlap: bool = False):
         L = _lib.lib()
         dev = X.device
         X, W1, b1, w2, b2 = X.contiguous(), W1.contiguous(), b1.contiguous(), w2.contiguous(), b2.contiguous()
@@ -132,13 +133,45 @@ class _MLPObjective(torch.autograd.Function):
         scratch = torch.empty(int(L.midagma_mlp_tail_scratch(n, d, m1)), **f64)
         ssq = torch.empty((), **f64)
         obj = torch.empty((), **f64)
+        ctx.ev_done = None
         with torch.cuda.device(dev):
             _lib.check(L.midagma_fc1_terms(_vp(W1), d, m1, _vp(A), _vp(l1part), st), None, "fc1_terms")
-            _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None, "logdet_h_dev")
-            _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
-                                              _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
-            _lib.check(L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(h), float(mu),
-                                               float(lambda1), 0.5 * d, 1 / n, _vp(obj), st), None, "mlp_objective")
+            if overlap:
+                # The log-det chain (Gauss-Jordan block steps: latency-bound, ~40% of a config-5
+                # step) depends on fc1 only: it runs on a side stream beside the tail forward and
+                # the backward up to the weight gradient, which never read h or the objective's
+                # value; the side stream also forms the objective once the tail's ssq is ready,
+                # and backward joins before the fc1 terms' backward needs (sI - A)^-T.  Only for
+                # callers that run backward right away (DagmaNonlinear.minimize): the join is there.
+                # (capture order matters in the replayed graph: the log-det chain captured first
+                # measured 5215 steps/s at config 5, the tail first 3817, one stream 4943)
+                main = torch.cuda.current_stream(dev)
+                side = _side_stream(dev)
+                ev_fc1 = torch.cuda.Event()
+                ev_fc1.record(main)
+                side.wait_event(ev_fc1)
+                ss = C.c_void_p(side.cuda_stream)
+                _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, ss), None,
+                           "logdet_h_dev")
+                _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
+                                                  _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
+                ev_tail = torch.cuda.Event()
+                ev_tail.record(main)
+                side.wait_event(ev_tail)
+                _lib.check(L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(h), float(mu),
+                                                   float(lambda1), 0.5 * d, 1 / n, _vp(obj), ss), None,
+                           "mlp_objective")
+                ctx.ev_done = torch.cuda.Event()
+                ctx.ev_done.record(side)
+                ctx.keep = (A, l1part)  # read on the side stream: alive until the join
+            else:
+                _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None,
+                           "logdet_h_dev")
+                _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
+                                                  _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
+                _lib.check(L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(h), float(mu),
+                                                   float(lambda1), 0.5 * d, 1 / n, _vp(obj), st), None,
+                           "mlp_objective")
         ctx.save_for_backward(X, W1, b1, w2, Z, R, Mt, ssq, scratch)
         ctx.consts = (n, d, m1, float(mu), float(lambda1), l1part.numel())
         ctx.set_materialize_grads(False)  # h's own gradient stays None (no zero fill and add)
@@ -172,9 +205,23 @@ class _MLPObjective(torch.autograd.Function):
             else:
                 lin = (dZ.t() @ X).contiguous()
                 nlin = 1
+            if ctx.ev_done is not None:  # join the side stream's log-det and objective
+                torch.cuda.current_stream(dev).wait_event(ctx.ev_done)
             _lib.check(L.midagma_fc1_terms_bwd(_vp(W1), d, m1, _vp(Mt), _vp(gh), _vp(gl1), _vp(lin), nlin,
                                                _vp(dW1), st), None, "fc1_terms_bwd")
-        return None, dW1, db1, dw2, db2, None, None, None, None, None
+        return None, dW1, db1, dw2, db2, None, None, None, None, None, None
+
+
+_SIDE: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    """One side stream per device for the MLP objective's log-det (created outside any capture:
+    the first step of every minimize call is a warm-up launched eagerly)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=key)
+    return _SIDE[key]
 
 
 def logdet_h(A: torch.Tensor, s: float = 1.0) -> torch.Tensor:
@@ -296,13 +343,15 @@ class DagmaNonlinear:
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         # one Adam step captured once per minimize call and replayed (hipGraph); False: eager steps
         self.graph = graph and not os.environ.get("MIDAGMA_NO_GRAPH")
+        # the log-det on a side stream beside the rest of the step (MIDAGMA_NO_OVERLAP=1: one stream)
+        self.overlap = not os.environ.get("MIDAGMA_NO_OVERLAP")
 
     def log_mse_loss(self, output: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         """d/2 log(1/n sum (output - target)^2)  (nonlinear.py:139-159)."""
         n, d = target.shape
         return 0.5 * d * torch.log(1 / n * torch.sum((output - target) ** 2))
 
-    def _h_and_objective(self, mu: float, lambda1: float, s: float):
+    def _h_and_objective(self, mu: float, lambda1: float, s: float, overlap: bool = False):
         """(h, mu * (score + lambda1 * |fc1|_1) + h) (nonlinear.py:198-204): for a [d, m1, 1] MLP
         on the GPU through the fused kernels (fc1 terms, log-det, tail, scalar objective),
         otherwise the reference's expressions."""
@@ -311,7 +360,8 @@ class DagmaNonlinear:
             n, d = self.X.shape
             m1 = m.dims[1]
             fc = m.fc2[0]
-            return _MLPObjective.apply(self.X, m.fc1.weight, m.fc1.bias, fc.weight, fc.bias, d, m1, s, mu, lambda1)
+            return _MLPObjective.apply(self.X, m.fc1.weight, m.fc1.bias, fc.weight, fc.bias, d, m1, s, mu, lambda1,
+                                       overlap)
         h_val = m.h_func(s)
         return h_val, mu * (self._score() + lambda1 * m.fc1_l1_reg()) + h_val
 
@@ -349,7 +399,7 @@ class DagmaNonlinear:
         for i in range(max_iter):
             for p in params:
                 p.grad = None
-            h_val, obj = self._h_and_objective(mu, lambda1, s)
+            h_val, obj = self._h_and_objective(mu, lambda1, s, overlap=self.overlap)
             obj.backward()
             step = i + 1
             bc1 = 1 - beta1 ** step
@@ -405,7 +455,7 @@ class DagmaNonlinear:
         def body(gate):
             for p in params:
                 p.grad = None
-            h_val, obj = self._h_and_objective(mu, lambda1, s)
+            h_val, obj = self._h_and_objective(mu, lambda1, s, overlap=self.overlap)
             obj.backward()
             stream = torch.cuda.current_stream(dev).cuda_stream
             st = C.c_void_p(stream) if stream else None

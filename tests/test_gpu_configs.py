@@ -110,3 +110,30 @@ def test_config5_mlp_minimize_d200(K):
         dev = np.abs(sd[k].cpu().numpy() - r).max()
         print(f"K={K} {k}: max|d| = {dev:.3e} (max|p| {np.abs(r).max():.3e})")
         assert dev <= 1e-9 * max(1.0, np.abs(r).max()), k
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_config5_logdet_side_stream_bit_identical(graph, monkeypatch):
+    """The MLP objective's log-det on a side stream (overlapping the tail and the backward, joined
+    before the fc1 terms' backward) runs the same kernels on the same data as the one-stream
+    step: after 200 Adam steps at dims [200, 10, 1] every parameter is bit-identical, in the
+    graph-replayed and the eager loop."""
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    d, n = 200, 1000
+    X, _, _ = make_dataset(d, n, seed=1)
+    out = {}
+    for overlap in (True, False):
+        if overlap:
+            monkeypatch.delenv("MIDAGMA_NO_OVERLAP", raising=False)
+        else:
+            monkeypatch.setenv("MIDAGMA_NO_OVERLAP", "1")
+        torch.manual_seed(7)
+        model = DagmaMLP(dims=[d, 10, 1], bias=True).to("cuda:0")
+        dn = DagmaNonlinear(model, device=0, graph=graph)
+        assert dn.overlap == overlap
+        dn.X = torch.from_numpy(X).to("cuda:0")
+        dn.checkpoint = 50
+        assert dn.minimize(200, 2e-4, 0.02, 0.005, 0.1, 1.0)
+        out[overlap] = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    for k in out[True]:
+        assert np.array_equal(out[True][k], out[False][k]), k
