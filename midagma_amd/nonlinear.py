@@ -452,11 +452,13 @@ class DagmaNonlinear:
         no_step = torch.full((), -1.0, dtype=torch.float64, device=dev)
         L = _lib.lib()
 
+        seed = torch.ones((), dtype=torch.float64, device=dev)  # d obj / d obj: no fill node per step
+
         def body(gate):
             for p in params:
                 p.grad = None
             h_val, obj = self._h_and_objective(mu, lambda1, s, overlap=self.overlap)
-            obj.backward()
+            obj.backward(seed)
             stream = torch.cuda.current_stream(dev).cuda_stream
             st = C.c_void_p(stream) if stream else None
             g_ptr = C.c_void_p((h_val if gate is None else gate).data_ptr())
