@@ -24,6 +24,7 @@
 //         then set ST_NEED_GJ and the host re-runs the slot on the slow path.
 #include <cstdlib>
 
+#include "binv_tile.h"
 #include "launch.h"
 #include "nm16.h"
 
@@ -32,11 +33,6 @@ namespace midagma {
 namespace {
 
 
-__device__ __forceinline__ int xcd_spread(int w, int nwg) {
-  // consecutive jobs (which share operand panels) onto one XCD: blocks b, b+8 share an XCD
-  const int q = nwg / 8, r = nwg % 8, x = w % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
-}
 
 template <int L>
 __device__ __forceinline__ void splitk_load_a(const double* __restrict__ A, int64_t lda, int m0, double (&a)[L]) {
@@ -167,75 +163,11 @@ __global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restr
   store_row_partial(abs_or_inf(qq), part_next, m0, n0, nt);
 }
 
-// acc += A[0:32, 0:K] B[0:K, 0:32] (global operands, K <= 256), 32-deep chunks through double-
-// buffered LDS images; the register loads run PF chunks ahead of the MFMAs (the operands were
-// written by the previous launch on other XCDs: each chunk is a MALL round trip).  One barrier
-// per chunk.
-template <int PF, int NK>
-__device__ __forceinline__ void tile32_gemm_pf(const double* __restrict__ A, int64_t lda,
-                                               const double* __restrict__ B, int64_t ldb, dbl4& acc,
-                                               double* As0, double* As1, double* Bs0, double* Bs1) {
-  const int tid = threadIdx.x;
-  const int r0 = tid >> 4, c0 = (tid & 15) * 2;  // items tid and tid + 256: rows r0, r0 + 16
-  double2 a0[PF], a1[PF], b0[PF], b1[PF];
-  constexpr int nk = NK;
-#define T32_LOAD(slot, kc)                                                                 \
-  do {                                                                                     \
-    const double* ap = A + (int64_t)r0 * lda + (kc) * 32 + c0;                             \
-    const double* bp = B + ((int64_t)(kc) * 32 + r0) * ldb + c0;                           \
-    a0[slot] = *reinterpret_cast<const double2*>(ap);                                      \
-    a1[slot] = *reinterpret_cast<const double2*>(ap + 16 * lda);                           \
-    b0[slot] = *reinterpret_cast<const double2*>(bp);                                      \
-    b1[slot] = *reinterpret_cast<const double2*>(bp + 16 * ldb);                           \
-  } while (0)
-#pragma unroll
-  for (int p = 0; p < PF; ++p)
-    if (p < nk) T32_LOAD(p, p);
-  // slot 0 holds chunk kc; the queue shifts by one each chunk (constant register indices:
-  // the loop need not be unrolled for the arrays to stay in registers)
-  for (int kc = 0; kc < nk; ++kc) {
-    double* As = (kc & 1) ? As1 : As0;
-    double* Bs = (kc & 1) ? Bs1 : Bs0;
-    *reinterpret_cast<double2*>(As + r0 * ST + c0) = a0[0];
-    *reinterpret_cast<double2*>(As + (r0 + 16) * ST + c0) = a1[0];
-    *reinterpret_cast<double2*>(Bs + r0 * ST + c0) = b0[0];
-    *reinterpret_cast<double2*>(Bs + (r0 + 16) * ST + c0) = b1[0];
-    __syncthreads();
-#pragma unroll
-    for (int p = 0; p + 1 < PF; ++p) {
-      a0[p] = a0[p + 1];
-      a1[p] = a1[p + 1];
-      b0[p] = b0[p + 1];
-      b1[p] = b1[p + 1];
-    }
-    if (kc + PF < nk) T32_LOAD(PF - 1, kc + PF);
-    mma32(As, Bs, acc);
-  }
-#undef T32_LOAD
-}
-
 // prefetch depth of the panel / trailing tiles (experiment knob MIDAGMA_EXP_T32_PF: 1, 2, 3;
 // d=1000 fast slot: 4160 steps/s at 1, 4340 at 3, two runs each)
 static int t32_pf() {
   static const int pf = getenv("MIDAGMA_EXP_T32_PF") ? atoi(getenv("MIDAGMA_EXP_T32_PF")) : 3;
   return pf < 1 ? 1 : (pf > 3 ? 3 : pf);
-}
-
-__device__ __forceinline__ void tile32_gemm_any(int pf, const double* __restrict__ A, int64_t lda,
-                                                const double* __restrict__ B, int64_t ldb, int K, dbl4& acc,
-                                                double* As0, double* As1, double* Bs0, double* Bs1) {
-  if (K == 128) {
-    if (pf >= 2)
-      tile32_gemm_pf<2, 4>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
-    else
-      tile32_gemm_pf<1, 4>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
-  } else if (pf == 3) {
-    tile32_gemm_pf<3, 8>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
-  } else if (pf == 2) {
-    tile32_gemm_pf<2, 8>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
-  } else {
-    tile32_gemm_pf<1, 8>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
-  }
 }
 
 // Panels of outer step g (one 32 x 32 tile per workgroup):
@@ -301,35 +233,14 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
   }
 }
 
-// Trailing update of outer step g: Aout[i, j] = Ain[i, j] - Ain[i, G] Aout[G, j] for i, j
-// outside G (Aout[G, j] = P Ain[G, j] from the panel launch).
+// Trailing update of outer step g, one 32 x 32 tile per workgroup (binv_trail_tile).
 __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __restrict__ Ain,
                                                               double* __restrict__ Aout, int64_t D, int B2, int g,
                                                               int check, State* __restrict__ st, int pf) {
   if (st && st->status != ST_RUNNING) return;
   __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
-  const int nb = (int)(D / NB), gb = B2 / NB, g0 = g * gb, mb = nb - gb;
-  const int job = xcd_spread(blockIdx.x, gridDim.x);
-  const int iq = job / mb, jq = job % mb;
-  const int i = iq < g0 ? iq : iq + gb, j = jq < g0 ? jq : jq + gb;
-  const int64_t G0 = (int64_t)g0 * NB;
-  const double* Ci = Ain + (int64_t)i * NB * D + (int64_t)j * NB;
-  dbl4 c_old;
-  acc_foreach(c_old, [&](int row, int col, double& v) { v = Ci[(int64_t)row * D + col]; });
-  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  tile32_gemm_any(pf, Ain + (int64_t)i * NB * D + G0, D, Aout + G0 * D + (int64_t)j * NB, D, B2, acc, img[0],
-                  img[1], img[2], img[3]);
-  double* out = Aout + (int64_t)i * NB * D + (int64_t)j * NB;
-  const int lane = threadIdx.x & 63, m0 = q_m0(), n0 = q_n0();
-  int flag = 0;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int row = m0 + acc_row(lane, t), col = n0 + acc_col(lane);
-    const double v = c_old[t] - acc[t];
-    st_wt(out + (int64_t)row * D + col, v);
-    flag |= domain_flag(v);
-  }
-  if (check && flag) atomicOr(&st->flags, flag);
+  binv_trail_tile(xcd_spread(blockIdx.x, gridDim.x), Ain, Aout, D, B2, g, check, st, pf, img[0], img[1], img[2],
+                  img[3]);
 }
 
 }  // namespace
@@ -368,8 +279,9 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
   }
 }
 
-void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
-                            hipStream_t stream, int passes) {
+bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
+                            hipStream_t stream, int passes, const GemmSpec* fuse) {
+  bool fused = false;
   const int B2 = binv_block(D);
   if (B2 == 0) throw std::invalid_argument("blocked inverse needs D >= 256, D % 128 == 0");
   const int K2 = (int)(D / B2), gb = B2 / NB, mb = (int)(D / NB) - gb;
@@ -406,14 +318,19 @@ void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
                        g, P, ldp, Pe, Po, done, check, st, t32_pf());
     if (mb > 0) {
       // large D: 128 x 128 tiles (operand reuse; enough tiles to fill the chip), else 32 x 32
-      if (D - B2 >= TRAIL128_MIN)
+      if (D - B2 >= TRAIL128_MIN) {
         launch_trail128(Ain, Aout, D, B2, g, check, st, stream);
-      else
+      } else if (fuse && fast && g == K2 - 1 && gemm_trail_supported(*fuse)) {
+        launch_gemm_trail(*fuse, Ain, Aout, D, B2, g, check, st, t32_pf(), mb * mb, stream);
+        fused = true;
+      } else {
         hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2, g, check,
                            st, t32_pf());
+      }
     }
   }
   HIP_TRY(hipGetLastError());
+  return fused;
 }
 
 }  // namespace midagma

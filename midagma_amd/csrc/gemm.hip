@@ -10,6 +10,7 @@
 // the shard) is split over blockIdx.z into fixed slices summed in fixed order.
 #include <cstdlib>
 
+#include "binv_tile.h"
 #include "launch.h"
 #include "mfma64.h"
 
@@ -323,17 +324,16 @@ constexpr int P_S = 132;
 constexpr int P_IMG = 16 * P_S;
 constexpr size_t kGemmPipeLds = 2 * P_IMG * sizeof(double);
 
+// One 128 x 128 output tile (t: its index after the XCD remap) of the pipelined GEMM; smem:
+// kGemmPipeLds bytes.  The body of gemm_pipe_kernel, and of the launch that runs the cov score
+// GEMM beside the blocked inverse's last trailing update (gemm_trail_kernel).
 template <int AMODE, int BMODE, int EPI>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64_t kslice, int tiles_m, int tiles_n,
-                                                                const double* __restrict__ A, int64_t lda,
-                                                                const double* __restrict__ B, int64_t ldb,
-                                                                double* __restrict__ C, int64_t ldc,
-                                                                int64_t slice_stride, double* __restrict__ loss_part,
-                                                                int64_t m_valid, int64_t n_valid,
-                                                                const State* __restrict__ st) {
-  if (st && st->status != ST_RUNNING) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+__device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice, int tiles_m, int tiles_n,
+                                               const double* __restrict__ A, int64_t lda,
+                                               const double* __restrict__ B, int64_t ldb, double* __restrict__ C,
+                                               int64_t ldc, int64_t slice_stride, double* __restrict__ loss_part,
+                                               int64_t m_valid, int64_t n_valid, const State* __restrict__ st,
+                                               double* __restrict__ smem) {
   const int per_slice = tiles_m * tiles_n;
   const int z = t / per_slice, rem = t % per_slice;
   int bm, bn;
@@ -573,6 +573,57 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64
   if (tid == 0) loss_part[blockIdx.x] = red[0];
 }
 
+template <int AMODE, int BMODE, int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64_t kslice, int tiles_m, int tiles_n,
+                                                                const double* __restrict__ A, int64_t lda,
+                                                                const double* __restrict__ B, int64_t ldb,
+                                                                double* __restrict__ C, int64_t ldc,
+                                                                int64_t slice_stride, double* __restrict__ loss_part,
+                                                                int64_t m_valid, int64_t n_valid,
+                                                                const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  gemm_pipe_tile<AMODE, BMODE, EPI>(xcd_remap(blockIdx.x, gridDim.x), K, kslice, tiles_m, tiles_n, A, lda, B, ldb, C,
+                                    ldc, slice_stride, loss_part, m_valid, n_valid, st, smem);
+}
+
+
+// The cov score GEMM and the blocked inverse's LAST trailing update in one launch: the first
+// n_gemm workgroups run gemm_pipe_tile (the GEMM's own launch, bit-identical), the rest the
+// 32 x 32 trailing tiles (binv_trail_tile).  The GEMM reads W and cov only, so it needs nothing
+// of the inverse; the trailing tiles (≈12 us at d = 1000) run beside it instead of as a
+// launch of their own.
+struct GemmTrailArgs {
+  int64_t K, kslice;
+  int tm, tn, n_gemm;
+  const double* A;
+  int64_t lda;
+  const double* B;
+  int64_t ldb;
+  double* C;
+  int64_t ldc, slice_stride;
+  const double* Ain;
+  double* Aout;
+  int64_t D;
+  int B2, g, check, pf;
+  State* st;
+};
+constexpr size_t kGemmTrailLds = (4 * NB * ST * sizeof(double) > kGemmPipeLds) ? 4 * NB * ST * sizeof(double)
+                                                                                : kGemmPipeLds;
+
+template <int AMODE, int BMODE>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_trail_kernel(GemmTrailArgs a) {
+  if (a.st->status != ST_RUNNING) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x;
+  if (b < a.n_gemm) {
+    gemm_pipe_tile<AMODE, BMODE, EPI_STORE>(xcd_remap(b, a.n_gemm), a.K, a.kslice, a.tm, a.tn, a.A, a.lda, a.B, a.ldb,
+                                            a.C, a.ldc, a.slice_stride, nullptr, 0, 0, a.st, smem);
+  } else {
+    binv_trail_tile(xcd_spread(b - a.n_gemm, (int)gridDim.x - a.n_gemm), a.Ain, a.Aout, a.D, a.B2, a.g, a.check, a.st,
+                    a.pf, smem, smem + NB * ST, smem + 2 * NB * ST, smem + 3 * NB * ST);
+  }
+}
 
 constexpr size_t kGemmLds = (2 * 64 * SB) * sizeof(double);
 
@@ -594,7 +645,17 @@ static void set_attr_pipe() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmPipeLds));
 }
 
+template <int AM, int BM>
+static void set_attr_gt() {
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_trail_kernel<AM, BM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmTrailLds));
+}
+
 void gemm_setup_attributes() {
+  set_attr_gt<1, B_PLAIN>();
+  set_attr_gt<1, B_IMINUS>();
+  set_attr_gt<0, B_PLAIN>();
+  set_attr_gt<0, B_IMINUS>();
   set_attr_pipe<1, B_PLAIN, EPI_STORE>();
   set_attr_pipe<1, B_IMINUS, EPI_STORE>();
   set_attr_pipe<0, B_PLAIN, EPI_STORE>();
@@ -708,6 +769,53 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
     MIDAGMA_GEMM(true, B_IMINUS, EPI_STORE);
   }
 #undef MIDAGMA_GEMM
+  HIP_TRY(hipGetLastError());
+}
+
+bool gemm_trail_supported(const GemmSpec& gs) {
+  return gs.M % 128 == 0 && gs.N % 128 == 0 && gs.K % 16 == 0 && gs.split >= 1 &&
+         getenv("MIDAGMA_EXP_GEMM64") == nullptr && getenv("MIDAGMA_EXP_NO_PIPE") == nullptr;
+}
+
+void launch_gemm_trail(const GemmSpec& gs, const double* Ain, double* Aout, int64_t D, int B2, int g, bool check,
+                       State* st, int pf, int n_trail, hipStream_t stream) {
+  if (!gemm_trail_supported(gs)) throw std::invalid_argument("launch_gemm_trail: shape");
+  const int64_t ktiles16 = gs.K / 16;
+  const int64_t per16 = (ktiles16 + gs.split - 1) / gs.split;
+  const int nsplit = (int)((ktiles16 + per16 - 1) / per16);
+  GemmTrailArgs a{};
+  a.K = gs.K;
+  a.kslice = per16 * 16;
+  a.tm = (int)(gs.M / 128);
+  a.tn = (int)(gs.N / 128);
+  a.n_gemm = a.tm * a.tn * nsplit;
+  a.A = gs.A;
+  a.lda = gs.lda;
+  a.B = gs.B;
+  a.ldb = gs.ldb;
+  a.C = gs.C;
+  a.ldc = gs.ldc;
+  a.slice_stride = gs.slice_stride;
+  a.Ain = Ain;
+  a.Aout = Aout;
+  a.D = D;
+  a.B2 = B2;
+  a.g = g;
+  a.check = check ? 1 : 0;
+  a.pf = pf;
+  a.st = st;
+  const dim3 grid((unsigned)(a.n_gemm + n_trail));
+#define MIDAGMA_GT(AM, BM) \
+  hipLaunchKernelGGL((gemm_trail_kernel<AM, BM>), grid, dim3(NTHREADS), kGemmTrailLds, stream, a)
+  if (gs.a_trans && gs.bmode == B_PLAIN)
+    MIDAGMA_GT(1, B_PLAIN);
+  else if (gs.a_trans)
+    MIDAGMA_GT(1, B_IMINUS);
+  else if (gs.bmode == B_PLAIN)
+    MIDAGMA_GT(0, B_PLAIN);
+  else
+    MIDAGMA_GT(0, B_IMINUS);
+#undef MIDAGMA_GT
   HIP_TRY(hipGetLastError());
 }
 

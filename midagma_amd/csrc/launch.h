@@ -37,6 +37,22 @@ void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int6
 // leading dimension lda (D multiple of 32), pivot logs into w.pivlog.
 void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
 
+// A GEMM launch's arguments (launch_gemm's meaning), for launches that carry one beside other work.
+enum GemmB : int;
+struct GemmSpec {
+  int64_t M, N, K;
+  const double* A;
+  int64_t lda;
+  bool a_trans;
+  const double* B;
+  int64_t ldb;
+  int bmode;  // GemmB
+  double* C;
+  int64_t ldc;
+  int split;
+  int64_t slice_stride;
+};
+
 // --- blockinv.hip -----------------------------------------------------------
 // product-form pass slots per outer block (buffers) and the passes of the fallback fast graph
 // (the default fast graph runs 2: the extrapolated warm start converges in 2 almost always;
@@ -64,8 +80,11 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
 // flags into st->flags from the last outer step's outputs.
 // passes: product-form pass launches per outer block on the fast path (2 covers the
 // extrapolated warm start's usual residual, 3 the rest; an unconverged block hands back).
-void launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
-                            hipStream_t stream, int passes = NM_PASSES_RUN);
+// fuse (nullable; fast path): a GEMM (EPI_STORE, split-K slices) that runs in the launch of the
+// last outer step's 32 x 32 trailing update (gemm.hip, launch_gemm_trail); false is returned
+// when that launch is not available for this D and the caller must launch the GEMM itself.
+bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
+                            hipStream_t stream, int passes = NM_PASSES_RUN, const GemmSpec* fuse = nullptr);
 
 // --- dfinv.hip --------------------------------------------------------------
 // The fast slot's blocked inverse as one dataflow launch (tile tasks, host-planned order).
@@ -255,6 +274,11 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
 // with `check`, ORs the domain flags of the outputs into st->flags.
 void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
                      hipStream_t stream);
+// The GEMM gs (EPI_STORE) and the blocked inverse's 32 x 32 trailing update of outer step g
+// (n_trail tiles) in one launch.
+bool gemm_trail_supported(const GemmSpec& gs);
+void launch_gemm_trail(const GemmSpec& gs, const double* Ain, double* Aout, int64_t D, int B2, int g, bool check,
+                       State* st, int pf, int n_trail, hipStream_t stream);
 // dst[c][r] = src[r][c] (rows x cols)
 void launch_transpose(const double* src, int64_t ld_src, int64_t rows, int64_t cols, double* dst, int64_t ld_dst,
                       hipStream_t stream);

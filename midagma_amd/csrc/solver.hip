@@ -195,8 +195,14 @@ struct midagma_solver {
   // ---- the slot -----------------------------------------------------------
   // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
   void enqueue_part1(bool fast = false, int passes = NM_PASSES_RUN) {
+    bool gemm_done = false;
     if (blocked()) {
-      enqueue_build_inverse(fast, passes);
+      // cov fast slot: the score GEMM rides in the last trailing update's launch (its split-K
+      // slices are what fused_update sums anyway); MIDAGMA_EXP_FUSE_GEMM=0 keeps it apart
+      GemmSpec gs{};
+      const bool fuse = fast && mode == MIDAGMA_MODE_COV && cov_split > 1 && fuse_gemm;
+      if (fuse) gs = score_cov_spec();
+      gemm_done = enqueue_build_inverse(fast, passes, fuse ? &gs : nullptr);
     } else if (forked_inverse()) {
       // fork: the inverse (latency-bound, a few % of the chip) on the side stream, the n x d
       // GEMMs on the main one; joined before anything reads Mt.  With the blocked layout the
@@ -221,7 +227,7 @@ struct midagma_solver {
     if (mode == MIDAGMA_MODE_COV) {
       // rhs = ((-mu) cov) @ (I - W)    (linear.py:244); a fast slot leaves the split-K slices
       // for fused_update to sum (its only reader there)
-      enqueue_score_cov(zbuf, d_state, /*sum=*/!(fast && blocked()));
+      if (!gemm_done) enqueue_score_cov(zbuf, d_state, /*sum=*/!(fast && blocked()));
     } else {
       enqueue_data_partial(W.p, d_state, IW.p);
       if (forked_inverse()) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
@@ -238,15 +244,36 @@ struct midagma_solver {
 
   // blocked layout: build_at and the two-level inverse (fast: warm-started diagonal blocks, as
   // one dataflow launch when df_on)
-  void enqueue_build_inverse(bool fast, int passes) {
+  // fuse (nullable): a GEMM the inverse may carry in its last trailing launch; returns whether it did
+  bool enqueue_build_inverse(bool fast, int passes, const GemmSpec* fuse = nullptr) {
     if (fast && df_on) {
       launch_build_at(W.p, D, /*square=*/true, dfw.A[0], D, d, 0.0, d_params, d_state, stream, IW.p);
       launch_df_inverse(Mt.p, D, dfw, binv(), passes <= 2 ? 2 : 3, d_state, stream);
-    } else {
-      launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
-                      stream, IW.p);
-      launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes);
+      return false;
     }
+    launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state, stream,
+                    IW.p);
+    return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse);
+  }
+  bool fuse_gemm = !(getenv("MIDAGMA_EXP_FUSE_GEMM") && atoi(getenv("MIDAGMA_EXP_FUSE_GEMM")) == 0);
+
+  // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
+  GemmSpec score_cov_spec() const {
+    GemmSpec gs{};
+    gs.M = D;
+    gs.N = D;
+    gs.K = Kd();
+    gs.A = cov_at ? covsT.p : covs.p;
+    gs.lda = D;
+    gs.a_trans = cov_at;
+    gs.B = IW.p ? IW.p : W.p;
+    gs.ldb = D;
+    gs.bmode = IW.p ? B_PLAIN : B_IMINUS;
+    gs.C = cov_parts.p;
+    gs.ldc = D;
+    gs.split = cov_split;
+    gs.slice_stride = D * D;
+    return gs;
   }
 
   // rhs = ((-mu) cov) @ (I - W) from the slot's operands: A read k-major from ((-mu) cov)^T

@@ -104,6 +104,13 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_DF={df}", end=" ")
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_DF")
+    if which == "fusecmp":  # the cov score GEMM inside the last trailing launch, or apart
+        for d, K in ((1000, 2000), (500, 2000), (1400, 1000)):
+            for f in ("1", "0"):
+                os.environ["MIDAGMA_EXP_FUSE_GEMM"] = f
+                print(f"MIDAGMA_EXP_FUSE_GEMM={f}", end=" ")
+                cov_case(d, 2 * d, 10, K)
+        os.environ.pop("MIDAGMA_EXP_FUSE_GEMM")
     if which == "d1000short":  # PMC passes: few dispatches
         cov_case(1000, 2000, 10, 40)
     if which == "fit":
