@@ -879,7 +879,9 @@ __global__ __launch_bounds__(NTHREADS) void sum_slices_kernel(const double* __re
 __global__ __launch_bounds__(NTHREADS) void sum_vector_kernel(const double* __restrict__ v, int64_t n,
                                                               double* __restrict__ out,
                                                               const State* __restrict__ st) {
-  if (st && st->status != ST_RUNNING) return;
+  // (with a State: the logistic loss partials, which the sigmoid GEMM writes and the controller
+  // reads on checkpoint slots only)
+  if (st && (st->status != ST_RUNNING || !st->ckpt_pending)) return;
   __shared__ double red[NTHREADS];
   double acc = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += NTHREADS) acc += v[i];
