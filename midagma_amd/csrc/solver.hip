@@ -328,7 +328,7 @@ struct midagma_solver {
     if (!lean) launch_reduce_check(Mt.p, W.p, zbuf, d_params, d_state, partials.p, d, D, stream);
     launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
                    trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream);
-    const bool slices = lean && cov_split > 1;
+    const bool slices = lean && mode == MIDAGMA_MODE_COV && cov_split > 1;
     launch_fused_update(d_params, d_state, W.p, m.p, v.p, Mt.p, slices ? cov_parts.p : zbuf,
                         slices ? cov_split : 1, D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr,
                         trek_on && tcfg.mode == 2 ? Gtrek.p : nullptr, d, D, npart.p, stream);
@@ -1047,6 +1047,17 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     s->split = std::min(split, 32);
     if (s->split > 1) s->Zparts.alloc((size_t)s->split * D * D);
     s->loss_part_count = (s->n_pad / 64) * (D / 64);
+    // small shards run the cov-mode slot structure: the warm-started fast blocked inverse in
+    // sequence with the GEMMs (hand-backs and checkpoint slots on the pivoted path).  Forked beside
+    // GEMMs that fill the chip, the pivoted inverse's 20-odd dependent launches wait for CU slots
+    // and end after the GEMMs (logistic d=1000, n=1e4: 1.01 ms per slot for 0.70 ms of GEMMs);
+    // large shards keep the fork, which hides it (MIDAGMA_EXP_DATA_FAST_ROWS: the row bound)
+    static const int64_t fast_rows =
+        getenv("MIDAGMA_EXP_DATA_FAST_ROWS") ? atoll(getenv("MIDAGMA_EXP_DATA_FAST_ROWS")) : 16384;
+    const int b2 = binv_block(D);
+    const int B2_new = (b2 > 0 && s->n_pad <= fast_rows && s->Malt.p) ? b2 : 0;
+    if (B2_new != s->B2) s->graphs_valid = false;
+    s->B2 = B2_new;
     if (s->loss == MIDAGMA_LOSS_LOGISTIC) {
       s->loss_part.alloc(s->loss_part_count);
       HIP_TRY(hipMemsetAsync(s->loss_part.p, 0, s->loss_part_count * sizeof(double), s->stream));

@@ -528,3 +528,32 @@ def test_mlp_h_func(hip, golden, d, s):
     assert abs(h.item() - float(g[f"h_d{d}_s{s}"])) <= 1e-12 * max(1.0, abs(float(g[f"h_d{d}_s{s}"])))
     grad = model.fc1.weight.grad.detach().cpu().numpy().reshape(-1)[g[f"pick_d{d}"]]
     np.testing.assert_allclose(grad, g[f"gradpick_d{d}_s{s}"], rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.parametrize("d,n", [(300, 2000), (1000, 4000)])
+def test_data_mode_small_shard_fast_inverse(hip, d, n, monkeypatch):
+    """Data-mode shards of <= 16384 rows run the cov-mode slot structure (the warm-started fast
+    blocked inverse in sequence with the GEMMs; pivoted slots at the first step, checkpoints and
+    hand-backs).  l2 against the oracle's reference-algorithm steps (K=130, checkpoints every
+    40: iterations, W and the checkpoint objectives), and against the forked pivoted path
+    (MIDAGMA_EXP_DATA_FAST_ROWS=0)."""
+    X, _, _ = make_dataset(d, n, seed=d + 3)
+    o = _oracle(X)
+    o.checkpoint = 40
+    Xc = o.X
+    K = 130
+    res = {}
+    for rows in ("16384", "0"):
+        monkeypatch.setenv("MIDAGMA_EXP_DATA_FAST_ROWS", rows)
+        s = _solver(d, mode="data")
+        s.set_data(Xc, n_global=n)
+        W = np.zeros((d, d))
+        r = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, checkpoint=40, want_checkpoints=True)
+        res[rows] = (W, r)
+        s.close()
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    (Wf, rf), (Wk, rk) = res["16384"], res["0"]
+    assert rf.iters == rk.iters == tr.iters == K and rf.success
+    assert np.abs(Wf - Wr).max() <= 1e-9 and np.abs(Wf - Wk).max() <= 1e-9
+    for c, (_, obj_r, _, _) in zip(rf.checkpoints, tr.checkpoints):
+        assert abs(c[1] - obj_r) <= 1e-10 * abs(obj_r)
