@@ -176,28 +176,47 @@ def test_full_fit_d20(hip, golden):
 def test_full_fit_d1000_matches_reference_algorithm(hip, golden):
     """BASELINE config 2 end to end: the default fit at d=1000, n=1e4 (ER(s0=d) Gaussian SEM,
     seed 0) against the oracle's run of the reference algorithm (fit_d1000_ref.npz, 2.5 h of
-    CPU; tests/golden/make_fit_d1000.py).  The early-stop checkpoints land differently by a
-    checkpoint or two per stage (the chaos test_full_fit_d20 documents; GPU versions of this
-    round took 53k-56k steps, the oracle 58k), so the check is on the result: the identical
-    thresholded support, the weights on it, h_final and score_final."""
+    CPU; tests/golden/make_fit_d1000.py), with tolerances from the reference's own noise
+    envelope (fit_d1000_envelope.npz, tests/golden/make_fit_d1000_envelope.py: the same fit
+    with 1e-16 relative noise in every inverse, 3 seeds, ~3 h each at one BLAS thread).  The
+    perturbed refits keep the identical 1007-edge support but move W on it by up to 1.9e-2,
+    h_final by 1.7e-9, score_final by 3.7e-6 relative and the early-stop checkpoints of the
+    stages by up to 3000 iterations (the literal 1e-5 after a full fit is below
+    the reference's own reproducibility).  Bar: the identical thresholded support, W on it,
+    h_final and score_final within 2x the envelope's widest deviation from the unperturbed run,
+    and every stage's iteration count inside the envelope's range widened by one checkpoint."""
     from midagma_amd import DagmaLinear
     f = golden("fit_d1000_ref.npz")
+    e = golden("fit_d1000_envelope.npz")
     X, _, _ = make_dataset(1000, 10000, seed=0)
     m = DagmaLinear("l2")
     W = m.fit(X, lambda1=0.03)
-    iters = [e["iters"] for e in m.minimize_log]
+    iters = [e_["iters"] for e_ in m.minimize_log]
     rows, cols = np.nonzero(W)
     gr, gc, gv = f["rows"], f["cols"], f["vals"]
-    dw = float(np.abs(W[gr, gc] - gv).max()) if len(gr) else 0.0
+    ref = np.zeros((1000, 1000))
+    ref[gr, gc] = gv
+    env_w = env_h = env_s = 0.0
+    lo = f["stages"][:, 1].astype(np.int64).copy()
+    hi = lo.copy()
+    for sd in e["seeds"]:
+        Wp = np.zeros((1000, 1000))
+        Wp[e[f"s{sd}_rows"], e[f"s{sd}_cols"]] = e[f"s{sd}_vals"]
+        env_w = max(env_w, float(np.abs(Wp - ref).max()))
+        env_h = max(env_h, abs(float(e[f"s{sd}_h_final"]) - float(f["h_final"])))
+        env_s = max(env_s, abs(float(e[f"s{sd}_score_final"]) - float(f["score_final"])) / float(f["score_final"]))
+        st = e[f"s{sd}_stages"][:, 1]
+        lo, hi = np.minimum(lo, st), np.maximum(hi, st)
+    dw = float(np.abs(W - ref).max())
     ds = abs(m.score_final - float(f["score_final"])) / abs(float(f["score_final"]))
     dh = abs(m.h_final - float(f["h_final"]))
-    print(f"stages gpu {iters} ref {f['stages'][:, 1].tolist()}; nnz {len(rows)} vs {len(gr)}; "
-          f"max|dW| on support {dw:.3e}; score rel {ds:.3e}; h abs {dh:.3e}")
+    print(f"stages gpu {iters} envelope {lo.tolist()}..{hi.tolist()}; nnz {len(rows)} vs {len(gr)}; "
+          f"max|dW| {dw:.3e} (env {env_w:.3e}); score rel {ds:.3e} (env {env_s:.3e}); h abs {dh:.3e} (env {env_h:.3e})")
     assert len(iters) == len(f["stages"])
-    for a, b in zip(iters, f["stages"][:, 1]):
-        assert abs(a - int(b)) <= 3000
+    for a, l_, h_ in zip(iters, lo, hi):
+        assert l_ - 1000 <= a <= h_ + 1000
     assert set(zip(rows.tolist(), cols.tolist())) == set(zip(gr.tolist(), gc.tolist()))
-    assert dw <= 5e-3 and ds <= 2e-5 and dh <= 1e-8
+    assert dw <= 2 * env_w and ds <= 2 * env_s and dh <= 2 * env_h
 
 
 def test_fit_stages_from_reference_start(hip, golden):

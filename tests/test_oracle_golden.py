@@ -126,3 +126,22 @@ def test_mlp_h_func(golden, d, s):
     grad = (2 * w.reshape(d, 10, d) * dA.T[:, None, :]).reshape(d * 10, d)
     np.testing.assert_allclose(grad.reshape(-1)[g[f"pick_d{d}"]], g[f"gradpick_d{d}_s{s}"],
                                rtol=1e-10, atol=1e-14)
+
+
+def test_fit_d1000_envelope_fixture():
+    """fit_d1000_envelope.npz (tests/golden/make_fit_d1000_envelope.py): the oracle's default
+    d=1000 fit refitted with 1e-16 relative noise in every inverse, 3 seeds.  Each refit keeps the
+    unperturbed fit's thresholded support; its W, h_final and score_final deviate by amounts
+    that set the GPU full-fit test's tolerances (tests/test_gpu_parity.py)."""
+    import os
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    f = np.load(os.path.join(here, "fit_d1000_ref.npz"))
+    e = np.load(os.path.join(here, "fit_d1000_envelope.npz"))
+    ref = set(zip(f["rows"].tolist(), f["cols"].tolist()))
+    assert len(e["seeds"]) == 3
+    for s in e["seeds"]:
+        assert set(zip(e[f"s{s}_rows"].tolist(), e[f"s{s}_cols"].tolist())) == ref
+        assert e[f"s{s}_stages"].shape == f["stages"].shape
+        assert np.all(e[f"s{s}_stages"][:, 2] == 1)  # every stage succeeded
+        assert abs(float(e[f"s{s}_h_final"]) - float(f["h_final"])) < 1e-8
+        assert abs(float(e[f"s{s}_score_final"]) / float(f["score_final"]) - 1) < 1e-5
