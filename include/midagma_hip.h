@@ -218,6 +218,13 @@ int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double*
  * epilogue; the GJ on the 32-padded problem). */
 int midagma_logdet_h_dev(const double* A, int64_t d, int64_t lda, double s, double* h_dev, double* Mt_dev, int64_t ldm,
                          void* stream);
+/* The same, enqueued in midagma_logdet_h_parts(d) parts that must be issued in order (part 0:
+ * build and prologue; parts 1 .. ceil(d/32): the Gauss-Jordan block steps; the last: h and
+ * (sI - A)^-T), so a caller can interleave them with other work of its step (DagmaNonlinear's
+ * side-stream log-det).  The parts of one h share a per-device workspace: one h at a time. */
+int64_t midagma_logdet_h_parts(int64_t d);
+int midagma_logdet_h_dev_part(const double* A, int64_t d, int64_t lda, double s, double* h_dev, double* Mt_dev,
+                              int64_t ldm, void* stream, int64_t part);
 int midagma_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
                           double lambda1, double half_d, double inv_n, double* obj, void* stream);
 int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,

@@ -97,6 +97,8 @@ EXPORTED = {
     "midagma_fc1_terms": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "midagma_fc1_terms_bwd": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "midagma_logdet_h_dev": (_int, [_vp, _i64, _i64, _d, _vp, _vp, _i64, _vp]),
+    "midagma_logdet_h_parts": (_i64, [_i64]),
+    "midagma_logdet_h_dev_part": (_int, [_vp, _i64, _i64, _d, _vp, _vp, _i64, _vp, _i64]),
     "midagma_mlp_objective": (_int, [_vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp, _vp]),
     "midagma_mlp_objective_bwd": (_int, [_vp, _vp, _i64, _d, _d, _d, _d, _vp, _vp, _vp, _vp]),
     "midagma_mlp_tail_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),

@@ -370,20 +370,23 @@ void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int6
   HIP_TRY(hipGetLastError());
 }
 
-void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream) {
+void launch_gj_prologue(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream) {
   const int K = (int)(D / NB);
-  double* C0 = w.C;
-  double* C1 = w.C + D * NB;
-  double* R0 = w.R;
-  double* R1 = w.R + NB * D;
-  double* P0 = w.P;
-  double* P1 = w.P + NB * NB;
-  hipLaunchKernelGGL(gj_prologue_kernel, dim3(K), dim3(NTHREADS), 0, stream, A, lda, D, C0, R0, P0, w.pivlog, w.Pstore,
-                     st);
-  for (int k = 0; k < K; ++k)
-    hipLaunchKernelGGL(gj_step_kernel, dim3(K, K), dim3(NTHREADS), 0, stream, A, lda, D, k, C0, C1, R0, R1, P0, P1,
-                       w.pivlog, w.Pstore, st);
+  hipLaunchKernelGGL(gj_prologue_kernel, dim3(K), dim3(NTHREADS), 0, stream, A, lda, D, w.C, w.R, w.P, w.pivlog,
+                     w.Pstore, st);
   HIP_TRY(hipGetLastError());
+}
+
+void launch_gj_step(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, int k, hipStream_t stream) {
+  const int K = (int)(D / NB);
+  hipLaunchKernelGGL(gj_step_kernel, dim3(K, K), dim3(NTHREADS), 0, stream, A, lda, D, k, w.C, w.C + D * NB, w.R,
+                     w.R + NB * D, w.P, w.P + NB * NB, w.pivlog, w.Pstore, st);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream) {
+  launch_gj_prologue(A, lda, D, w, st, stream);
+  for (int k = 0; k < (int)(D / NB); ++k) launch_gj_step(A, lda, D, w, st, k, stream);
 }
 
 }  // namespace midagma

@@ -36,6 +36,9 @@ void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int6
 // In place: A <- inv(A) (unpivoted blocked Gauss-Jordan) on the D x D matrix at A with
 // leading dimension lda (D multiple of 32), pivot logs into w.pivlog.
 void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
+// the same as its parts: the prologue, then block steps k = 0 .. D/32 - 1 in order
+void launch_gj_prologue(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
+void launch_gj_step(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, int k, hipStream_t stream);
 
 // A GEMM launch's arguments (launch_gemm's meaning), for launches that carry one beside other work.
 enum GemmB : int;

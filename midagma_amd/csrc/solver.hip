@@ -1504,34 +1504,64 @@ std::mutex g_ws_mu;
 std::vector<LogdetWorkspace*> g_ws;
 }  // namespace
 
+// the 32-padded workspace of the h log-det for this device (created on first use)
+static LogdetWorkspace* logdet_h_ws(int64_t d) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  const int64_t D = (d + 31) / 32 * 32;  // the 32-block Gauss-Jordan's own granularity
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  for (auto* w : g_ws)
+    if (w->device == dev && w->D == D) return w;
+  LogdetWorkspace* ws = new LogdetWorkspace();
+  ws->device = dev;
+  ws->D = D;
+  ws->A.alloc((size_t)D * D);
+  ws->P.alloc(64 * 64);
+  ws->R.alloc((size_t)64 * D);
+  ws->C.alloc((size_t)D * 64);
+  ws->piv.alloc(D);
+  g_ws.push_back(ws);
+  return ws;
+}
+
+// part 0: build + the Gauss-Jordan prologue; parts 1 .. D/32: its block steps; part D/32 + 1: the
+// epilogue (h and (sI - A)^-T).  part < 0: all of them.
+static void logdet_h_enqueue(const double* A, int64_t d, int64_t lda, double s, double* h_dev, double* Mt_dev,
+                             int64_t ldm, hipStream_t st, int part) {
+  setup_attributes_once();
+  LogdetWorkspace* ws = logdet_h_ws(d);
+  const int64_t D = ws->D;
+  const int K = (int)(D / 32);
+  const GJWork w{ws->P.p, ws->R.p, ws->C.p, ws->piv.p};
+  if (part < 0 || part == 0) {
+    launch_build_at(A, lda, false, ws->A.p, D, d, s, nullptr, nullptr, st);
+    launch_gj_prologue(ws->A.p, D, D, w, nullptr, st);
+  }
+  for (int k = 0; k < K; ++k)
+    if (part < 0 || part == k + 1) launch_gj_step(ws->A.p, D, D, w, nullptr, k, st);
+  if (part < 0 || part == K + 1)
+    launch_logdet_post(ws->piv.p, d, (double)d * std::log(s), h_dev, ws->A.p, D, Mt_dev, ldm, st);
+}
+
 extern "C" int midagma_logdet_h_dev(const double* A, int64_t d, int64_t lda, double s, double* h_dev, double* Mt_dev,
                                     int64_t ldm, void* stream) {
   if (!A || !h_dev || d < 1 || lda < d || !(s > 0.0) || (Mt_dev && ldm < d))
     return fail(nullptr, MIDAGMA_E_ARG, "logdet_h_dev: bad arguments");
   return guarded(nullptr, [&] {
-    setup_attributes_once();
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    const int64_t D = (d + 31) / 32 * 32;  // the 32-block Gauss-Jordan's own granularity
-    std::lock_guard<std::mutex> lock(g_ws_mu);
-    LogdetWorkspace* ws = nullptr;
-    for (auto* w : g_ws)
-      if (w->device == dev && w->D == D) ws = w;
-    if (!ws) {
-      ws = new LogdetWorkspace();
-      ws->device = dev;
-      ws->D = D;
-      ws->A.alloc((size_t)D * D);
-      ws->P.alloc(64 * 64);
-      ws->R.alloc((size_t)64 * D);
-      ws->C.alloc((size_t)D * 64);
-      ws->piv.alloc(D);
-      g_ws.push_back(ws);
-    }
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    launch_build_at(A, lda, false, ws->A.p, D, d, s, nullptr, nullptr, st);
-    launch_gj_inverse(ws->A.p, D, D, GJWork{ws->P.p, ws->R.p, ws->C.p, ws->piv.p}, nullptr, st);
-    launch_logdet_post(ws->piv.p, d, (double)d * std::log(s), h_dev, ws->A.p, D, Mt_dev, ldm, st);
+    logdet_h_enqueue(A, d, lda, s, h_dev, Mt_dev, ldm, reinterpret_cast<hipStream_t>(stream), -1);
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int64_t midagma_logdet_h_parts(int64_t d) { return d < 1 ? 0 : (d + 31) / 32 + 2; }
+
+extern "C" int midagma_logdet_h_dev_part(const double* A, int64_t d, int64_t lda, double s, double* h_dev,
+                                         double* Mt_dev, int64_t ldm, void* stream, int64_t part) {
+  if (!A || !h_dev || d < 1 || lda < d || !(s > 0.0) || (Mt_dev && ldm < d) || part < 0 ||
+      part >= midagma_logdet_h_parts(d))
+    return fail(nullptr, MIDAGMA_E_ARG, "logdet_h_dev_part: bad arguments");
+  return guarded(nullptr, [&] {
+    logdet_h_enqueue(A, d, lda, s, h_dev, Mt_dev, ldm, reinterpret_cast<hipStream_t>(stream), (int)part);
     return MIDAGMA_OK;
   });
 }

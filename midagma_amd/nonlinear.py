@@ -133,7 +133,7 @@ class _MLPObjective(torch.autograd.Function):
         scratch = torch.empty(int(L.midagma_mlp_tail_scratch(n, d, m1)), **f64)
         ssq = torch.empty((), **f64)
         obj = torch.empty((), **f64)
-        ctx.ev_done = None
+        ctx.chain = None
         with torch.cuda.device(dev):
             _lib.check(L.midagma_fc1_terms(_vp(W1), d, m1, _vp(A), _vp(l1part), st), None, "fc1_terms")
             if overlap:
@@ -143,26 +143,23 @@ class _MLPObjective(torch.autograd.Function):
                 # value; the side stream also forms the objective once the tail's ssq is ready,
                 # and backward joins before the fc1 terms' backward needs (sI - A)^-T.  Only for
                 # callers that run backward right away (DagmaNonlinear.minimize): the join is there.
-                # (capture order matters in the replayed graph: the log-det chain captured first
-                # measured 5215 steps/s at config 5, the tail first 3817, one stream 4943)
+                # Its parts are enqueued between the main stream's launches (a replayed graph
+                # submits nodes in capture order, ~4 us each: a branch captured whole ahead of the
+                # other holds the other back by its whole submission time).
                 main = torch.cuda.current_stream(dev)
                 side = _side_stream(dev)
                 ev_fc1 = torch.cuda.Event()
                 ev_fc1.record(main)
                 side.wait_event(ev_fc1)
-                ss = C.c_void_p(side.cuda_stream)
-                _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, ss), None,
-                           "logdet_h_dev")
+                chain = _SideLogdet(L, side, A, d, float(s), h, Mt)
+                chain.enqueue(1)
                 _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
                                                   _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
                 ev_tail = torch.cuda.Event()
                 ev_tail.record(main)
-                side.wait_event(ev_tail)
-                _lib.check(L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(h), float(mu),
-                                                   float(lambda1), 0.5 * d, 1 / n, _vp(obj), ss), None,
-                           "mlp_objective")
-                ctx.ev_done = torch.cuda.Event()
-                ctx.ev_done.record(side)
+                chain.enqueue(2)
+                chain.objective = (ev_tail, ssq, l1part, float(mu), float(lambda1), 0.5 * d, 1 / n, obj)
+                ctx.chain = chain
                 ctx.keep = (A, l1part)  # read on the side stream: alive until the join
             else:
                 _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None,
@@ -191,13 +188,18 @@ class _MLPObjective(torch.autograd.Function):
         dZ = torch.empty_like(Z)
         dw2, db2, db1 = torch.empty_like(w2), torch.empty((d, 1), **f64), torch.empty(d * m1, **f64)
         dW1 = torch.empty_like(W1)
+        chain = ctx.chain
         with torch.cuda.device(dev):
             _lib.check(L.midagma_mlp_objective_bwd(_vp(g), _vp(ssq), np_, mu, lambda1, 0.5 * d, 1 / n, _vp(gssq),
                                                    _vp(gl1), _vp(gh), st), None, "mlp_objective_bwd")
+            if chain is not None:
+                chain.enqueue(2)
             if gh_out is not None:  # h is also an output (the Adam gate): its own gradient adds in
                 gh = gh + gh_out
             _lib.check(L.midagma_mlp_tail_bwd(_vp(Z), _vp(b1), _vp(w2), _vp(R), _vp(gssq), n, d, m1, _vp(dZ),
                                               _vp(dw2), _vp(db2), _vp(db1), _vp(scratch), st), None, "mlp_tail_bwd")
+            if chain is not None:
+                chain.enqueue(2)
             if n % 4 == 0 and n >= 64:
                 r = n // 4
                 lin = torch.bmm(dZ.view(4, r, -1).transpose(1, 2), X.view(4, r, -1))  # (4, d m1, d)
@@ -205,14 +207,46 @@ class _MLPObjective(torch.autograd.Function):
             else:
                 lin = (dZ.t() @ X).contiguous()
                 nlin = 1
-            if ctx.ev_done is not None:  # join the side stream's log-det and objective
-                torch.cuda.current_stream(dev).wait_event(ctx.ev_done)
+            if chain is not None:  # the rest of the chain and the objective, then join
+                torch.cuda.current_stream(dev).wait_event(chain.finish())
+                ctx.chain = None
             _lib.check(L.midagma_fc1_terms_bwd(_vp(W1), d, m1, _vp(Mt), _vp(gh), _vp(gl1), _vp(lin), nlin,
                                                _vp(dW1), st), None, "fc1_terms_bwd")
         return None, dW1, db1, dw2, db2, None, None, None, None, None, None
 
 
 _SIDE: dict = {}
+
+
+class _SideLogdet:
+    """The h log-det (midagma_logdet_h_dev_part) enqueued part by part on a side stream, then the
+    scalar objective once the tail's ssq is ready (objective = (event, ssq, l1part, mu, lambda1,
+    half_d, inv_n, out))."""
+
+    def __init__(self, L, side, A, d, s, h, Mt):
+        self.L, self.side, self.A, self.d, self.s, self.h, self.Mt = L, side, A, d, s, h, Mt
+        self.parts = int(L.midagma_logdet_h_parts(d))
+        self.next = 0
+        self.objective = None
+
+    def enqueue(self, k):
+        ss = C.c_void_p(self.side.cuda_stream)
+        while k > 0 and self.next < self.parts:
+            _lib.check(self.L.midagma_logdet_h_dev_part(_vp(self.A), self.d, self.d, self.s, _vp(self.h), _vp(self.Mt),
+                                                        self.d, ss, self.next), None, "logdet_h_dev_part")
+            self.next += 1
+            k -= 1
+
+    def finish(self) -> torch.cuda.Event:
+        self.enqueue(self.parts)
+        ev_tail, ssq, l1part, mu, lambda1, half_d, inv_n, out = self.objective
+        self.side.wait_event(ev_tail)
+        _lib.check(self.L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(self.h), mu, lambda1,
+                                                half_d, inv_n, _vp(out), C.c_void_p(self.side.cuda_stream)), None,
+                   "mlp_objective")
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        return ev
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
