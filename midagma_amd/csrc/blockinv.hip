@@ -319,7 +319,12 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     if (mb > 0) {
       // large D: 128 x 128 tiles (operand reuse; enough tiles to fill the chip), else 32 x 32
       if (D - B2 >= TRAIL128_MIN) {
-        launch_trail128(Ain, Aout, D, B2, g, check, st, stream);
+        if (fuse && fast && g == K2 - 1 && gemm_trail_supported(*fuse)) {
+          launch_gemm_trail(*fuse, Ain, Aout, D, B2, g, check, st, t32_pf(), -1, stream);
+          fused = true;
+        } else {
+          launch_trail128(Ain, Aout, D, B2, g, check, st, stream);
+        }
       } else if (fuse && fast && g == K2 - 1 && gemm_trail_supported(*fuse)) {
         launch_gemm_trail(*fuse, Ain, Aout, D, B2, g, check, st, t32_pf(), mb * mb, stream);
         fused = true;

@@ -625,6 +625,31 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_trail_kernel(GemmTrailArgs a
   }
 }
 
+// The same pairing at large D, where the trailing update itself runs on the 128-tile GEMM
+// (launch_trail128): the score GEMM's tiles, then the band-skipping C0 - A B tiles.
+struct Gemm2Args {
+  GemmTrailArgs g;  // the score GEMM (its trailing-update fields unused)
+  int tm2;          // trailing tiles per dimension: (D - B2) / 128
+};
+
+template <int AMODE, int BMODE>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_trail128_kernel(Gemm2Args a2) {
+  const GemmTrailArgs& a = a2.g;
+  if (a.st->status != ST_RUNNING) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x;
+  if (b < a.n_gemm) {
+    gemm_pipe_tile<AMODE, BMODE, EPI_STORE>(xcd_remap(b, a.n_gemm), a.K, a.kslice, a.tm, a.tn, a.A, a.lda, a.B, a.ldb,
+                                            a.C, a.ldc, a.slice_stride, nullptr, 0, 0, a.st, smem);
+  } else {
+    const int64_t G0 = (int64_t)a.g * a.B2;
+    gemm_pipe_tile<0, B_PLAIN, EPI_SUB_BAND>(xcd_remap(b - a.n_gemm, (int)gridDim.x - a.n_gemm), a.B2, a.B2, a2.tm2,
+                                             a2.tm2, a.Ain + G0, a.D, a.Aout + G0 * a.D, a.D, a.Aout, a.D,
+                                             (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, a.B2 / 128, a.st,
+                                             smem);
+  }
+}
+
 constexpr size_t kGemmLds = (2 * 64 * SB) * sizeof(double);
 
 template <bool AT, int BM, int EP>
@@ -649,6 +674,8 @@ template <int AM, int BM>
 static void set_attr_gt() {
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_trail_kernel<AM, BM>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmTrailLds));
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_trail128_kernel<AM, BM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmPipeLds));
 }
 
 void gemm_setup_attributes() {
@@ -777,6 +804,7 @@ bool gemm_trail_supported(const GemmSpec& gs) {
          getenv("MIDAGMA_EXP_GEMM64") == nullptr && getenv("MIDAGMA_EXP_NO_PIPE") == nullptr;
 }
 
+// n_trail < 0: the trailing update of the 128-tile kind (launch_trail128's grid)
 void launch_gemm_trail(const GemmSpec& gs, const double* Ain, double* Aout, int64_t D, int B2, int g, bool check,
                        State* st, int pf, int n_trail, hipStream_t stream) {
   if (!gemm_trail_supported(gs)) throw std::invalid_argument("launch_gemm_trail: shape");
@@ -804,6 +832,24 @@ void launch_gemm_trail(const GemmSpec& gs, const double* Ain, double* Aout, int6
   a.check = check ? 1 : 0;
   a.pf = pf;
   a.st = st;
+  if (n_trail < 0) {
+    if (D % 128 || B2 % 128) throw std::invalid_argument("launch_gemm_trail: D, B2 must be multiples of 128");
+    Gemm2Args a2{a, (int)((D - B2) / 128)};
+    const dim3 grid2((unsigned)(a.n_gemm + a2.tm2 * a2.tm2));
+#define MIDAGMA_GT2(AM, BM) \
+  hipLaunchKernelGGL((gemm_trail128_kernel<AM, BM>), grid2, dim3(NTHREADS), kGemmPipeLds, stream, a2)
+    if (gs.a_trans && gs.bmode == B_PLAIN)
+      MIDAGMA_GT2(1, B_PLAIN);
+    else if (gs.a_trans)
+      MIDAGMA_GT2(1, B_IMINUS);
+    else if (gs.bmode == B_PLAIN)
+      MIDAGMA_GT2(0, B_PLAIN);
+    else
+      MIDAGMA_GT2(0, B_IMINUS);
+#undef MIDAGMA_GT2
+    HIP_TRY(hipGetLastError());
+    return;
+  }
   const dim3 grid((unsigned)(a.n_gemm + n_trail));
 #define MIDAGMA_GT(AM, BM) \
   hipLaunchKernelGGL((gemm_trail_kernel<AM, BM>), grid, dim3(NTHREADS), kGemmTrailLds, stream, a)

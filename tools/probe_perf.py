@@ -105,7 +105,8 @@ if __name__ == "__main__":
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_DF")
     if which == "fusecmp":  # the cov score GEMM inside the last trailing launch, or apart
-        for d, K in ((1000, 2000), (500, 2000), (1400, 1000)):
+        big = len(sys.argv) > 2 and sys.argv[2] == "big"
+        for d, K in (((2000, 200), (5000, 30)) if big else ((1000, 2000), (500, 2000), (1400, 1000))):
             for f in ("1", "0"):
                 os.environ["MIDAGMA_EXP_FUSE_GEMM"] = f
                 print(f"MIDAGMA_EXP_FUSE_GEMM={f}", end=" ")
