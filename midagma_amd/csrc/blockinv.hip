@@ -250,6 +250,10 @@ __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __re
 static const int64_t TRAIL128_MIN = getenv("MIDAGMA_EXP_TRAIL128") ? atoll(getenv("MIDAGMA_EXP_TRAIL128")) : 1792;
 
 int binv_block(int64_t D) {
+  // D = 128 (64 < d <= 128): one outer block, so the fast slot's whole inverse is the warm-started
+  // product form (3 launches instead of the Gauss-Jordan's prologue and 4 block steps)
+  static const bool b128 = !(getenv("MIDAGMA_EXP_BINV128") && atoi(getenv("MIDAGMA_EXP_BINV128")) == 0);
+  if (D == 128) return b128 ? 128 : 0;
   if (D < 256 || D % 128 != 0) return 0;  // fast path not available: plain GJ
   return D % 256 == 0 ? 256 : 128;
 }

@@ -112,6 +112,10 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_FUSE_GEMM={f}", end=" ")
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_FUSE_GEMM")
+    if which == "b128":  # 64 < d <= 128 (run with MIDAGMA_EXP_BINV128=0 / 1: read once per process)
+        for d in (65, 100, 128):
+            print(f"MIDAGMA_EXP_BINV128={os.environ.get('MIDAGMA_EXP_BINV128', '1')}", end=" ")
+            cov_case(d, 2000, 20, 5000)
     if which == "d1000short":  # PMC passes: few dispatches
         cov_case(1000, 2000, 10, 40)
     if which == "fit":
