@@ -115,7 +115,7 @@ int midagma_begin(midagma_solver* s, const double* W, double mu, int64_t max_ite
                   double tol, double beta1, double beta2, double lambda1, int64_t checkpoint);
 int midagma_step_partial(midagma_solver* s);
 /* enqueue n whole slots (part 1 + part 2); midagma_sync waits.  Without host polling,
- * except in cov mode with the blocked inverse (d > 192), where the host picks the fast or
+ * except in cov mode with the blocked inverse (d > 64, D = 128 or a multiple of 128 from 256), where the host picks the fast or
  * the GJ path per batch (one sync per batch of <= 64 slots). */
 int midagma_run_slots(midagma_solver* s, int64_t n);
 int midagma_sync(midagma_solver* s);

@@ -1,5 +1,5 @@
 // Two-level blocked Gauss-Jordan inverse of sI - W∘W (transposed), the cov-mode slot's
-// replacement for `sla.inv(s*I - W*W)` (linear.py:226, 240) when d > 192.
+// replacement for `sla.inv(s*I - W*W)` (linear.py:226, 240) when D = 128 or D >= 256 (D % 128 == 0).
 //
 // Outer block Gauss-Jordan over B2-wide pivot blocks (B2 = 256, or 128 when 256 does not
 // divide D).  Outer step g sweeps pivot block G = [g B2, (g+1) B2):

@@ -930,7 +930,12 @@ int midagma_create(midagma_solver** out, int loss, int mode, int64_t d, int devi
   s->loss = loss;
   s->mode = mode;
   s->d = d;
-  s->D = d > 192 ? (d + 127) / 128 * 128 : round_up64(d);  // 128-multiples feed the 128x128 GEMM tiles
+  // 128-multiples feed the 128x128 GEMM tiles.  Cov mode pads 129 <= d <= 192 to 256 as well: the
+  // blocked inverse then has one 256-wide outer block, and its warm-started product form beats
+  // the flat Gauss-Jordan's 6 block steps on 192 (data mode keeps 192: X's columns are GEMM work)
+  const char* p256 = getenv("MIDAGMA_EXP_COV_PAD256");
+  const bool pad256 = mode == MIDAGMA_MODE_COV && !(p256 && atoi(p256) == 0);
+  s->D = d > 192 || (pad256 && d > 128) ? (d + 127) / 128 * 128 : round_up64(d);
   s->device = device;
   int rc = guarded(s, [&] {
     setup_attributes_once();

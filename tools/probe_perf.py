@@ -116,6 +116,13 @@ if __name__ == "__main__":
         for d in (65, 100, 128):
             print(f"MIDAGMA_EXP_BINV128={os.environ.get('MIDAGMA_EXP_BINV128', '1')}", end=" ")
             cov_case(d, 2000, 20, 5000)
+    if which == "pad256":  # 128 < d <= 192 in cov mode: D = 256 (one-block fast path) or 192 (flat GJ)
+        for d in (129, 150, 192):
+            for f in ("1", "0"):
+                os.environ["MIDAGMA_EXP_COV_PAD256"] = f
+                print(f"MIDAGMA_EXP_COV_PAD256={f}", end=" ")
+                cov_case(d, 2000, 20, 3000)
+        os.environ.pop("MIDAGMA_EXP_COV_PAD256")
     if which == "d1000short":  # PMC passes: few dispatches
         cov_case(1000, 2000, 10, 40)
     if which == "fit":
