@@ -1,4 +1,4 @@
-// Small-d cov-mode inner loop in ONE persistent workgroup (d <= 32, l2, no trek regularizer).
+// Small-d cov-mode inner loop in ONE persistent workgroup (d <= 64, l2, no trek regularizer).
 //
 // At d = 20 a graph-replayed slot is 8 dependent launches of a 64 x 64 padded problem, each
 // 4-6 us (profiles/r01_rocprof_cov_small_kernel_stats.csv): the GPU ran the reference's loop
@@ -22,7 +22,7 @@
 // Element ownership follows the f64 16x16x4 MFMA accumulator map, so every product's output
 // lands in the registers of the lane that owns the element: wave w owns the 16 x 16 tile
 // (w / (DS/16), w % (DS/16)); lane l owns column 16 tc + (l & 15), rows 16 tr + (l >> 4) + 4 t
-// for t = 0..3.  DS = 16, 32 -> 1, 4 waves.
+// for t = 0..3.  DS = 16, 32, 64 -> 1, 4, 16 waves.
 // Arithmetic per element is step.hip's, in the same order (built with -ffp-contract=off).
 #include "launch.h"
 #include "mfma64.h"
@@ -54,6 +54,13 @@ __device__ __forceinline__ int cpos(int i) { return (i & ~15) + 4 * (i & 3) + ((
 template <int DS, int SA_, int SB_>
 __device__ __forceinline__ dbl4 tile_mma(const double* __restrict__ A, const double* __restrict__ B, int row0,
                                          int col0, int q, int c, int kd, dbl4 acc) {
+  if (DS >= 64) {  // (a full unroll keeps 32 operands in flight: the 1024-thread kernel's registers spill)
+#pragma unroll 4
+    for (int kk = 0; 4 * kk < kd; ++kk)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(row0 + c) * SA_ + 4 * kk + q], B[(4 * kk + q) * SB_ + col0 + c],
+                                                 acc, 0, 0, 0);
+    return acc;
+  }
 #pragma unroll
   for (int kk = 0; kk < DS / 4; ++kk)
     if (4 * kk < kd)
@@ -193,7 +200,14 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   static_assert(TPW * NW == TPR * TPR, "whole tiles per wave");
   constexpr int SW = DS + 2;                         // W, cov images: 16 rows x 4 cols per read
   constexpr int SI = ((DS + 15) / 32) * 32 + 16;     // I - W image: B operand rows, = 16 mod 32
-  __shared__ double Wimg[DS * SW];
+  // DS = 64: the images are single-buffered (an extra barrier before each rewrite), R / Q serve
+  // as A and B operand from one [m][k] image, and W is not imaged (its transpose is read from
+  // the I - W image, whose off-diagonal entries are -W exactly, the diagonal from wdiag): 4
+  // images of 64 x 66 / 64 x 80 doubles fit the CU's 160 KB of LDS
+  constexpr bool ONE = DS >= 64;
+  constexpr int SB = ONE ? SW : SI;                  // stride of the product form's B images
+  __shared__ double Wimg[ONE ? 1 : DS * SW];
+  __shared__ double wdiag[DS];
   __shared__ double Cimg[DS * SW];
   __shared__ double IWimg[DS * SI];
   __shared__ __attribute__((aligned(32))) double rowb[2][DS];
@@ -201,9 +215,12 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   __shared__ double piv[DS];
   // product-form inverse operands, two sets: [m][k] images (PA: the left factor, PR: R as a
   // left factor) and [k][n] images (PB)
-  __shared__ double PA[2][DS * SW];
-  __shared__ double PR[2][DS * SW];
-  __shared__ double PB[2][DS * SI];
+  __shared__ double PAbuf[(ONE ? 1 : 2) * DS * SW];
+  __shared__ double PRbuf[(ONE ? 1 : 2) * DS * SW];
+  __shared__ double PBbuf[ONE ? 1 : 2 * DS * SI];
+  double* const PA[2] = {PAbuf, ONE ? PAbuf : PAbuf + DS * SW};
+  double* const PR[2] = {PRbuf, ONE ? PRbuf : PRbuf + DS * SW};
+  double* const PB[2] = {ONE ? PRbuf : PBbuf, ONE ? PRbuf : PBbuf + DS * SI};
   __shared__ double nrm[NW];
   __shared__ double red[3][NW];               // checkpoint objective: (I - W) o Z, |W|, log|pivot|
   __shared__ double nred[NORM_FIELDS][NW];    // the checkpoint step's norms, per wave
@@ -252,14 +269,17 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     const int r = e / SW, k = e % SW;
     Cimg[e] = (r < di && k < di) ? covs[(int64_t)r * D + k] : 0.0;
   }
-  for (int e = tid; e < DS * SW; e += NT) Wimg[e] = 0.0;
+  if (!ONE)
+    for (int e = tid; e < DS * SW; e += NT) Wimg[e] = 0.0;
+  for (int e = tid; e < DS; e += NT) wdiag[e] = 0.0;
   for (int e = tid; e < DS * SI; e += NT) IWimg[e] = 0.0;
   __syncthreads();
   if (!ctl.run) return;
 #pragma unroll
   for (int e = 0; e < E; ++e)
     if (real[e]) {
-      Wimg[rows[e] * SW + cols[e]] = wv[e];
+      if (!ONE) Wimg[rows[e] * SW + cols[e]] = wv[e];
+      if (rows[e] == cols[e]) wdiag[rows[e]] = wv[e];
       IWimg[rows[e] * SI + cols[e]] = ((rows[e] == cols[e]) ? 1.0 : 0.0) - wv[e];
     }
   const double s_dom = pr->s;
@@ -290,7 +310,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     for (int e = 0; e < E; ++e) {
       const int i = rows[e], j = cols[e];
       if (real[e]) {
-        const double wji = Wimg[j * SW + i];
+        const double wji = ONE ? (i == j ? wdiag[i] : -IWimg[j * SI + i]) : Wimg[j * SW + i];
         a[e] = ((i == j) ? s_dom : 0.0) - wji * wji;
       } else {
         a[e] = (i == j) ? 1.0 : 0.0;
@@ -310,12 +330,12 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
         const int i = rows[e], j = cols[e];
         x0[e] = real[e] ? (warm >= 2 ? 2.0 * p1[e] - p2[e] : p1[e]) : ((i == j) ? 1.0 : 0.0);
         PA[1][i * SW + j] = a[e];
-        PB[1][i * SI + j] = x0[e];
+        PB[1][i * SB + j] = x0[e];
       }
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < TPW; ++u) {
-        const dbl4 t4 = tile_mma<DS, SW, SI>(PA[1], PB[1], 16 * tr[u], cols[4 * u] - c, q, c, di,
+        const dbl4 t4 = tile_mma<DS, SW, SB>(PA[1], PB[1], 16 * tr[u], cols[4 * u] - c, q, c, di,
                                              dbl4{0.0, 0.0, 0.0, 0.0});
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -325,10 +345,11 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
           mx = ar != ar ? INFINITY : fmax(mx, ar);
         }
       }
+      if (ONE) __syncthreads();  // every wave is done reading the images it overwrites
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         PA[0][rows[e] * SW + cols[e]] = x0[e];
-        PB[0][rows[e] * SI + cols[e]] = r[e];
+        PB[0][rows[e] * SB + cols[e]] = r[e];
         PR[0][rows[e] * SW + cols[e]] = r[e];
       }
       mx = wave_max(mx);
@@ -344,9 +365,9 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
           const int row0 = 16 * tr[u], col0 = cols[4 * u] - c;
-          const dbl4 yv = tile_mma<DS, SW, SI>(PA[0], PB[0], row0, col0, q, c, di,
+          const dbl4 yv = tile_mma<DS, SW, SB>(PA[0], PB[0], row0, col0, q, c, di,
                                                dbl4{x0[4 * u], x0[4 * u + 1], x0[4 * u + 2], x0[4 * u + 3]});
-          const dbl4 rv = tile_mma<DS, SW, SI>(PR[0], PB[0], row0, col0, q, c, di, dbl4{0.0, 0.0, 0.0, 0.0});
+          const dbl4 rv = tile_mma<DS, SW, SB>(PR[0], PB[0], row0, col0, q, c, di, dbl4{0.0, 0.0, 0.0, 0.0});
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const int e = 4 * u + t;
@@ -354,20 +375,21 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
             r2[e] = real[e] ? rv[t] : 0.0;
           }
         }
+        if (ONE) __syncthreads();
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           PA[1][rows[e] * SW + cols[e]] = y[e];
-          PB[1][rows[e] * SI + cols[e]] = r2[e];
+          PB[1][rows[e] * SB + cols[e]] = r2[e];
           if (three) PR[1][rows[e] * SW + cols[e]] = r2[e];
         }
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
           const int row0 = 16 * tr[u], col0 = cols[4 * u] - c;
-          const dbl4 yv = tile_mma<DS, SW, SI>(PA[1], PB[1], row0, col0, q, c, di,
+          const dbl4 yv = tile_mma<DS, SW, SB>(PA[1], PB[1], row0, col0, q, c, di,
                                                dbl4{y[4 * u], y[4 * u + 1], y[4 * u + 2], y[4 * u + 3]});
           dbl4 rv = dbl4{0.0, 0.0, 0.0, 0.0};
-          if (three) rv = tile_mma<DS, SW, SI>(PR[1], PB[1], row0, col0, q, c, di, rv);
+          if (three) rv = tile_mma<DS, SW, SB>(PR[1], PB[1], row0, col0, q, c, di, rv);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const int e = 4 * u + t;
@@ -376,15 +398,16 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
           }
         }
         if (three) {
+          if (ONE) __syncthreads();
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             PA[0][rows[e] * SW + cols[e]] = y[e];
-            PB[0][rows[e] * SI + cols[e]] = r2[e];
+            PB[0][rows[e] * SB + cols[e]] = r2[e];
           }
           __syncthreads();
 #pragma unroll
           for (int u = 0; u < TPW; ++u) {
-            const dbl4 yv = tile_mma<DS, SW, SI>(PA[0], PB[0], 16 * tr[u], cols[4 * u] - c, q, c, di,
+            const dbl4 yv = tile_mma<DS, SW, SB>(PA[0], PB[0], 16 * tr[u], cols[4 * u] - c, q, c, di,
                                                  dbl4{y[4 * u], y[4 * u + 1], y[4 * u + 2], y[4 * u + 3]});
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -557,7 +580,8 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
           wv[e] = wo + lr_a * gd;
         }
       }
-      Wimg[rows[e] * SW + cols[e]] = wv[e];
+      if (!ONE) Wimg[rows[e] * SW + cols[e]] = wv[e];
+      if (rows[e] == cols[e]) wdiag[rows[e]] = wv[e];
       IWimg[rows[e] * SI + cols[e]] = ((rows[e] == cols[e]) ? 1.0 : 0.0) - wv[e];
     }
     if (norms) {
@@ -602,24 +626,29 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 
 }  // namespace
 
-// d <= 32 (the operand images of the product form outgrow the LDS at DS = 64, and the
-// Gauss-Jordan-only kernel measured slower than the graph-replayed slots for 32 < d <= 64)
-int small_block(int64_t d) { return d <= 16 ? 16 : (d <= 32 ? 32 : 0); }
+// d <= 64 (DS = 64: single-buffered images, 16 waves; MIDAGMA_EXP_SMALL64=0 keeps 32 < d <= 64 on
+// the graph-replayed slots)
+int small_block(int64_t d) {
+  static const bool s64 = !(getenv("MIDAGMA_EXP_SMALL64") && atoi(getenv("MIDAGMA_EXP_SMALL64")) == 0);
+  return d <= 16 ? 16 : (d <= 32 ? 32 : (d <= 64 && s64 ? 64 : 0));
+}
 
 void launch_small_minimize(const Params* pr, State* st, double* W, double* m, double* v, const double* covs,
                            const double* minc, const double* mexc, const double* bc_table, CkptRec* ckpt,
                            int64_t ckpt_cap, double* carry, double* pstore, int64_t d, int64_t n_slots,
                            hipStream_t stream) {
   const int ds = small_block(d);
-  if (ds == 0) throw std::invalid_argument("small_minimize: d > 32");
+  if (ds == 0) throw std::invalid_argument("small_minimize: d > 64");
 #define MIDAGMA_SMALL(DS_, NW_)                                                                                  \
   hipLaunchKernelGGL((small_minimize_kernel<DS_, NW_>), dim3(1), dim3(64 * NW_), 0, stream, pr, st, W, m, v, covs, \
                      minc, mexc, bc_table, ckpt, ckpt_cap, carry, pstore, n_slots)
   // one wave per 16 x 16 tile
   if (ds == 16)
     MIDAGMA_SMALL(16, 1);
-  else
+  else if (ds == 32)
     MIDAGMA_SMALL(32, 4);
+  else
+    MIDAGMA_SMALL(64, 16);
 #undef MIDAGMA_SMALL
   HIP_TRY(hipGetLastError());
 }

@@ -520,7 +520,7 @@ struct midagma_solver {
     HIP_TRY(hipMemsetAsync(npart.p, 0, npart.n * sizeof(double), stream));
     scarry.alloc(NORM_FIELDS + 1);
     HIP_TRY(hipMemsetAsync(scarry.p, 0, scarry.n * sizeof(double), stream));
-    if (small_block(d) > 0) sprev.alloc(2 * 32 * 32);
+    if (small_block(d) > 0) sprev.alloc(2 * (size_t)small_block(d) * small_block(d));
     if (D % 128 == 0) {
       // split-K of the cov score GEMM: small grids get slices to fill the chip; large ones the
       // split that best rounds the last wave of 128-tiles (2 workgroups per CU resident:

@@ -1,4 +1,4 @@
-"""The one-workgroup small-d inner loop (csrc/small.hip: cov mode, l2, d <= 32) against the
+"""The one-workgroup small-d inner loop (csrc/small.hip: cov mode, l2, d <= 64) against the
 oracle (the numpy/scipy restatement of linear.py:165-333), against the graph-replayed slot
 path it replaces (MIDAGMA_EXP_NO_SMALL), and across launch boundaries (run_slots chunks that
 end right after a checkpoint step, so the pending checkpoint norms cross launches)."""
@@ -42,7 +42,7 @@ def _check_records(res, tr):
             assert abs(got - want) <= 1e-9 * max(1.0, abs(want)), (c.iter, f, got, want)
 
 
-@pytest.mark.parametrize("d", [1, 4, 16, 17, 20, 31, 32, 33])
+@pytest.mark.parametrize("d", [1, 4, 16, 17, 20, 31, 32, 33, 48, 64])
 def test_small_path_matches_oracle(d):
     o = _oracle(d)
     K = 300
@@ -92,7 +92,7 @@ def test_small_path_line_search_branches(golden):
         s.close()
 
 
-@pytest.mark.parametrize("d", [20, 32])
+@pytest.mark.parametrize("d", [20, 32, 64])
 def test_small_path_launch_boundaries_bit_identical(d):
     """run_slots in chunks of 50 with checkpoint = 50: every launch ends right after a
     checkpoint step, so the step's norms cross to the next launch.  Same kernel arithmetic:
@@ -119,7 +119,7 @@ def test_small_path_launch_boundaries_bit_identical(d):
     b.close()
 
 
-@pytest.mark.parametrize("d", [5, 20, 32])
+@pytest.mark.parametrize("d", [5, 20, 32, 50, 64])
 def test_small_path_vs_graph_path(d, monkeypatch):
     """The persistent kernel and the graph-replayed slots (MIDAGMA_EXP_NO_SMALL) agree to
     rounding: same iterations, W within 1e-11 after 500 steps (checkpoint every 100: Gauss-Jordan
