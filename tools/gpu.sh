@@ -31,6 +31,14 @@ leg_args() {
   esac
 }
 
+# workload tag bench.py matches when it reads the committed PMC summary (data leg only)
+pmc_workload() {
+  case "$1" in
+    data) echo '{"d": 1000, "n": 1000000, "world": 1, "command": "tools/gpu.sh pmc data"}' ;;
+    *) echo '{"leg": "'"$1"'"}' ;;
+  esac
+}
+
 run_task() {
   local task=$1; shift
   case "$task" in
@@ -59,7 +67,7 @@ run_task() {
           --output-format csv -- python3 $a > "$R/gpurun_out/pmc_${leg}_$c.log" 2>&1) || { echo "pmc $leg $c failed"; return 1; }
       done
       python3 tools/pmc_summary.py "gpurun_out/pmc_${leg}_FETCH_SIZE" "gpurun_out/pmc_${leg}_WRITE_SIZE" \
-        "gpurun_out/pmc_$leg.json"; return $? ;;
+        "gpurun_out/pmc_$leg.json" "$(pmc_workload "$leg")"; return $? ;;
     probe)
       local name=$1; shift
       timeout -k 10 900 python "tools/$name.py" "$@" > "gpurun_out/probe_$name.log" 2>&1; local rc=$?

@@ -112,6 +112,16 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_FUSE_GEMM={f}", end=" ")
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_FUSE_GEMM")
+    if which == "splitcmp":  # split-K count of the cov score GEMM (fused into the last trail launch or apart)
+        for d, K in ((1000, 2000), (1400, 1000)):
+            for sp in ("4", "8", "2"):
+                for f in ("1", "0"):
+                    os.environ["MIDAGMA_EXP_COV_SPLIT"] = sp
+                    os.environ["MIDAGMA_EXP_FUSE_GEMM"] = f
+                    print(f"MIDAGMA_EXP_COV_SPLIT={sp} MIDAGMA_EXP_FUSE_GEMM={f}", end=" ")
+                    cov_case(d, 2 * d, 10, K)
+        os.environ.pop("MIDAGMA_EXP_COV_SPLIT")
+        os.environ.pop("MIDAGMA_EXP_FUSE_GEMM")
     if which == "b128":  # 64 < d <= 128 (run with MIDAGMA_EXP_BINV128=0 / 1: read once per process)
         for d in (65, 100, 128):
             print(f"MIDAGMA_EXP_BINV128={os.environ.get('MIDAGMA_EXP_BINV128', '1')}", end=" ")
