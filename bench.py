@@ -97,6 +97,9 @@ def setup_dist(args):
     torch.cuda.set_device(local)
     if world > 1:
         if backend == "nccl":
+            # ring all-reduce hands every rank the same bits, so the replicated controllers
+            # decide identically; RCCL's other algorithms need not
+            os.environ.setdefault("NCCL_ALGO", "Ring")
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
@@ -191,8 +194,18 @@ def bench_data(args, world, rank, local):
     elapsed = float(elapsed.item())
     ok = (r.status == 0 and r.iters == Wm + K)
     prof = s.profile_parts(args.profile_reps) if rank == 0 else {}
+    replicas = None
+    if world > 1:  # W must be bit-identical on every rank: compare (sum, sum of squares) over ranks
+        Wf = np.zeros((d, d))
+        s.end(Wf)
+        v = np.array([Wf.sum(), (Wf * Wf).sum()])
+        t = torch.tensor(np.concatenate([v, -v]), dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        m = t.cpu().numpy()
+        replicas = bool(m[0] == -m[2] and m[1] == -m[3])
+        ok = ok and replicas
     out = dict(ms_per_step=elapsed / K * 1e3, value=K / elapsed, verified_iters=int(r.iters), verified=ok,
-               n_local=n_k, prof=prof, D=s.D, sem_gen_s=t_gen)
+               n_local=n_k, prof=prof, D=s.D, sem_gen_s=t_gen, replicas_identical=replicas)
     s.close()
     return out
 
@@ -728,6 +741,8 @@ def main():
                 "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
                 "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic", "config": cfg,
                 "verified": verified}
+        if args.workload == "data" and world > 1:
+            line["replicas_identical"] = res.get("replicas_identical")
         if roof is not None:
             line["roofline"] = roof
         if sem_gen is not None:
@@ -738,8 +753,10 @@ def main():
             cr = {"value": cov_res["value"], "unit": "steps/s", "ms_per_step": cov_res["ms_per_step"],
                   "workload": f"config2: d={d}, n={args.cov_n}, cov mode (reference algorithm), 1 GPU",
                   "verified": cov_res["verified"], "kernel_ms": {k: round(v, 4) for k, v in p.items()},
-                  "slot_tflops": F / (p["slot"] * 1e-3) / 1e12,
-                  "slot_frac_fp64_peak": F / (p["slot"] * 1e-3) / 1e12 / FP64_MFMA_PEAK_TF}
+                  # per Adam step of the timed run (fast slots with their GJ slots), not the
+                  # profile's one-slot figures (kernel_ms "slot" is the pivoted GJ slot)
+                  "slot_tflops": F / (cov_res["ms_per_step"] * 1e-3) / 1e12,
+                  "slot_frac_fp64_peak": F / (cov_res["ms_per_step"] * 1e-3) / 1e12 / FP64_MFMA_PEAK_TF}
             if args.workload == "cov":
                 line["roofline"] = {"bound": "mfma", "kernel": "slot", "achieved": cr["slot_tflops"],
                                     "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": cr["slot_frac_fp64_peak"],

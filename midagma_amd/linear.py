@@ -38,6 +38,7 @@ import typing
 import numpy as np
 
 from .slog import LogConfig, StructuredLogger, build_default_logger, checkpoint_row
+from ._lib import HipSolverError
 from .solver import HipSolver, run_allreduce_minimize
 
 __all__ = ["DagmaLinear"]
@@ -118,6 +119,22 @@ class DagmaLinear:
         t = t.to(torch.device("cuda", self.device)) if on_gpu else t.clone()
         dist.all_reduce(t, group=self.process_group)
         return t.cpu().numpy()
+
+    def _agree(self, status: int, iters: int) -> None:
+        """Raise unless every rank polled the same (status, iters) (run_allreduce_minimize)."""
+        v = np.array([status, iters, -status, -iters], dtype=np.float64)
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        import torch
+        on_gpu = dist.get_backend(self.process_group) == "nccl"
+        t = torch.from_numpy(v)
+        t = t.to(torch.device("cuda", self.device)) if on_gpu else t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
+        m = t.cpu().numpy()
+        if m[0] != -m[2] or m[1] != -m[3]:
+            raise HipSolverError(f"data-parallel replicas diverged: (status, iters) ranges over ranks "
+                                 f"[{-m[2]:.0f}, {m[0]:.0f}], [{-m[3]:.0f}, {m[1]:.0f}] (pin NCCL_ALGO=Ring)")
 
     def _setup_solver(self, X_local=None, cov_on_device=False):
         world, rank = self._world()
@@ -219,7 +236,8 @@ class DagmaLinear:
         logging_on = bool(self._log_cfg.enabled)
         if self.score_mode == "data" and self._allreduce is not None:
             res = run_allreduce_minimize(self._solver, W, mu, max_iter, s, lr, tol, beta_1, beta_2,
-                                         self.lambda1, self.checkpoint, allreduce=self._allreduce)
+                                         self.lambda1, self.checkpoint, allreduce=self._allreduce,
+                                         agree=self._agree)
             ckpts = self._solver.checkpoints() if logging_on else ()
         else:
             res = self._solver.minimize(W, mu, max_iter, s, lr, tol, beta_1, beta_2, self.lambda1,

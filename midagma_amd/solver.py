@@ -259,7 +259,7 @@ class HipSolver:
 
 
 def run_allreduce_minimize(backend, W, mu, max_iter, s, lr, tol=1e-6, beta_1=0.99, beta_2=0.999,
-                           lambda1=0.03, checkpoint=1000, allreduce=None, batch: int = 32):
+                           lambda1=0.03, checkpoint=1000, allreduce=None, batch: int = 32, agree=None):
     """Data-parallel inner loop over ranks.
 
     ``backend`` exposes begin/step_partial/step_finish/poll/end (HipSolver, or a
@@ -267,12 +267,20 @@ def run_allreduce_minimize(backend, W, mu, max_iter, s, lr, tol=1e-6, beta_1=0.9
     in place.  Termination is decided on the device by the controller kernel;
     the host polls every ``batch`` steps, extra steps after termination are
     no-ops, so every rank runs the same number of all-reduces.
+
+    The replicas decide identically only while the all-reduce hands every rank the
+    same bits (a ring all-reduce does; ``NCCL_ALGO=Ring`` pins it).  ``agree(status,
+    iters)``, called at every poll, compares the ranks' states with one small
+    collective and raises on a mismatch, so a divergent replica fails loudly instead
+    of leaving the other ranks waiting in an all-reduce it no longer issues.
     """
     backend.begin(W, mu, max_iter, s, lr, tol, beta_1, beta_2, lambda1, checkpoint)
     slots = 0
     cap = int(max_iter) + int(max_iter) // max(int(checkpoint), 1) + 512
     while True:
         last = backend.poll()
+        if agree is not None:
+            agree(int(last.status), int(last.iters))
         if last.status != _lib.ST_RUNNING:
             break
         if slots > cap:

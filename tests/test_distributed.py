@@ -147,6 +147,65 @@ def test_data_parallel_matches_single_process(world, golden):
     assert np.abs(W0 - W_ref).max() <= 1e-9
 
 
+class _EarlyStopBackend(_ShardBackend):
+    """A replica whose controller stops early (as a rank handed different all-reduce bits
+    could): it reports ST_DONE after `stop_at` steps."""
+
+    def __init__(self, *a, stop_at):
+        super().__init__(*a)
+        self.stop_at = stop_at
+
+    def step_finish(self):
+        super().step_finish()
+        if self.status == _lib.ST_RUNNING and self.it >= self.stop_at:
+            self.status = _lib.ST_DONE
+
+
+def _diverge_worker(rank, world, port, X, out_q):
+    import types
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from midagma_amd.linear import DagmaLinear
+        from midagma_amd.solver import run_allreduce_minimize
+        n, d = X.shape
+        lo, hi = _row_range(n, world, rank)
+        be = _EarlyStopBackend(X[lo:hi], n, 0.03, stop_at=10 if rank == 1 else 10 ** 9)
+        me = types.SimpleNamespace(process_group=None, device=0)
+
+        def allreduce():
+            dist.all_reduce(be.z)
+
+        try:
+            run_allreduce_minimize(be, np.zeros((d, d)), 1.0, 100, 1.0, 3e-4, tol=-1.0, lambda1=0.03,
+                                   checkpoint=1000, allreduce=allreduce, batch=7,
+                                   agree=lambda st, it: DagmaLinear._agree(me, st, it))
+            out_q.put((rank, "returned", ""))
+        except _lib.HipSolverError as e:
+            out_q.put((rank, "raised", str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_divergent_replica_raises_instead_of_hanging(golden):
+    """A rank whose controller decides differently stops issuing all-reduces; the poll-time
+    agreement (DagmaLinear._agree) makes every rank raise instead of waiting forever."""
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    X = X - X.mean(axis=0, keepdims=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_diverge_worker, args=(r, 2, port, X, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [o[1] for o in outs] == ["raised", "raised"], outs
+    assert "diverged" in outs[0][2]
+
+
 class _ShardSolver(_ShardBackend):
     """CPU double of HipSolver for DagmaLinear.fit in data mode: the calls fit() makes
     (set_data / data_gram / torch_zbuf / cov_from_zbuf / get_cov / the step protocol / h / score),

@@ -122,6 +122,13 @@ if __name__ == "__main__":
                     cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_COV_SPLIT")
         os.environ.pop("MIDAGMA_EXP_FUSE_GEMM")
+    if which == "splitmid":  # 128-tile grids of 81..196 tiles: split-K 1..4 of the fused cov score GEMM
+        for d, K in ((1150, 1000), (1400, 1000), (1700, 600)):
+            for sp in ("1", "2", "3", "4"):
+                os.environ["MIDAGMA_EXP_COV_SPLIT"] = sp
+                print(f"MIDAGMA_EXP_COV_SPLIT={sp}", end=" ")
+                cov_case(d, 2 * d, 10, K)
+        os.environ.pop("MIDAGMA_EXP_COV_SPLIT")
     if which == "b128":  # 64 < d <= 128 (run with MIDAGMA_EXP_BINV128=0 / 1: read once per process)
         for d in (65, 100, 128):
             print(f"MIDAGMA_EXP_BINV128={os.environ.get('MIDAGMA_EXP_BINV128', '1')}", end=" ")
