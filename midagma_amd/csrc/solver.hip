@@ -527,7 +527,11 @@ struct midagma_solver {
       // 1600 tiles at d = 5000 leave the 4th wave 1/8 full, split 4 -> 13 full-ish waves)
       const int64_t tiles = (D / 128) * (D / 128), slots = 2 * 256;
       if (tiles < 256) {
-        cov_split = (int)std::min<int64_t>(4, D / 128);
+        // about one workgroup per CU: round(256 / tiles + 1/4), at most 4 and D / 128 (measured,
+        // fused with the last trailing update: D = 1152 split 3 2909 vs 4 2770 steps/s; D = 1408
+        // split 2 2016 vs 4 1985; D = 1792 split 2 1480 vs 4 1452 vs 1 1406; D = 1024 split 4)
+        cov_split = (int)std::max<int64_t>(
+            1, std::min<int64_t>({4, D / 128, (int64_t)(256.0 / (double)tiles + 0.75)}));
       } else if (tiles >= 1024) {  // (256..1023 tiles: split 1 measured best at d = 2000)
         double best = 1e30;
         for (int sp = 1; sp <= 4; ++sp) {
@@ -936,6 +940,15 @@ int midagma_create(midagma_solver** out, int loss, int mode, int64_t d, int devi
   const char* p256 = getenv("MIDAGMA_EXP_COV_PAD256");
   const bool pad256 = mode == MIDAGMA_MODE_COV && !(p256 && atoi(p256) == 0);
   s->D = d > 192 || (pad256 && d > 128) ? (d + 127) / 128 * 128 : round_up64(d);
+  // Cov mode, 256 < d <= 640: D to a multiple of 256, so the blocked inverse runs B2 = 256 outer
+  // blocks (2 instead of 3 at D = 384 -> 512, 3 instead of 5 at 640 -> 768: d=300 11.1k -> 11.3k,
+  // d=600 6.4k -> 7.0k steps/s).  Larger D keep B2 = 128 (d=1150 even, d=1400 -3.5%, d=1700
+  // even: the padded GEMM work outweighs the saved outer steps).  Knob MIDAGMA_EXP_COV_PAD_B2:
+  // 0 off, 1 at every d > 256.
+  const char* pb2 = getenv("MIDAGMA_EXP_COV_PAD_B2");
+  const int pad_b2 = pb2 ? atoi(pb2) : -1;
+  if (mode == MIDAGMA_MODE_COV && d > 256 && (pad_b2 == 1 || (pad_b2 < 0 && d <= 640)))
+    s->D = (d + 255) / 256 * 256;
   s->device = device;
   int rc = guarded(s, [&] {
     setup_attributes_once();

@@ -413,11 +413,13 @@ def test_minimize_d1000_short(hip):
     assert np.abs(W - Wr).max() <= 1e-10
 
 
-@pytest.mark.parametrize("d", [300, 600, 1000, 2000])
+@pytest.mark.parametrize("d", [300, 600, 1000, 1150, 1400, 2000])
 def test_blocked_fast_path_trajectory(hip, d):
     """Cov mode at d > 192 runs the two-level blocked inverse: warm-started fast slots between
-    Gauss-Jordan slots (first slot, every checkpoint).  d=300 -> D=384 (B2=128, 3 outer
-    blocks), 600 -> 640 (B2=128, 5), 1000 -> 1024 (B2=256, 4), 2000 -> 2048 (B2=256, 8;
+    Gauss-Jordan slots (first slot, every checkpoint).  d=300 -> D=512 (cov mode pads
+    256 < d <= 640 to 256-multiples: B2=256, 2 outer blocks), 600 -> 768 (B2=256, 3), 1000 ->
+    1024 (B2=256, 4; score GEMM split-K 4), 1150 ->
+    1152 (B2=128, 9; split 3), 1400 -> 1408 (B2=128, 11; split 2), 2000 -> 2048 (B2=256, 8;
     trailing update on the 128-tile GEMM).  Same iterations, W and checkpoint objectives as
     the oracle (LAPACK inverse)."""
     X, _, _ = make_dataset(d, 2 * d, seed=d)

@@ -43,7 +43,7 @@ def test_trek_value_grad_matches_reference(hip, golden, seq, agg, d):
 
 @pytest.mark.parametrize("seq", ["exp", "inv", "log"])
 def test_trek_large_d_matches_oracle(hip, seq):
-    """d=300 (D=384): split-K GEMMs, several squarings for exp, dense pair list."""
+    """d=300 (D=512 in cov mode): split-K GEMMs, several squarings for exp, dense pair list."""
     d = 300
     rng = np.random.default_rng(3)
     W = (rng.uniform(-1, 1, (d, d)) * (rng.uniform(size=(d, d)) < 3.0 / d)) * 0.6

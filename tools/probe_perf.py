@@ -129,6 +129,13 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_COV_SPLIT={sp}", end=" ")
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_COV_SPLIT")
+    if which == "padb2":  # cov mode, d > 256 with 256 not dividing the 128-padded size: D to 256-multiples
+        for d, K in ((300, 3000), (600, 3000), (1150, 1000), (1400, 1000), (1700, 600)):
+            for f in ("0", "1"):
+                os.environ["MIDAGMA_EXP_COV_PAD_B2"] = f
+                print(f"MIDAGMA_EXP_COV_PAD_B2={f}", end=" ")
+                cov_case(d, 2 * d, 10, K)
+        os.environ.pop("MIDAGMA_EXP_COV_PAD_B2")
     if which == "b128":  # 64 < d <= 128 (run with MIDAGMA_EXP_BINV128=0 / 1: read once per process)
         for d in (65, 100, 128):
             print(f"MIDAGMA_EXP_BINV128={os.environ.get('MIDAGMA_EXP_BINV128', '1')}", end=" ")
