@@ -2,7 +2,8 @@
 // replacement for `sla.inv(s*I - W*W)` (linear.py:226, 240) when D = 128 or D >= 256 (D % 128 == 0).
 //
 // Outer block Gauss-Jordan over B2-wide pivot blocks (B2 = 256, or 128 when 256 does not
-// divide D).  Outer step g sweeps pivot block G = [g B2, (g+1) B2):
+// divide D; one block, B2 = D, at D = 128, and at 512 as an experiment).  Outer step g sweeps pivot block
+// G = [g B2, (g+1) B2):
 //     P = S^-1 with S = A_GG (the Schur complement left by the steps before g)
 //     A_Gj <- P A_Gj     A_iG <- -A_iG P     A_ij <- A_ij - A_iG (P A_Gj)     A_GG <- P
 // -- the sweep gj.hip applies at 32 granularity; after every block is swept A holds A^-1.
@@ -254,6 +255,13 @@ int binv_block(int64_t D) {
   // product form (3 launches instead of the Gauss-Jordan's prologue and 4 block steps)
   static const bool b128 = !(getenv("MIDAGMA_EXP_BINV128") && atoi(getenv("MIDAGMA_EXP_BINV128")) == 0);
   if (D == 128) return b128 ? 128 : 0;
+  // Experiment (MIDAGMA_EXP_BINV512=1): D = 512 as one 512-wide block, the fast slot's inverse
+  // the product form alone (a residual and two pass launches instead of two outer steps of
+  // five).  Correct (the GPU tier passes with it on) but slower: d=300/400/500 7.2k/6.9k/6.8k
+  // vs 11.2k/10.7k/10.4k steps/s (the 512-wide pass kernel holds 256 VGPRs, one wave per SIMD,
+  // and its 1024 workgroups run in four rounds).
+  static const bool b512 = getenv("MIDAGMA_EXP_BINV512") && atoi(getenv("MIDAGMA_EXP_BINV512")) == 1;
+  if (D == 512 && b512) return 512;
   if (D < 256 || D % 128 != 0) return 0;  // fast path not available: plain GJ
   return D % 256 == 0 ? 256 : 128;
 }
@@ -301,7 +309,9 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     int64_t ldp;
     const int* done = nullptr;
     if (fast) {
-      if (B2 == 256)
+      if (B2 == 512)
+        launch_neumann<32>(Ain, D, G0, bw, g, st, passes, stream);
+      else if (B2 == 256)
         launch_neumann<16>(Ain, D, G0, bw, g, st, passes, stream);
       else
         launch_neumann<8>(Ain, D, G0, bw, g, st, passes, stream);

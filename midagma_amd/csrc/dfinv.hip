@@ -585,7 +585,7 @@ Plan make_plan(int64_t D, int passes, int nwg, double hop_us) {
 }  // namespace
 
 bool df_available(int64_t D) {
-  if (D % DF_B2 != 0 || D < 2 * DF_B2 || D / DF_B2 > DF_MAX_K2) return false;
+  if (D % DF_B2 != 0 || D < 2 * DF_B2 || D / DF_B2 > DF_MAX_K2 || binv_block(D) != DF_B2) return false;
   static const int64_t maxd = getenv("MIDAGMA_EXP_DF_MAXD") ? atoll(getenv("MIDAGMA_EXP_DF_MAXD")) : 1536;
   return D <= maxd;
 }

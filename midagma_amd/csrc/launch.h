@@ -62,7 +62,7 @@ struct GemmSpec {
 // from a warm start one Adam step old, 3 always converged in the default d=1000 fit)
 constexpr int NM_PASSES = 4;
 constexpr int NM_PASSES_RUN = 3;
-constexpr int PART_STRIDE = 4096;   // doubles per pass: row partials of |Q| (B2 x B2/16)
+constexpr int PART_STRIDE = 16384;  // doubles per pass: row partials of |Q| (B2 x B2/16, B2 <= 512)
 struct BInvWork {
   double* Aalt;    // second D x D buffer (outer steps ping-pong)
   double* Pst;     // D x B2: the outer diagonal blocks' inverses of the slots with even /

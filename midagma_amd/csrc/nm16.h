@@ -79,20 +79,26 @@ __device__ __forceinline__ double row_sum16(double a) {
 }
 
 // ||Q||_inf from the row partials (row r's NT = B2 / 16 tile partials at rowpart[r NT + t]),
-// B2 <= NTHREADS rows, one per thread; load(i) returns rowpart[i].  Non-finite propagates as
+// one row per thread (B2 = 512: two); load(i) returns rowpart[i].  Non-finite propagates as
 // inf/nan; widened by 1e-6 against the float max.
 template <int B2, class Load>
 __device__ __forceinline__ double inf_norm_rows(Load&& load, float* red4) {
   constexpr int NT = B2 / 16;
-  double r = 0.0;
-  if ((int)threadIdx.x < B2) {
-    double v[NT];  // all loads in flight before the (ordered) sum
+  constexpr int RPT = B2 > NTHREADS ? B2 / NTHREADS : 1;  // rows per thread
+  float f = 0.0f;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) v[t] = load((int)threadIdx.x * NT + t);
+  for (int h = 0; h < RPT; ++h) {
+    const int row = (int)threadIdx.x + h * NTHREADS;
+    double r = 0.0;
+    if (row < B2) {
+      double v[NT];  // all loads in flight before the (ordered) sum
 #pragma unroll
-    for (int t = 0; t < NT; ++t) r += v[t];
+      for (int t = 0; t < NT; ++t) v[t] = load(row * NT + t);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) r += v[t];
+    }
+    f = fmaxf(f, isfinite(r) ? (float)(r * (1.0 + 1e-6)) : INFINITY);
   }
-  const float f = isfinite(r) ? (float)(r * (1.0 + 1e-6)) : INFINITY;
   return (double)block_max(f, red4);
 }
 

@@ -136,6 +136,10 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_COV_PAD_B2={f}", end=" ")
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_COV_PAD_B2")
+    if which == "b512":  # 256 < d <= 512, cov mode (run with MIDAGMA_EXP_BINV512=0 / 1: read once per process)
+        for d in (300, 400, 500):
+            print(f"MIDAGMA_EXP_BINV512={os.environ.get('MIDAGMA_EXP_BINV512', '0')}", end=" ")
+            cov_case(d, 2 * d, 20, 3000)
     if which == "b128":  # 64 < d <= 128 (run with MIDAGMA_EXP_BINV128=0 / 1: read once per process)
         for d in (65, 100, 128):
             print(f"MIDAGMA_EXP_BINV128={os.environ.get('MIDAGMA_EXP_BINV128', '1')}", end=" ")
