@@ -61,6 +61,45 @@ __device__ __forceinline__ double inf_norm(const double* __restrict__ rowpart, f
   return inf_norm_rows<B2>([&](int i) { return rowpart[i]; }, red4);
 }
 
+// The warm start X0 of a block (see nm_resid_kernel) as the B operand of a split-K tile
+template <int L>
+__device__ __forceinline__ void load_x0_b(const double* __restrict__ Pe, const double* __restrict__ Po,
+                                          const State* __restrict__ st, int n0, double (&b)[L]) {
+  constexpr int B2 = 16 * L;
+  const bool odd = (st->slots & 1) != 0;
+  splitk_load_b<L>(odd ? Pe : Po, B2, n0, b);
+  if (st->warm_run >= 2) {
+    double b2[L];
+    splitk_load_b<L>(odd ? Po : Pe, B2, n0, b2);
+#pragma unroll
+    for (int q = 0; q < L; ++q) b[q] = 2.0 * b[q] - b2[q];
+  }
+}
+
+// Look-ahead residual of the next outer block gn = g + 1 (fast path).  With X0 its warm start
+// and S = A(gn,gn) - A(gn,G) P_g A(G,gn) the Schur complement the trailing update of step g
+// leaves,  R = I - S X0 = I - (LW - A(gn,G) LPZ),  LW = A(gn,gn) X0,  LZ = A(G,gn) X0,
+// LPZ = P_g LZ: LW and LZ are extra tiles of block g's first and second pass, LPZ of its panel launch and
+// R of its trailing update, so block gn needs no residual launch of its own.
+struct NmLA {  // extra tiles of a pass launch: out = A X0(gn) (A: a block of step g's input)
+  const double* A;   // pass 1: A(gn, gn) -> LW; pass 2: A(G, gn) -> LZ
+  int64_t lda;
+  const double* Pe;  // block gn's warm-start stores
+  const double* Po;
+  double* out;
+};
+struct TrailLA {  // trailing-launch extra tiles
+  const double* LW;
+  const double* LPZ;
+  const double* Pe;
+  const double* Po;
+  double* Y0;     // block gn's first iterate X0 and residual R, its row partials, its done word
+  double* Q0;
+  double* part0;
+  int* done;
+  int gn;
+};
+
 // X0 = the warm start of this block: with two consecutive stored slots (st->warm_run >= 2)
 // the linear extrapolation 2 P1 - P2 of the last two inverses (P1 = slot k-1's, P2 = slot
 // k-2's, by the parity of k = st->slots), else P1.  Adam moves W smoothly (beta1 = 0.99), so
@@ -119,16 +158,31 @@ __global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restr
                                                            double* __restrict__ Qn, double* __restrict__ P,
                                                            const double* __restrict__ part_prev,
                                                            double* __restrict__ part_next, int* __restrict__ done,
-                                                           int pass, State* __restrict__ st) {
+                                                           int pass, State* __restrict__ st, NmLA la) {
   if (st->status != ST_RUNNING) return;
+  constexpr int B2 = 16 * L;
+  __shared__ double red[4 * 256];
+  __shared__ float red4[4];
+  const int nt = B2 / 16, tid = threadIdx.x;
+  if ((int)blockIdx.x >= nt * nt) {  // look-ahead tiles of the next block (LW or LZ)
+    const int t = (int)blockIdx.x - nt * nt;
+    const int m0 = (t / nt) * 16, n0 = (t % nt) * 16;
+    double a[L], b[L];
+    splitk_load_a<L>(la.A, la.lda, m0, a);
+    load_x0_b<L>(la.Pe, la.Po, st, n0, b);
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    splitk_mfma<L>(a, b, acc);
+    const double sum = splitk_sum(acc, red);
+    int row, col;
+    tile_elem(tid, row, col);
+    st_wt(la.out + (int64_t)(m0 + row) * B2 + n0 + col, sum);
+    return;
+  }
   // an EARLIER pass converged (done holds its number; this pass's own workgroups may store
   // theirs meanwhile, which must not make a sibling skip its tile of P)
   const int dn = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (dn != 0 && dn < pass) return;
-  constexpr int B2 = 16 * L;
-  __shared__ double red[4 * 256];
-  __shared__ float red4[4];
-  const int nt = B2 / 16, wg = blockIdx.x, tid = threadIdx.x;
+  const int wg = blockIdx.x;
   const int m0 = (wg / nt) * 16, n0 = (wg % nt) * 16;
   // operands first: their latency overlaps the rho reduction (Y, Q are complete: the
   // previous launch wrote them)
@@ -181,7 +235,9 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
                                                               const double* __restrict__ P, int64_t ldp,
                                                               double* __restrict__ Pe, double* __restrict__ Po,
                                                               const int* __restrict__ done, int check,
-                                                              State* __restrict__ st, int pf) {
+                                                              State* __restrict__ st, int pf,
+                                                              const double* __restrict__ LZ,
+                                                              double* __restrict__ LPZ) {
   if (st && st->status != ST_RUNNING) return;
   if (done && *done == 0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
@@ -215,6 +271,12 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
       flag |= domain_flag(-v);
     });
     if (check && flag) atomicOr(&st->flags, flag);
+  } else if (job >= 2 * nu + gb * gb) {  // look-ahead: LPZ = P LZ (next block's residual)
+    const int j4 = job - 2 * nu - gb * gb, a = j4 / gb, c = j4 % gb;
+    tile32_gemm_any(pf, P + (int64_t)a * NB * ldp, ldp, LZ + (int64_t)c * NB, B2, B2, acc, img[0], img[1], img[2],
+                    img[3]);
+    double* out = LPZ + (int64_t)a * NB * B2 + (int64_t)c * NB;
+    acc_foreach(acc, [&](int row, int col, double& v) { st_wt(out + (int64_t)row * B2 + col, v); });
   } else {
     const int j3 = job - 2 * nu, a = j3 / gb, c = j3 % gb;
     const double* src = P + (int64_t)a * NB * ldp + (int64_t)c * NB;
@@ -235,13 +297,39 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
 }
 
 // Trailing update of outer step g, one 32 x 32 tile per workgroup (binv_trail_tile).
+// With la.LW: the next block's residual tiles follow the mb x mb trailing tiles (TrailLA).
 __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __restrict__ Ain,
                                                               double* __restrict__ Aout, int64_t D, int B2, int g,
-                                                              int check, State* __restrict__ st, int pf) {
+                                                              int check, State* __restrict__ st, int pf, TrailLA la) {
   if (st && st->status != ST_RUNNING) return;
   __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
-  binv_trail_tile(xcd_spread(blockIdx.x, gridDim.x), Ain, Aout, D, B2, g, check, st, pf, img[0], img[1], img[2],
-                  img[3]);
+  const int job = xcd_spread(blockIdx.x, gridDim.x);
+  const int gb = B2 / NB, mb = (int)(D / NB) - gb;
+  if (job < mb * mb) {
+    binv_trail_tile(job, Ain, Aout, D, B2, g, check, st, pf, img[0], img[1], img[2], img[3]);
+    return;
+  }
+  // R = I - (LW - A(gn, G) LPZ) on the 32 x 32 tile (a, c) of block gn; X0 -> Y0, |R| row partials
+  const int j = job - mb * mb, a = j / gb, c = j % gb;
+  const int64_t GN0 = (int64_t)la.gn * B2, G0 = (int64_t)g * B2;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  tile32_gemm_any(pf, Ain + (GN0 + (int64_t)a * NB) * D + G0, D, la.LPZ + (int64_t)c * NB, B2, B2, acc, img[0],
+                  img[1], img[2], img[3]);
+  const bool odd = (st->slots & 1) != 0, extrap = st->warm_run >= 2;
+  const double* P1 = odd ? la.Pe : la.Po;
+  const double* P2 = odd ? la.Po : la.Pe;
+  const int lane = threadIdx.x & 63, m0 = q_m0(), n0 = q_n0(), nt = B2 / 16;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int row = a * NB + m0 + acc_row(lane, t), col = c * NB + n0 + acc_col(lane);
+    const int64_t e = (int64_t)row * B2 + col;
+    const double r = (row == col ? 1.0 : 0.0) - (la.LW[e] - acc[t]);
+    st_wt(la.Q0 + e, r);
+    st_wt(la.Y0 + e, extrap ? 2.0 * P1[e] - P2[e] : P1[e]);
+    const double rs = row_sum16(abs_or_inf(r));  // the 16 lanes of this row: one DPP row
+    if (acc_col(lane) == 0) st_wt(la.part0 + (int64_t)row * nt + (c * NB + n0) / 16, rs);
+  }
+  if (j == 0 && threadIdx.x == 0) *la.done = 0;
 }
 
 }  // namespace
@@ -274,21 +362,37 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw) {
 
 template <int L>
 static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& bw, int g, State* st, int passes,
-                           hipStream_t stream) {
+                           bool resid, const NmLA* la, hipStream_t stream) {
   constexpr int B2 = 16 * L;
   const int nwg = (B2 / 16) * (B2 / 16);
   const double* Pe = bw.Pst + (int64_t)g * B2 * B2;
   const double* Po = bw.Pst1 + (int64_t)g * B2 * B2;
   int* done = bw.done + g;
   double* part = bw.part + (int64_t)g * (NM_PASSES + 1) * PART_STRIDE;  // per block: kept for diagnostics
-  hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Ain + G0 * D + G0, D, Pe, Po,
-                     bw.Y[0], bw.Q[0], part, done, st);
+  if (resid)  // else the previous block's launches left X0, R and its row partials (look-ahead)
+    hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Ain + G0 * D + G0, D, Pe, Po,
+                       bw.Y[0], bw.Q[0], part, done, st);
+  const NmLA none{};
   for (int p = 1; p <= passes && p <= NM_PASSES; ++p) {
-    const double* Y = bw.Y[(p - 1) & 1];  // pass 1: X0 from nm_resid
-    hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, Y, bw.Q[(p - 1) & 1],
-                       bw.Y[p & 1], bw.Q[p & 1], bw.P, part + (p - 1) * PART_STRIDE, part + p * PART_STRIDE,
-                       done, p, st);
+    const double* Y = bw.Y[(p - 1) & 1];  // pass 1: X0 from nm_resid (or the look-ahead)
+    // passes 1 and 2 carry the look-ahead products LW and LZ (one more tile grid each: the pass
+    // kernel's registers admit two workgroups per CU, so both grids stay one round)
+    const bool ext = la != nullptr && p <= 2;
+    hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(ext ? 2 * nwg : nwg), dim3(NTHREADS), 0, stream, Y,
+                       bw.Q[(p - 1) & 1], bw.Y[p & 1], bw.Q[p & 1], bw.P, part + (p - 1) * PART_STRIDE,
+                       part + p * PART_STRIDE, done, p, st, ext ? la[p - 1] : none);
   }
+}
+
+// Experiment knob MIDAGMA_EXP_RESID_LA=1: the look-ahead residual (read at each enqueue, i.e.
+// when a slot graph is captured).  Correct (the blocked parity tests pass with it on) but not
+// faster: the extra tiles lengthen the latency-bound pass, panel and trailing launches by more
+// than the residual launch they remove (d=1000 4422 -> 4342, d=700 6709 -> 6414, d=1150 even,
+// d=1400 1968 -> 2000 steps/s; with LW and LZ both in the first pass, whose grid then needs two
+// rounds: d=1000 4285).
+static bool resid_lookahead() {
+  const char* e = getenv("MIDAGMA_EXP_RESID_LA");
+  return e && atoi(e) == 1;
 }
 
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
@@ -299,6 +403,8 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
   const int K2 = (int)(D / B2), gb = B2 / NB, mb = (int)(D / NB) - gb;
   double* bufs[2] = {binv_build_target(Mt, D, bw), nullptr};
   bufs[1] = bufs[0] == Mt ? bw.Aalt : Mt;
+  // look-ahead residual (NmLA / TrailLA): fast path with 32 x 32 trailing updates
+  const bool look = fast && bw.LW && K2 > 1 && D - B2 < TRAIL128_MIN && resid_lookahead();
   for (int g = 0; g < K2; ++g) {
     double* Ain = bufs[g & 1];
     double* Aout = bufs[(g + 1) & 1];
@@ -308,13 +414,24 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     const double* P;
     int64_t ldp;
     const int* done = nullptr;
+    const bool ahead = look && g + 1 < K2;  // this block's launches prepare block g + 1's residual
+    const int64_t GN0 = G0 + B2;
+    NmLA la[2] = {};
+    TrailLA tla{};
+    if (ahead) {
+      la[0] = NmLA{Ain + GN0 * D + GN0, D, bw.Pst + GN0 * B2, bw.Pst1 + GN0 * B2, bw.LW};
+      la[1] = NmLA{Ain + G0 * D + GN0, D, bw.Pst + GN0 * B2, bw.Pst1 + GN0 * B2, bw.LZ};
+      tla = TrailLA{bw.LW, bw.LPZ, bw.Pst + GN0 * B2, bw.Pst1 + GN0 * B2, bw.Y[0], bw.Q[0],
+                    bw.part + (int64_t)(g + 1) * (NM_PASSES + 1) * PART_STRIDE, bw.done + g + 1, g + 1};
+    }
     if (fast) {
+      const bool resid = !look || g == 0;
       if (B2 == 512)
-        launch_neumann<32>(Ain, D, G0, bw, g, st, passes, stream);
+        launch_neumann<32>(Ain, D, G0, bw, g, st, passes, resid, ahead ? la : nullptr, stream);
       else if (B2 == 256)
-        launch_neumann<16>(Ain, D, G0, bw, g, st, passes, stream);
+        launch_neumann<16>(Ain, D, G0, bw, g, st, passes, resid, ahead ? la : nullptr, stream);
       else
-        launch_neumann<8>(Ain, D, G0, bw, g, st, passes, stream);
+        launch_neumann<8>(Ain, D, G0, bw, g, st, passes, resid, ahead ? la : nullptr, stream);
       P = bw.P;
       ldp = B2;
       done = bw.done + g;
@@ -328,8 +445,9 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     }
     // the fast slot takes the domain flags from the last outer step's outputs (no reduce_check)
     const int check = fast && g == K2 - 1;
-    hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2,
-                       g, P, ldp, Pe, Po, done, check, st, t32_pf());
+    hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb * (ahead ? 2 : 1)), dim3(NTHREADS), 0, stream,
+                       Ain, Aout, D, B2, g, P, ldp, Pe, Po, done, check, st, t32_pf(), ahead ? bw.LZ : nullptr,
+                       ahead ? bw.LPZ : nullptr);
     if (mb > 0) {
       // large D: 128 x 128 tiles (operand reuse; enough tiles to fill the chip), else 32 x 32
       if (D - B2 >= TRAIL128_MIN) {
@@ -343,8 +461,8 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
         launch_gemm_trail(*fuse, Ain, Aout, D, B2, g, check, st, t32_pf(), mb * mb, stream);
         fused = true;
       } else {
-        hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb), dim3(NTHREADS), 0, stream, Ain, Aout, D, B2, g, check,
-                           st, t32_pf());
+        hipLaunchKernelGGL(binv_trail_kernel, dim3(mb * mb + (ahead ? gb * gb : 0)), dim3(NTHREADS), 0, stream, Ain,
+                           Aout, D, B2, g, check, st, t32_pf(), tla);
       }
     }
   }

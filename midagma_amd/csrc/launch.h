@@ -72,6 +72,11 @@ struct BInvWork {
   double* P;       // B2 x B2 converged inverse of the current block
   double* part;    // (D / B2) x (NM_PASSES + 1) x PART_STRIDE row partials
   int* done;       // D / B2 convergence words
+  // look-ahead residual (fast path, 32-tile trailing updates): block g's launches prepare block
+  // g+1's R = I - S X0 instead of a residual launch of its own (B2 x B2 each; null: off)
+  double* LW;      // A(g+1, g+1) X0(g+1)      (extra tiles of block g's first pass)
+  double* LZ;      // A(G, g+1) X0(g+1)        (same launch)
+  double* LPZ;     // P_g LZ                   (extra tiles of block g's panel launch)
 };
 // Outer block width of the two-level inverse (0: not available, use launch_gj_inverse).
 int binv_block(int64_t D);

@@ -91,7 +91,7 @@ struct midagma_solver {
   State* cgates = nullptr;
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
-  DevBuf Malt, Pst2, Pst2b, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone;
+  DevBuf Malt, Pst2, Pst2b, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone, nmLW, nmLZ, nmLPZ;
   // the fast slot's inverse as one dataflow launch (dfinv.hip; MIDAGMA_EXP_DF=1 enables: measured
   // slower than the launch-per-phase inverse at d = 500 and 1000)
   bool df_on = false;
@@ -143,7 +143,7 @@ struct midagma_solver {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
-                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &npart, &XT, &IW, &scarry, &sprev, &dfA, &dfY,
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &npart, &XT, &IW, &scarry, &sprev, &dfA, &dfY,
                       &dfQ, &dfP, &dfCtl, &dfTasks[0], &dfTasks[1], &dfWoff[0], &dfWoff[1], &dfStamps})
       b->release();
     for (DevBuf& b : tbufs) b.release();
@@ -181,7 +181,10 @@ struct midagma_solver {
                     {nmQ0.p, nmQ1.p},
                     nmP.p,
                     nmPart.p,
-                    reinterpret_cast<int*>(nmDone.p)};
+                    reinterpret_cast<int*>(nmDone.p),
+                    nmLW.p,
+                    nmLZ.p,
+                    nmLPZ.p};
   }
   bool blocked() const { return B2 > 0; }
   // k extent of the GEMMs whose K is the padded node dimension: the rows of A past d are zero
@@ -550,7 +553,7 @@ struct midagma_solver {
       Malt.alloc(DD);
       Pst2.alloc((size_t)D * b2);
       Pst2b.alloc((size_t)D * b2);
-      for (DevBuf* b : {&nmY0, &nmY1, &nmQ0, &nmQ1, &nmP}) b->alloc((size_t)b2 * b2);
+      for (DevBuf* b : {&nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmLW, &nmLZ, &nmLPZ}) b->alloc((size_t)b2 * b2);
       nmPart.alloc((size_t)(D / b2) * (NM_PASSES + 1) * PART_STRIDE);
       nmDone.alloc(D / b2);
     }

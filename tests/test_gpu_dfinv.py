@@ -26,6 +26,14 @@ def hip():
     return _lib
 
 
+@pytest.fixture(autouse=True)
+def _no_lookahead(monkeypatch):
+    """The one-launch inverse repeats the per-block residual launch's arithmetic; the
+    launch-per-phase path it is compared with bit for bit runs that form too
+    (MIDAGMA_EXP_RESID_LA=0; the default look-ahead residual rounds differently)."""
+    monkeypatch.setenv("MIDAGMA_EXP_RESID_LA", "0")
+
+
 def _solver(d, cov, df):
     from midagma_amd.solver import HipSolver
     old = os.environ.get("MIDAGMA_EXP_DF")

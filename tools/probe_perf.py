@@ -140,6 +140,13 @@ if __name__ == "__main__":
         for d in (300, 400, 500):
             print(f"MIDAGMA_EXP_BINV512={os.environ.get('MIDAGMA_EXP_BINV512', '0')}", end=" ")
             cov_case(d, 2 * d, 20, 3000)
+    if which == "lacmp":  # look-ahead residual experiment (block g's launches prepare block g+1's R) on / off
+        for d, K in ((1000, 2000), (700, 2000), (1150, 1000), (1400, 1000)):
+            for f in ("1", "0"):
+                os.environ["MIDAGMA_EXP_RESID_LA"] = f
+                print(f"MIDAGMA_EXP_RESID_LA={f}", end=" ")
+                cov_case(d, 2 * d, 10, K)
+        os.environ.pop("MIDAGMA_EXP_RESID_LA")
     if which == "b128":  # 64 < d <= 128 (run with MIDAGMA_EXP_BINV128=0 / 1: read once per process)
         for d in (65, 100, 128):
             print(f"MIDAGMA_EXP_BINV128={os.environ.get('MIDAGMA_EXP_BINV128', '1')}", end=" ")
