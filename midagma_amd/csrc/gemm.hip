@@ -742,7 +742,9 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
     HIP_TRY(hipGetLastError());
     return;
   }
-  if (K % 64) throw std::invalid_argument("launch_gemm: K % 64 outside the pipelined kernel");
+  // the older kernels step K by 64: a k extent cut at a 16-multiple (Kd(): the operands' rows
+  // past it are zero and allocated up to the 64-padded size) is rounded back up
+  if (K % 64) K = (K + 63) / 64 * 64;
   if (M % 128 == 0 && N % 128 == 0 && K % 128 == 0 && !force64) {
     const int64_t ktiles16 = K / G_BK;
     const int64_t per16 = (ktiles16 + split - 1) / split;

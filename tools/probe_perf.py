@@ -147,6 +147,13 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_RESID_LA={f}", end=" ")
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_RESID_LA")
+    if which == "groupcmp":  # fast slots captured per graph (MIDAGMA_EXP_FAST_GROUP, default 4)
+        for d, K in ((1000, 2000), (300, 4000), (2000, 300)):
+            for g in ("4", "8", "16"):
+                os.environ["MIDAGMA_EXP_FAST_GROUP"] = g
+                print(f"MIDAGMA_EXP_FAST_GROUP={g}", end=" ")
+                cov_case(d, 2 * d, 10, K)
+        os.environ.pop("MIDAGMA_EXP_FAST_GROUP")
     if which == "b128":  # 64 < d <= 128 (run with MIDAGMA_EXP_BINV128=0 / 1: read once per process)
         for d in (65, 100, 128):
             print(f"MIDAGMA_EXP_BINV128={os.environ.get('MIDAGMA_EXP_BINV128', '1')}", end=" ")
