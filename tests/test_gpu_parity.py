@@ -438,6 +438,27 @@ def test_blocked_fast_path_trajectory(hip, d):
         assert abs(obj - obj_r) <= 1e-10 * abs(obj_r) and abs(h - h_r) <= 1e-9 * max(1.0, abs(h_r))
 
 
+@pytest.mark.parametrize("d", [700, 1150])
+def test_blocked_lookahead_residual_experiment(hip, monkeypatch, d):
+    """The look-ahead residual experiment (MIDAGMA_EXP_RESID_LA=1, DESIGN.md section 8: block
+    g's launches prepare block g+1's R = I - (A X0 - A(g+1,G) P_g A(G,g+1) X0)) keeps the
+    oracle's iterations, W and checkpoint objectives.  d=700 -> D=768 (B2=256, 3 outer blocks),
+    1150 -> 1152 (B2=128, 9)."""
+    monkeypatch.setenv("MIDAGMA_EXP_RESID_LA", "1")
+    X, _, _ = make_dataset(d, 2 * d, seed=d + 3)
+    o = _oracle(X)
+    o.checkpoint = 40
+    K = 130
+    sol = _solver(d, o.cov)
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=40, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert res.iters == tr.iters == K and res.success
+    assert np.abs(W - Wr).max() <= 1e-9
+    for c, (_, obj_r, _, h_r) in zip(res.checkpoints, tr.checkpoints):
+        assert abs(c[1] - obj_r) <= 1e-10 * abs(obj_r) and abs(c[3] - h_r) <= 1e-9 * max(1.0, abs(h_r))
+
+
 def test_blocked_path_line_search(hip):
     """The domain line search (linear.py:230-241) on the blocked-inverse path: at d=300, lr=0.3
     the reference halves lr three times in 60 steps.  The fast slots take the domain flags from
