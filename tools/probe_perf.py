@@ -181,6 +181,9 @@ if __name__ == "__main__":
     if which == "tcc":
         for d, K in ((20, 2000), (100, 500), (300, 200), (1000, 50)):
             trek_case(d, "tcc", K)
+    if which == "shards":  # config 4's per-rank shard at N = 1, 2, 4, 8 GPUs, timed on one GPU
+        for n, K in ((1_000_000, 10), (500_000, 20), (250_000, 40), (125_000, 80)):
+            data_case(1000, n, 2, K)
     if which == "data125k":
         data_case(1000, 125000, 3, 60)
     if which == "data1m":
