@@ -221,7 +221,7 @@ __global__ __launch_bounds__(NTHREADS) void nm_pass_kernel(const double* __restr
 // prefetch depth of the panel / trailing tiles (experiment knob MIDAGMA_EXP_T32_PF: 1, 2, 3;
 // d=1000 fast slot: 4160 steps/s at 1, 4340 at 3, two runs each)
 static int t32_pf() {
-  static const int pf = getenv("MIDAGMA_EXP_T32_PF") ? atoi(getenv("MIDAGMA_EXP_T32_PF")) : 3;
+  static const int pf = (int)knob("MIDAGMA_EXP_T32_PF", 3);
   return pf < 1 ? 1 : (pf > 3 ? 3 : pf);
 }
 
@@ -336,19 +336,19 @@ __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __re
 
 // (D - B2) from which the trailing update runs on the 128-tile GEMM: (D - B2)/128 >= 14
 // gives >= 196 workgroups
-static const int64_t TRAIL128_MIN = getenv("MIDAGMA_EXP_TRAIL128") ? atoll(getenv("MIDAGMA_EXP_TRAIL128")) : 1792;
+static const int64_t TRAIL128_MIN = knob("MIDAGMA_EXP_TRAIL128", 1792);
 
 int binv_block(int64_t D) {
   // D = 128 (64 < d <= 128): one outer block, so the fast slot's whole inverse is the warm-started
   // product form (3 launches instead of the Gauss-Jordan's prologue and 4 block steps)
-  static const bool b128 = !(getenv("MIDAGMA_EXP_BINV128") && atoi(getenv("MIDAGMA_EXP_BINV128")) == 0);
+  static const bool b128 = knob("MIDAGMA_EXP_BINV128", 1) != 0;
   if (D == 128) return b128 ? 128 : 0;
   // Experiment (MIDAGMA_EXP_BINV512=1): D = 512 as one 512-wide block, the fast slot's inverse
   // the product form alone (a residual and two pass launches instead of two outer steps of
   // five).  Correct (the GPU tier passes with it on) but slower: d=300/400/500 7.2k/6.9k/6.8k
   // vs 11.2k/10.7k/10.4k steps/s (the 512-wide pass kernel holds 256 VGPRs, one wave per SIMD,
   // and its 1024 workgroups run in four rounds).
-  static const bool b512 = getenv("MIDAGMA_EXP_BINV512") && atoi(getenv("MIDAGMA_EXP_BINV512")) == 1;
+  static const bool b512 = knob("MIDAGMA_EXP_BINV512", 0) == 1;
   if (D == 512 && b512) return 512;
   if (D < 256 || D % 128 != 0) return 0;  // fast path not available: plain GJ
   return D % 256 == 0 ? 256 : 128;
@@ -391,8 +391,7 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
 // d=1400 1968 -> 2000 steps/s; with LW and LZ both in the first pass, whose grid then needs two
 // rounds: d=1000 4285).
 static bool resid_lookahead() {
-  const char* e = getenv("MIDAGMA_EXP_RESID_LA");
-  return e && atoi(e) == 1;
+  return knob("MIDAGMA_EXP_RESID_LA", 0) == 1;
 }
 
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,

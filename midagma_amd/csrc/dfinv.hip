@@ -586,7 +586,7 @@ Plan make_plan(int64_t D, int passes, int nwg, double hop_us) {
 
 bool df_available(int64_t D) {
   if (D % DF_B2 != 0 || D < 2 * DF_B2 || D / DF_B2 > DF_MAX_K2 || binv_block(D) != DF_B2) return false;
-  static const int64_t maxd = getenv("MIDAGMA_EXP_DF_MAXD") ? atoll(getenv("MIDAGMA_EXP_DF_MAXD")) : 1536;
+  static const int64_t maxd = knob("MIDAGMA_EXP_DF_MAXD", 1536);
   return D <= maxd;
 }
 
@@ -599,7 +599,7 @@ int64_t df_ctl_ints(int64_t D) {
 DfPlanHost df_plan(int64_t D, int passes, int nwg) {
   static std::mutex mu;
   static std::map<std::pair<int64_t, int>, std::pair<int, Plan>> cache;  // (D, passes) -> (nwg, plan)
-  static const double hop = getenv("MIDAGMA_EXP_DF_HOP") ? atof(getenv("MIDAGMA_EXP_DF_HOP")) : 1.0;
+  static const double hop = knob_f("MIDAGMA_EXP_DF_HOP", 1.0);
   std::lock_guard<std::mutex> lk(mu);
   auto key = std::make_pair(D, passes);
   auto it = cache.find(key);

@@ -710,8 +710,8 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
   // (K % 16 suffices for the pipelined kernel: the k loop of a padded problem may stop at the
   // first 16-multiple past the logical size, the rest of A's k range being zero)
   if (M % 64 || N % 64 || K % 16 || split < 1) throw std::invalid_argument("launch_gemm: bad shape");
-  static const bool force64 = getenv("MIDAGMA_EXP_GEMM64") != nullptr;  // experiment knobs
-  static const bool no_pipe = getenv("MIDAGMA_EXP_NO_PIPE") != nullptr;
+  static const bool force64 = knob_set("MIDAGMA_EXP_GEMM64");  // experiment knobs (knobs.h)
+  static const bool no_pipe = knob_set("MIDAGMA_EXP_NO_PIPE");
   if (M % 128 == 0 && N % 128 == 0 && K % 16 == 0 && !force64 && !no_pipe &&
       (epi == EPI_STORE || (epi == EPI_SIGMOID && split == 1 && bmode == B_PLAIN))) {
     const int64_t ktiles16 = K / 16;
@@ -803,7 +803,7 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
 
 bool gemm_trail_supported(const GemmSpec& gs) {
   return gs.M % 128 == 0 && gs.N % 128 == 0 && gs.K % 16 == 0 && gs.split >= 1 &&
-         getenv("MIDAGMA_EXP_GEMM64") == nullptr && getenv("MIDAGMA_EXP_NO_PIPE") == nullptr;
+         !knob_set("MIDAGMA_EXP_GEMM64") && !knob_set("MIDAGMA_EXP_NO_PIPE");
 }
 
 // n_trail < 0: the trailing update of the 128-tile kind (launch_trail128's grid)
@@ -874,7 +874,7 @@ void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int
   if (tm <= 0) return;
   const int64_t G0 = g * B2;
   // A = Ain[:, G] (lda D), B = Aout[G, :] (the row panel), C = Aout, C0 = Ain; K = B2
-  static const bool no_pipe = getenv("MIDAGMA_EXP_NO_PIPE") != nullptr;  // experiment knob
+  static const bool no_pipe = knob_set("MIDAGMA_EXP_NO_PIPE");  // experiment knob
   if (!no_pipe)
     hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
                        kGemmPipeLds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,

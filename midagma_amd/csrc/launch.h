@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "common.h"
+#include "knobs.h"
 
 namespace midagma {
 

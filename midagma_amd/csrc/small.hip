@@ -629,7 +629,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 // d <= 64 (DS = 64: single-buffered images, 16 waves; MIDAGMA_EXP_SMALL64=0 keeps 32 < d <= 64 on
 // the graph-replayed slots)
 int small_block(int64_t d) {
-  static const bool s64 = !(getenv("MIDAGMA_EXP_SMALL64") && atoi(getenv("MIDAGMA_EXP_SMALL64")) == 0);
+  static const bool s64 = knob("MIDAGMA_EXP_SMALL64", 1) != 0;
   return d <= 16 ? 16 : (d <= 32 ? 32 : (d <= 64 && s64 ? 64 : 0));
 }
 

@@ -60,18 +60,18 @@ struct midagma_solver {
   // depends on W only); fork / join are events inside the captured slot graph
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  bool fork_inv = getenv("MIDAGMA_EXP_NO_FORK") == nullptr;  // experiment knob
+  bool fork_inv = !knob_set("MIDAGMA_EXP_NO_FORK");  // experiment knobs: knobs.h
   std::string err;
 
   DevBuf W, m, v, Mt, cov, covs, minc, mexc, P, R, C, pivlog, partials, bc_table, zown, scratch, Gtmp, Pstore;
   // ((-mu) cov)^T: the cov-mode score GEMM reads its A operand k-major (coalesced tile rows)
   DevBuf covsT;
-  bool cov_at = getenv("MIDAGMA_EXP_COV_AMODE0") == nullptr;  // experiment knob
-  bool cov_iw = getenv("MIDAGMA_EXP_COV_IW") != nullptr;      // experiment knob
+  bool cov_at = !knob_set("MIDAGMA_EXP_COV_AMODE0");
+  bool cov_iw = knob_set("MIDAGMA_EXP_COV_IW");
   DevBuf npart;  // checkpoint-step norm partials (fused_update -> control)
   // cov mode, l2, d <= 64, no trek regularizer: the one-workgroup persistent loop (small.hip)
   DevBuf scarry, sprev;  // between two small-loop launches: pending norms + warm count, last inverses
-  bool use_small = getenv("MIDAGMA_EXP_NO_SMALL") == nullptr;  // experiment knob
+  bool use_small = !knob_set("MIDAGMA_EXP_NO_SMALL");
   bool small_on() const {
     return use_small && mode == MIDAGMA_MODE_COV && loss == MIDAGMA_LOSS_L2 && !trek_on && small_block(d) > 0;
   }
@@ -92,11 +92,13 @@ struct midagma_solver {
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
   DevBuf Malt, Pst2, Pst2b, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone, nmLW, nmLZ, nmLPZ;
-  // the fast slot's inverse as one dataflow launch (dfinv.hip; MIDAGMA_EXP_DF=1 enables: measured
-  // slower than the launch-per-phase inverse at d = 500 and 1000)
+  // the fast slot's inverse as one dataflow launch (dfinv.hip; experiments build only,
+  // MIDAGMA_EXP_DF=1: measured slower than the launch-per-phase inverse)
   bool df_on = false;
+#ifdef MIDAGMA_EXPERIMENTS
   DevBuf dfA, dfY, dfQ, dfP, dfCtl, dfTasks[2], dfWoff[2], dfStamps;
   DfWork dfw{};
+#endif
   bool fast_ready = false;  // Pst2 holds the previous slot's outer-block inverses
   double* zbuf = nullptr;  // d x d (+64 tail) score partial; internal or bound
   int64_t zbuf_cap = 0;
@@ -135,7 +137,7 @@ struct midagma_solver {
   // warm start usually converges in 2); the host falls back to 3 for a while after a hand-back
   hipGraphExec_t g_part1 = nullptr, g_part2 = nullptr, g_full = nullptr, g_fast = nullptr, g_fastN = nullptr;
   hipGraphExec_t g_fast2 = nullptr, g_fastN2 = nullptr;
-  bool nm_adapt = !(getenv("MIDAGMA_EXP_NM_ADAPT") && atoi(getenv("MIDAGMA_EXP_NM_ADAPT")) == 0);  // knob
+  bool nm_adapt = knob("MIDAGMA_EXP_NM_ADAPT", 1) != 0;
   int64_t three_pass_left = 0;  // fast slots still to run with 3 passes (after a 2-pass hand-back)
   bool graphs_valid = false;
 
@@ -143,9 +145,13 @@ struct midagma_solver {
     destroy_graphs();
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
-                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &npart, &XT, &IW, &scarry, &sprev, &dfA, &dfY,
-                      &dfQ, &dfP, &dfCtl, &dfTasks[0], &dfTasks[1], &dfWoff[0], &dfWoff[1], &dfStamps})
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &npart, &XT, &IW, &scarry,
+                      &sprev})
       b->release();
+#ifdef MIDAGMA_EXPERIMENTS
+    for (DevBuf* b : {&dfA, &dfY, &dfQ, &dfP, &dfCtl, &dfTasks[0], &dfTasks[1], &dfWoff[0], &dfWoff[1], &dfStamps})
+      b->release();
+#endif
     for (DevBuf& b : tbufs) b.release();
     for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices, &cA, &cMi, &cS, &cvec, &cpart, &cP, &cR, &cC}) b->release();
     if (cgates) (void)hipFree(cgates);
@@ -192,7 +198,7 @@ struct midagma_solver {
   // 128-tile kernel, D % 128 == 0; bit-identical: the skipped terms are exact zeros)
   int64_t Kd() const { return D % 128 == 0 ? (d + 15) / 16 * 16 : D; }
   bool forked_inverse() const { return side != nullptr && !blocked() && mode == MIDAGMA_MODE_DATA; }
-  bool data_binv = getenv("MIDAGMA_EXP_DATA_FLAT_GJ") == nullptr;  // experiment knob
+  bool data_binv = !knob_set("MIDAGMA_EXP_DATA_FLAT_GJ");
   bool data_binv_on() const { return data_binv && mode == MIDAGMA_MODE_DATA && binv_block(D) > 0; }
 
   // ---- the slot -----------------------------------------------------------
@@ -249,16 +255,18 @@ struct midagma_solver {
   // one dataflow launch when df_on)
   // fuse (nullable): a GEMM the inverse may carry in its last trailing launch; returns whether it did
   bool enqueue_build_inverse(bool fast, int passes, const GemmSpec* fuse = nullptr) {
+#ifdef MIDAGMA_EXPERIMENTS
     if (fast && df_on) {
       launch_build_at(W.p, D, /*square=*/true, dfw.A[0], D, d, 0.0, d_params, d_state, stream, IW.p);
       launch_df_inverse(Mt.p, D, dfw, binv(), passes <= 2 ? 2 : 3, d_state, stream);
       return false;
     }
+#endif
     launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state, stream,
                     IW.p);
     return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse);
   }
-  bool fuse_gemm = !(getenv("MIDAGMA_EXP_FUSE_GEMM") && atoi(getenv("MIDAGMA_EXP_FUSE_GEMM")) == 0);
+  bool fuse_gemm = knob("MIDAGMA_EXP_FUSE_GEMM", 1) != 0;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
   GemmSpec score_cov_spec() const {
@@ -542,7 +550,7 @@ struct midagma_solver {
           if (waves < best) best = waves, cov_split = sp;
         }
       }
-      if (const char* e = getenv("MIDAGMA_EXP_COV_SPLIT")) cov_split = atoi(e);  // experiment knob
+      if (knob_set("MIDAGMA_EXP_COV_SPLIT")) cov_split = (int)knob("MIDAGMA_EXP_COV_SPLIT", cov_split);
       if (cov_split > 1) cov_parts.alloc((size_t)cov_split * DD);
     }
     if (mode == MIDAGMA_MODE_COV) B2 = binv_block(D);
@@ -557,8 +565,9 @@ struct midagma_solver {
       nmPart.alloc((size_t)(D / b2) * (NM_PASSES + 1) * PART_STRIDE);
       nmDone.alloc(D / b2);
     }
-    const char* dfe = getenv("MIDAGMA_EXP_DF");
-    if (blocked() && mode == MIDAGMA_MODE_COV && df_available(D) && dfe && atoi(dfe) != 0) setup_df();
+#ifdef MIDAGMA_EXPERIMENTS
+    if (blocked() && mode == MIDAGMA_MODE_COV && df_available(D) && knob("MIDAGMA_EXP_DF", 0) != 0) setup_df();
+#endif
     zown.alloc(DD + 64);
     HIP_TRY(hipMemsetAsync(zown.p, 0, (DD + 64) * sizeof(double), stream));
     zbuf = zown.p;
@@ -576,13 +585,14 @@ struct midagma_solver {
     }
   }
 
+#ifdef MIDAGMA_EXPERIMENTS
   // buffers and the two task plans (2 and 3 product-form passes) of the one-launch inverse
   void setup_df() {
     const int64_t K2 = D / 256, BB = 256 * 256, DD = D * D;
     int ncu = 0;
     HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
     // workgroups per CU (the kernel's registers admit 2; every one must be resident)
-    static const int per_cu = getenv("MIDAGMA_EXP_DF_PER_CU") ? std::max(1, std::min(2, atoi(getenv("MIDAGMA_EXP_DF_PER_CU")))) : 2;
+    static const int per_cu = std::max(1, std::min(2, (int)knob("MIDAGMA_EXP_DF_PER_CU", 2)));
     ncu *= per_cu;
     dfA.alloc((size_t)K2 * DD);
     dfY.alloc((size_t)K2 * (NM_PASSES + 1) * BB);
@@ -606,7 +616,7 @@ struct midagma_solver {
     dfw.P = dfP.p;
     dfw.ctl = reinterpret_cast<int*>(dfCtl.p);
     dfw.nwg = ncu;
-    if (getenv("MIDAGMA_DF_STAMPS")) {  // diagnostics: per-task timestamps of the last launch
+    if (knob_set("MIDAGMA_DF_STAMPS")) {  // diagnostics: per-task timestamps of the last launch
       dfStamps.alloc((size_t)3 * std::max(df_plan(D, 3, ncu).tasks->size(), df_plan(D, 2, ncu).tasks->size()) / 12);
       HIP_TRY(hipMemset(dfStamps.p, 0, dfStamps.n * sizeof(double)));
       dfw.stamps = reinterpret_cast<unsigned long long*>(dfStamps.p);
@@ -620,6 +630,9 @@ struct midagma_solver {
     HIP_TRY(hipMemcpy(&t, dfw.ctl + 2 * 32, sizeof(int), hipMemcpyDeviceToHost));
     return t;
   }
+#else
+  int df_timeouts() { return 0; }
+#endif
 
   void upload_matrix(DevBuf& dst, const double* src, int64_t ld_src) {
     HIP_TRY(hipMemcpy2DAsync(dst.p, D * sizeof(double), src, ld_src * sizeof(double), d * sizeof(double), d,
@@ -783,11 +796,11 @@ struct midagma_solver {
     handback_count += handbacks;
     fast_batch = bmax;
     if (const int to = df_timeouts()) throw std::runtime_error("one-launch inverse: " + std::to_string(to) + " wait timeouts");
-    static const bool dbg = getenv("MIDAGMA_DEBUG_HANDBACKS") != nullptr;  // diagnostics
+    static const bool dbg = knob_set("MIDAGMA_DEBUG_HANDBACKS");  // diagnostics (experiments build)
     if (dbg) fprintf(stderr, "drive_blocked: %lld slots, %lld hand-backs\n", (long long)launched, (long long)handbacks);
   }
   int64_t handback_count = 0;
-  int fast_group = getenv("MIDAGMA_EXP_FAST_GROUP") ? std::max(1, atoi(getenv("MIDAGMA_EXP_FAST_GROUP"))) : 4;
+  int fast_group = std::max(1, (int)knob("MIDAGMA_EXP_FAST_GROUP", 4));
   int64_t fast_batch = 64;
 
   // Small d: the whole inner loop in one persistent workgroup, kSmallBatch slots per launch
@@ -940,16 +953,14 @@ int midagma_create(midagma_solver** out, int loss, int mode, int64_t d, int devi
   // 128-multiples feed the 128x128 GEMM tiles.  Cov mode pads 129 <= d <= 192 to 256 as well: the
   // blocked inverse then has one 256-wide outer block, and its warm-started product form beats
   // the flat Gauss-Jordan's 6 block steps on 192 (data mode keeps 192: X's columns are GEMM work)
-  const char* p256 = getenv("MIDAGMA_EXP_COV_PAD256");
-  const bool pad256 = mode == MIDAGMA_MODE_COV && !(p256 && atoi(p256) == 0);
+  const bool pad256 = mode == MIDAGMA_MODE_COV && knob("MIDAGMA_EXP_COV_PAD256", 1) != 0;
   s->D = d > 192 || (pad256 && d > 128) ? (d + 127) / 128 * 128 : round_up64(d);
   // Cov mode, 256 < d <= 640: D to a multiple of 256, so the blocked inverse runs B2 = 256 outer
   // blocks (2 instead of 3 at D = 384 -> 512, 3 instead of 5 at 640 -> 768: d=300 11.1k -> 11.3k,
   // d=600 6.4k -> 7.0k steps/s).  Larger D keep B2 = 128 (d=1150 even, d=1400 -3.5%, d=1700
   // even: the padded GEMM work outweighs the saved outer steps).  Knob MIDAGMA_EXP_COV_PAD_B2:
   // 0 off, 1 at every d > 256.
-  const char* pb2 = getenv("MIDAGMA_EXP_COV_PAD_B2");
-  const int pad_b2 = pb2 ? atoi(pb2) : -1;
+  const int pad_b2 = (int)knob("MIDAGMA_EXP_COV_PAD_B2", -1);
   if (mode == MIDAGMA_MODE_COV && d > 256 && (pad_b2 == 1 || (pad_b2 < 0 && d <= 640)))
     s->D = (d + 255) / 256 * 256;
   s->device = device;
@@ -1073,8 +1084,7 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     // GEMMs that fill the chip, the pivoted inverse's 20-odd dependent launches wait for CU slots
     // and end after the GEMMs (logistic d=1000, n=1e4: 1.01 ms per slot for 0.70 ms of GEMMs);
     // large shards keep the fork, which hides it (MIDAGMA_EXP_DATA_FAST_ROWS: the row bound)
-    static const int64_t fast_rows =
-        getenv("MIDAGMA_EXP_DATA_FAST_ROWS") ? atoll(getenv("MIDAGMA_EXP_DATA_FAST_ROWS")) : 16384;
+    static const int64_t fast_rows = knob("MIDAGMA_EXP_DATA_FAST_ROWS", 16384);
     const int b2 = binv_block(D);
     const int B2_new = (b2 > 0 && s->n_pad <= fast_rows && s->Malt.p) ? b2 : 0;
     if (B2_new != s->B2) s->graphs_valid = false;
@@ -1812,6 +1822,7 @@ extern "C" int midagma_counter_advance(int64_t* counter, void* stream) {
   });
 }
 
+#ifdef MIDAGMA_EXPERIMENTS
 // Diagnostics (not part of the ABI header): the one-launch inverse's task plan for D, passes
 // and nwg workgroups, as planned on the host (no GPU needed).  tasks (12 ints per task, grouped
 // by workgroup) and woff (nwg + 1) may be null to query the sizes.  Returns 0, or -1.
@@ -1842,3 +1853,4 @@ extern "C" int64_t midagma_debug_df_stamps(midagma_solver* s, unsigned long long
   if (hipMemcpy(out, s->dfStamps.p, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return n;
 }
+#endif  // MIDAGMA_EXPERIMENTS

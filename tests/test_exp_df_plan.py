@@ -9,6 +9,8 @@ import heapq
 import numpy as np
 import pytest
 
+pytestmark = pytest.mark.experiment  # the plan lives in the experiments build (knobs.h)
+
 from midagma_amd import _lib
 
 TASK_INTS = 12

@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = pytest.mark.experiment
 
 torch = pytest.importorskip("torch")
 

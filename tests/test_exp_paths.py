@@ -1,0 +1,71 @@
+"""Experiment paths of the experiments build (`make -C midagma_amd/csrc exp`, knobs.h): rejected
+or diagnostic alternatives of the product paths, checked against the oracle and the product path
+so that their DESIGN.md section 8 measurements stay repeatable.  Not part of the default
+`-m gpu` tier; run with
+
+    MIDAGMA_LIB=midagma_amd/libmidagma_hip_exp.so python -m pytest -m experiment tests
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.experiment
+
+torch = pytest.importorskip("torch")
+
+from midagma_amd.simulate import make_dataset  # noqa: E402
+from oracle.dagma_oracle import LinearOracle  # noqa: E402
+
+
+def _solver(d, cov):
+    from midagma_amd.solver import HipSolver
+    s = HipSolver(d, "l2", "cov", device=0)
+    s.set_cov(cov)
+    return s
+
+
+def _oracle(X, checkpoint):
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, checkpoint)
+    return o
+
+
+@pytest.mark.parametrize("d", [5, 20, 32, 50, 64])
+def test_small_path_vs_graph_path(d, monkeypatch):
+    """The persistent kernel (small.hip) and the graph-replayed slots it replaces
+    (MIDAGMA_EXP_NO_SMALL) agree to rounding: same iterations, W within 1e-11 after 500 steps
+    (checkpoint every 100: Gauss-Jordan slots between runs of product-form slots)."""
+    X, _, _ = make_dataset(d, max(200, 10 * d), seed=11)
+    o = _oracle(X, 50)
+    K = 500
+    a = _solver(d, o.cov)
+    Wa = np.zeros((d, d))
+    ra = a.minimize(Wa, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100)
+    monkeypatch.setenv("MIDAGMA_EXP_NO_SMALL", "1")
+    b = _solver(d, o.cov)
+    monkeypatch.delenv("MIDAGMA_EXP_NO_SMALL")
+    Wb = np.zeros((d, d))
+    rb = b.minimize(Wb, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100)
+    assert ra.iters == rb.iters == K and ra.slots == rb.slots
+    assert np.abs(Wa - Wb).max() <= 1e-11
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("d", [700, 1150])
+def test_blocked_lookahead_residual_experiment(monkeypatch, d):
+    """The look-ahead residual (MIDAGMA_EXP_RESID_LA=1, DESIGN.md section 8: block g's launches
+    prepare block g+1's R = I - (A X0 - A(g+1,G) P_g A(G,g+1) X0)) keeps the oracle's
+    iterations, W and checkpoint objectives.  d=700 -> D=768 (B2=256, 3 outer blocks),
+    1150 -> 1152 (B2=128, 9)."""
+    monkeypatch.setenv("MIDAGMA_EXP_RESID_LA", "1")
+    X, _, _ = make_dataset(d, 2 * d, seed=d + 3)
+    o = _oracle(X, 40)
+    K = 130
+    sol = _solver(d, o.cov)
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=40, want_checkpoints=True)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert res.iters == tr.iters == K and res.success
+    assert np.abs(W - Wr).max() <= 1e-9
+    for c, (_, obj_r, _, h_r) in zip(res.checkpoints, tr.checkpoints):
+        assert abs(c[1] - obj_r) <= 1e-10 * abs(obj_r) and abs(c[3] - h_r) <= 1e-9 * max(1.0, abs(h_r))

@@ -27,7 +27,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("K", [1000, 2000])
-def test_config2_trajectory_d1000(golden, K):
+def test_config2_trajectory_d1000(golden, parity, K):
     from threadpoolctl import threadpool_limits
     from midagma_amd.solver import HipSolver
     f = golden("traj_d1000.npz")
@@ -43,13 +43,14 @@ def test_config2_trajectory_d1000(golden, K):
     env = float(f[f"env_K{K}"])
     dW = float(np.abs(W - f[f"W_K{K}"]).max())
     print(f"K={K}: max|W_gpu - W_ref| = {dW:.3e} (reference envelope {env:.3e})")
+    parity("config2", dW, 1e-9, f"max|dW| K={K}")
     assert res.iters == K and res.success
     assert env < 1e-6                      # the horizon is inside the calibrated range
     assert dW <= 1e-5                      # north star
     assert dW <= 1e-9                      # what the kernels deliver at this horizon
 
 
-def test_config3_d5000():
+def test_config3_d5000(parity):
     from midagma_amd.solver import HipSolver
     d = 5000
     X, _, _ = make_dataset(d, 50_000, seed=0)
@@ -71,6 +72,7 @@ def test_config3_d5000():
     res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=4, want_checkpoints=True)
     s.close()
     Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    parity("config3", float(np.abs(W - Wr).max()), 1e-9, f"max|dW| K={K}")
     assert res.iters == tr.iters == K and res.success
     assert np.abs(W - Wr).max() <= 1e-9
     assert [c[0] for c in res.checkpoints] == [c[0] for c in tr.checkpoints] == [4, 8]
@@ -84,7 +86,7 @@ KEYS = ["fc1.weight", "fc1.bias", "fc2.0.weight", "fc2.0.bias"]
 
 
 @pytest.mark.parametrize("K", [1, 10, 100])
-def test_config5_mlp_minimize_d200(K):
+def test_config5_mlp_minimize_d200(parity, K):
     from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
     from oracle.mlp_oracle import OracleMLP, load_params, nonlinear_minimize
     d, n = 200, 1000
@@ -105,11 +107,15 @@ def test_config5_mlp_minimize_d200(K):
     ok_ref, it = nonlinear_minimize(ref, torch.from_numpy(X), K, 2e-4, 0.02, 0.005, 0.1, 1.0)
     assert ok and ok_ref and it == K
     sd, rd = model.state_dict(), ref.state_dict()
+    devs = {}
     for k in KEYS:
         r = rd[k].numpy()
         dev = np.abs(sd[k].cpu().numpy() - r).max()
         print(f"K={K} {k}: max|d| = {dev:.3e} (max|p| {np.abs(r).max():.3e})")
-        assert dev <= 1e-9 * max(1.0, np.abs(r).max()), k
+        devs[k] = dev / max(1.0, np.abs(r).max())
+    parity("config5", max(devs.values()), 1e-9, f"max|dparam|/max(1,|p|) K={K}")
+    for k in KEYS:
+        assert devs[k] <= 1e-9, k
 
 
 @pytest.mark.parametrize("graph", [True, False])

@@ -1,6 +1,5 @@
 """The one-workgroup small-d inner loop (csrc/small.hip: cov mode, l2, d <= 64) against the
-oracle (the numpy/scipy restatement of linear.py:165-333), against the graph-replayed slot
-path it replaces (MIDAGMA_EXP_NO_SMALL), and across launch boundaries (run_slots chunks that
+oracle (the numpy/scipy restatement of linear.py:165-333) and across launch boundaries (run_slots chunks that
 end right after a checkpoint step, so the pending checkpoint norms cross launches)."""
 import numpy as np
 import pytest
@@ -119,28 +118,7 @@ def test_small_path_launch_boundaries_bit_identical(d):
     b.close()
 
 
-@pytest.mark.parametrize("d", [5, 20, 32, 50, 64])
-def test_small_path_vs_graph_path(d, monkeypatch):
-    """The persistent kernel and the graph-replayed slots (MIDAGMA_EXP_NO_SMALL) agree to
-    rounding: same iterations, W within 1e-11 after 500 steps (checkpoint every 100: Gauss-Jordan
-    slots between runs of product-form slots)."""
-    o = _oracle(d)
-    K = 500
-    a = _solver(d, o.cov)
-    Wa = np.zeros((d, d))
-    ra = a.minimize(Wa, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100)
-    monkeypatch.setenv("MIDAGMA_EXP_NO_SMALL", "1")
-    b = _solver(d, o.cov)
-    monkeypatch.delenv("MIDAGMA_EXP_NO_SMALL")
-    Wb = np.zeros((d, d))
-    rb = b.minimize(Wb, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100)
-    assert ra.iters == rb.iters == K and ra.slots == rb.slots
-    assert np.abs(Wa - Wb).max() <= 1e-11
-    a.close()
-    b.close()
-
-
-def test_small_path_long_trajectory_d20(golden):
+def test_small_path_long_trajectory_d20(golden, parity):
     """10000 steps at d=20 against the reference's own trajectory (traj_d20.npz): ~9990
     product-form slots between the Gauss-Jordan checkpoint slots."""
     t = golden("traj_d20.npz")
@@ -151,5 +129,6 @@ def test_small_path_long_trajectory_d20(golden):
     W = np.zeros((20, 20))
     res = s.minimize(W, 1.0, 10000, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
     assert res.iters == 10000
+    parity("config1", float(np.abs(W - t["W_K10000"]).max()), max(1e-9, 2 * float(t["env_K10000"])), "max|dW| K=10000")
     assert np.abs(W - t["W_K10000"]).max() <= max(1e-9, 2 * float(t["env_K10000"]))
     s.close()

@@ -5,13 +5,16 @@
 #
 # TASK
 #   tests [PATHS/ARGS]    pytest -m gpu (default path: tests) (one process, as the driver runs it) -> gpurun_out/gpu_tests.log
+#   exptests [ARGS]       pytest -m experiment on the experiments build (libmidagma_hip_exp.so, knobs.h)
+#                         -> gpurun_out/exp_tests.log
 #   smoke                 __graft_entry__.smoke()
 #   bench [BENCH ARGS]    python bench.py -> gpurun_out/bench.json (+ .err)
 #   prof LEG              rocprofv3 --kernel-trace --stats of one bench leg -> gpurun_out/prof_LEG/
 #                         LEG: data | cov | large | small | logistic | mlp (one bench leg each)
 #   pmc LEG               FETCH_SIZE and WRITE_SIZE passes (each its own run) of one leg,
 #                         summarised per kernel -> gpurun_out/pmc_LEG.json (tools/pmc_summary.py)
-#   probe NAME [ARGS]     python tools/NAME.py ARGS (probe_perf, peak_probe, blocked_debug, ...)
+#   probe NAME [ARGS]     python tools/NAME.py ARGS (probe_perf, peak_probe, blocked_debug, ...); probe_perf
+#                         loads the experiments build (its comparisons set MIDAGMA_EXP_* knobs)
 # Several tasks may be chained in one call: `bash tools/gpu.sh tests -- bench -- prof cov`.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
@@ -47,6 +50,11 @@ run_task() {
       timeout -k 10 1500 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
         > gpurun_out/gpu_tests.log 2>&1; local rc=$?
       grep -E "passed|failed|error" gpurun_out/gpu_tests.log | tail -3; return $rc ;;
+    exptests)
+      [ $# -eq 0 ] && set -- tests
+      MIDAGMA_LIB="$R/midagma_amd/libmidagma_hip_exp.so" timeout -k 10 900 python -u -m pytest -m experiment -x -v \
+        --timeout 300 --timeout-method thread "$@" > gpurun_out/exp_tests.log 2>&1; local rc=$?
+      grep -E "passed|failed|error" gpurun_out/exp_tests.log | tail -3; return $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; local rc=$?
       tail -3 gpurun_out/smoke.log; return $rc ;;

@@ -1,13 +1,16 @@
 """Per-task timing of the one-launch fast-slot inverse (csrc/dfinv.hip), development tool:
 python tools/probe_df.py [d] [passes] -- runs a few cov-mode slots with MIDAGMA_DF_STAMPS set,
 then prints per task type the compute and wait times and the outer steps' timeline of the
-last launch (100 MHz device clock)."""
+last launch (100 MHz device clock).  The one-launch inverse exists in the experiments build
+only (midagma_amd/libmidagma_hip_exp.so, `make -C midagma_amd/csrc exp`)."""
 import ctypes as C
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["MIDAGMA_DF_STAMPS"] = "1"
+os.environ.setdefault("MIDAGMA_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "midagma_amd", "libmidagma_hip_exp.so"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
 

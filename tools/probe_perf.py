@@ -1,9 +1,15 @@
-"""Quick GPU timing probe (development tool): steps/s of the slot at several sizes."""
+"""Quick GPU timing probe (development tool): steps/s of the slot at several sizes.
+
+Loads the experiments build (midagma_amd/libmidagma_hip_exp.so, `make -C midagma_amd/csrc exp`):
+its comparisons switch MIDAGMA_EXP_* knobs, which the product library compiles to their
+defaults (csrc/knobs.h).  MIDAGMA_LIB overrides."""
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, _REPO)
+os.environ.setdefault("MIDAGMA_LIB", os.path.join(_REPO, "midagma_amd", "libmidagma_hip_exp.so"))
 import numpy as np
 import torch  # noqa: F401
 
