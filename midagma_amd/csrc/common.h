@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "status.h"
+
 namespace midagma {
 
 constexpr int TILE = 64;          // tile edge of every blocked kernel
@@ -23,16 +25,6 @@ constexpr int NRED = 256;         // fixed number of partial-sum slots (determin
 // need stride = 16 mod 32.
 constexpr int SA = 66;            // operand image stored [m][k]
 constexpr int SB = 80;            // operand image stored [k][n] (or [k][m])
-
-enum Status : int32_t {
-  ST_RUNNING = 0,
-  ST_DONE = 1,          // max_iter reached or checkpoint tolerance met  -> (W, True)
-  ST_FAILED = 2,        // left the M-matrix domain at iter 1 or s <= 0.9 -> (W, False)
-  ST_LR_UNDERFLOW = 3,  // lr halved below 1e-16                         -> (W, True)
-  ST_SINGULAR = 4,      // non-finite inverse                            -> LinAlgError
-  ST_NEED_GJ = 5,       // internal: the fast inverse could not run this slot (no usable warm
-                        // start, or a log-det is due); the host re-runs it on the GJ path
-};
 
 enum Action : int32_t { ACT_NOOP = 0, ACT_STEP = 1, ACT_HALVE = 2, ACT_REVERT = 3 };
 

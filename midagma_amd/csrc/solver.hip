@@ -18,6 +18,7 @@
 
 #include "../../include/midagma_hip.h"
 #include "launch.h"
+#include "slot_sched.h"
 
 using namespace midagma;
 
@@ -198,6 +199,12 @@ struct midagma_solver {
   // 128-tile kernel, D % 128 == 0; bit-identical: the skipped terms are exact zeros)
   int64_t Kd() const { return D % 128 == 0 ? (d + 15) / 16 * 16 : D; }
   bool forked_inverse() const { return side != nullptr && !blocked() && mode == MIDAGMA_MODE_DATA; }
+  // cov mode at large D (the 128-tile trailing update): the score GEMM beside the inverse
+  // (experiment knob MIDAGMA_EXP_COV_FORK: 1 on, 0 off)
+  bool cov_fork = knob("MIDAGMA_EXP_COV_FORK", 0) != 0;
+  bool cov_fork_on() const {
+    return cov_fork && side != nullptr && mode == MIDAGMA_MODE_COV && blocked() && D - B2 >= 1792 && !trek_on;
+  }
   bool data_binv = !knob_set("MIDAGMA_EXP_DATA_FLAT_GJ");
   bool data_binv_on() const { return data_binv && mode == MIDAGMA_MODE_DATA && binv_block(D) > 0; }
 
@@ -205,7 +212,20 @@ struct midagma_solver {
   // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
   void enqueue_part1(bool fast = false, int passes = NM_PASSES_RUN) {
     bool gemm_done = false;
-    if (blocked()) {
+    if (cov_fork_on()) {
+      // large D, cov mode: the score GEMM (W and cov only) on the main stream beside the inverse
+      // on the high-priority side stream, so its tiles fill the CUs the inverse's serial
+      // series / panel phases leave idle; joined before anything reads Mt
+      launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
+                      stream, IW.p);
+      HIP_TRY(hipEventRecord(ev_fork, stream));
+      HIP_TRY(hipStreamWaitEvent(side, ev_fork, 0));
+      launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, side, passes, nullptr);
+      HIP_TRY(hipEventRecord(ev_join, side));
+      enqueue_score_cov(zbuf, d_state, /*sum=*/!fast);
+      HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
+      gemm_done = true;
+    } else if (blocked()) {
       // cov fast slot: the score GEMM rides in the last trailing update's launch (its split-K
       // slices are what fused_update sums anyway); MIDAGMA_EXP_FUSE_GEMM=0 keeps it apart
       GemmSpec gs{};
@@ -576,7 +596,7 @@ struct midagma_solver {
     HIP_TRY(hipMalloc(&d_state, sizeof(State)));
     HIP_TRY(hipHostMalloc(&h_state, 2 * sizeof(State), hipHostMallocDefault));
     for (auto& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (mode == MIDAGMA_MODE_DATA && fork_inv) {
+    if ((mode == MIDAGMA_MODE_DATA && fork_inv) || (mode == MIDAGMA_MODE_COV && cov_fork && B2 > 0 && D - B2 >= 1792)) {
       int lo = 0, hi = 0;  // hi: the greatest priority (numerically least)
       HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
       HIP_TRY(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, hi));
@@ -746,76 +766,63 @@ struct midagma_solver {
   // Cov mode with the blocked inverse: fast slots in batches, a GJ (slow) slot wherever a
   // log-det is due (checkpoint), there is no warm start (first slot) or a fast slot handed
   // back (ST_NEED_GJ).  Batches stop at the next checkpoint iteration, so the host knows
-  // when the slow slot is due; one host sync per batch.  n_slots < 0: until terminal.
+  // when the slow slot is due; one host sync per batch (the choices: slot_sched.h, BlockedScheduler).
+  // n_slots < 0: until terminal.
   void drive_blocked(int64_t n_slots) {
     ensure_graphs();
-    const int64_t max_iter = hp.max_iter, checkpoint = std::max<int64_t>(hp.checkpoint, 1);
-    const int64_t cap = max_iter + max_iter / checkpoint + 512;
-    int64_t launched = 0, handbacks = 0;
-    int64_t bmax = fast_batch;  // fast batch cap: 1 after a hand-back, doubling up to 64
-    State cur = h_state[0];
-    HIP_TRY(hipMemcpyAsync(&cur, d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
+    BlockedScheduler::Carry carry;
+    carry.bmax = fast_batch;
+    carry.three_pass_left = three_pass_left;
+    carry.fast_ready = fast_ready;
+    BlockedScheduler sc(hp.max_iter, hp.checkpoint, n_slots, fast_group, g_fast2 != nullptr, carry);
+    HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    for (;;) {
-      if (cur.status != ST_RUNNING && cur.status != ST_NEED_GJ) break;
-      if (n_slots >= 0 && launched >= n_slots) break;
-      if (n_slots < 0 && (cur.slots > cap || launched > 4 * cap))
-        throw std::runtime_error("minimize: slot budget exceeded (controller stuck)");
-      int64_t it_hi = cur.iter;
-      if (cur.status == ST_NEED_GJ || cur.ckpt_pending || !fast_ready) {
-        if (cur.status == ST_NEED_GJ) {
-          ++handbacks;
-          bmax = 1;
-          static const int32_t running = ST_RUNNING;
-          HIP_TRY(hipMemcpyAsync(&d_state->status, &running, sizeof(int32_t), hipMemcpyHostToDevice, stream));
-        }
-        HIP_TRY(hipGraphLaunch(g_full, stream));  // slow slot: pivots + fresh warm starts
-        ++launched;
-        ++it_hi;
-        fast_ready = true;
+    for (SlotView cur = view(h_state[1]);;) {
+      const BlockedPlan p = sc.next(cur);
+      if (p.done) break;
+      if (p.clear_handback) {
+        static const int32_t running = ST_RUNNING;
+        HIP_TRY(hipMemcpyAsync(&d_state->status, &running, sizeof(int32_t), hipMemcpyHostToDevice, stream));
       }
-      // fast slots up to the next checkpoint iteration (the slot after it must be slow)
-      const int64_t next_ck = std::min(max_iter, (it_hi / checkpoint + 1) * checkpoint);
-      int64_t B = std::min<int64_t>(bmax, next_ck - it_hi);
-      if (n_slots >= 0) B = std::min<int64_t>(B, n_slots - launched);
+      if (p.slow) HIP_TRY(hipGraphLaunch(g_full, stream));  // pivots + fresh warm starts
       // (a hand-back inside a group turns the group's later slots into no-op launches)
-      const bool two = g_fast2 != nullptr && three_pass_left <= 0;
-      hipGraphExec_t one = two ? g_fast2 : g_fast, grp = two ? g_fastN2 : g_fastN;
-      int64_t b = 0;
-      if (grp)
-        for (; b + fast_group <= B; b += fast_group) HIP_TRY(hipGraphLaunch(grp, stream));
-      for (; b < B; ++b) HIP_TRY(hipGraphLaunch(one, stream));
-      if (!two) three_pass_left -= std::max<int64_t>(B, 0);
-      launched += std::max<int64_t>(B, 0);
+      hipGraphExec_t one = p.two_pass ? g_fast2 : g_fast, grp = p.two_pass ? g_fastN2 : g_fastN;
+      for (int64_t b = 0; b < p.groups; ++b) HIP_TRY(hipGraphLaunch(grp, stream));
+      for (int64_t b = 0; b < p.singles; ++b) HIP_TRY(hipGraphLaunch(one, stream));
       HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
-      cur = h_state[1];
-      if (cur.status != ST_NEED_GJ) bmax = std::min<int64_t>(64, 2 * bmax);
-      else if (two) three_pass_left = 512;  // residuals this far need 3 passes: stay there a while
+      cur = view(h_state[1]);
+      sc.observe(cur);
     }
-    handback_count += handbacks;
-    fast_batch = bmax;
+    fast_batch = sc.carry().bmax;
+    three_pass_left = sc.carry().three_pass_left;
+    fast_ready = sc.carry().fast_ready;
+    handback_count += sc.handbacks();
     if (const int to = df_timeouts()) throw std::runtime_error("one-launch inverse: " + std::to_string(to) + " wait timeouts");
     static const bool dbg = knob_set("MIDAGMA_DEBUG_HANDBACKS");  // diagnostics (experiments build)
-    if (dbg) fprintf(stderr, "drive_blocked: %lld slots, %lld hand-backs\n", (long long)launched, (long long)handbacks);
+    if (dbg)
+      fprintf(stderr, "drive_blocked: %lld slots, %lld hand-backs\n", (long long)sc.launched(), (long long)sc.handbacks());
+  }
+  static SlotView view(const State& st) {
+    SlotView v;
+    v.status = st.status;
+    v.ckpt_pending = st.ckpt_pending;
+    v.iter = st.iter;
+    v.slots = st.slots;
+    return v;
   }
   int64_t handback_count = 0;
   int fast_group = std::max(1, (int)knob("MIDAGMA_EXP_FAST_GROUP", 4));
-  int64_t fast_batch = 64;
+  int64_t fast_batch = BlockedScheduler::kMaxBatch;
 
   // Small d: the whole inner loop in one persistent workgroup, kSmallBatch slots per launch
   // (one host sync per launch).  n_slots < 0: until terminal.
   static constexpr int64_t kSmallBatch = 4096;
   void drive_small(int64_t n_slots) {
-    const int64_t max_iter = hp.max_iter, checkpoint = std::max<int64_t>(hp.checkpoint, 1);
-    const int64_t cap = max_iter + max_iter / checkpoint + 512;
-    int64_t launched = 0;
-    for (;;) {
-      const int64_t B = std::min<int64_t>(kSmallBatch, (n_slots < 0 ? cap : n_slots) - launched);
-      if (B <= 0) {
-        if (n_slots < 0) throw std::runtime_error("minimize: slot budget exceeded (controller stuck)");
-        break;
-      }
+    const int64_t cap = slot_cap(hp.max_iter, hp.checkpoint);
+    for (int64_t launched = 0;;) {
+      const int64_t B = small_next_batch(n_slots, launched, cap, kSmallBatch);
+      if (B <= 0) break;
       launch_small_minimize(d_params, d_state, W.p, m.p, v.p, covs.p, has_inc ? minc.p : nullptr,
                             has_exc ? mexc.p : nullptr, bc_table.p, d_ckpt, ckpt_cap, scarry.p, sprev.p, d, B,
                             stream);
@@ -836,12 +843,12 @@ struct midagma_solver {
       return;
     }
     ensure_graphs();
-    const int64_t cap = max_iter + max_iter / std::max<int64_t>(checkpoint, 1) + 512;
+    const int64_t cap = slot_cap(max_iter, checkpoint);
     int64_t launched = 0, known_iter = 0;
     int cur = 0, pending = -1;
     bool stop = false;
     while (!stop) {
-      int64_t B = std::min<int64_t>(64, std::max<int64_t>(2, max_iter - known_iter + 2));
+      const int64_t B = graph_next_batch(max_iter, known_iter);
       for (int64_t b = 0; b < B; ++b) HIP_TRY(hipGraphLaunch(g_full, stream));
       launched += B;
       snapshot(cur);

@@ -64,3 +64,33 @@ def test_gpus_n_relaunches_as_torchrun_child(bench, monkeypatch):
     assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
     assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+
+
+def test_oracle_check_child_matches_in_process_oracle(bench):
+    """The value check's child process runs the same oracle steps as an in-process LinearOracle
+    (bit for bit at one BLAS thread), and check_l2 flags a W one part in 1e8 off."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    from midagma_amd.simulate import make_dataset
+    from oracle.dagma_oracle import LinearOracle
+    X, _, _ = make_dataset(30, 300, seed=4)
+    o = LinearOracle("l2")
+    o.prepare(X, 0.03, 10 ** 9)
+    with threadpool_limits(limits=1):
+        W, tr = o.minimize(np.zeros((30, 30)), 1.0, 50, 1.0, 3e-4, tol=-1.0)
+    c = bench.check_l2(W, o.cov, 50, "test", threads=1)
+    assert c["ok"] and c["max_dW"] == 0.0 and c["steps"] == 50
+    bad = W.copy()
+    bad[1, 2] += 1e-8
+    assert not bench.check_l2(bad, o.cov, 50, "test", threads=1)["ok"]
+
+
+def test_comm_summary_keys(bench):
+    """The N > 1 line's all-reduce breakdown (allreduce / compute split, bandwidths, the process
+    group's backend, world size and NCCL_ALGO)."""
+    c = bench.comm_summary(0.1, 0.08, 7.4, 8 * 1000 * 1000, 8, "nccl")
+    for k in ("allreduce_ms", "allreduce_ms_min_rank", "compute_ms", "allreduce_frac", "bytes", "algbw_GBps",
+              "busbw_GBps", "backend", "world_size", "NCCL_ALGO", "timing"):
+        assert k in c, k
+    assert abs(c["compute_ms"] - 7.3) < 1e-12 and c["world_size"] == 8
+    assert abs(c["algbw_GBps"] - 80.0) < 1e-9 and abs(c["busbw_GBps"] - 140.0) < 1e-9

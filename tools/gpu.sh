@@ -9,6 +9,8 @@
 #                         -> gpurun_out/exp_tests.log
 #   smoke                 __graft_entry__.smoke()
 #   bench [BENCH ARGS]    python bench.py -> gpurun_out/bench.json (+ .err)
+#   rehearse2             bench.py --gpus 2 with both ranks on cuda:0 over gloo (the N > 1 path end to end on
+#                         a one-GPU box; not a scaling number) -> gpurun_out/rehearse2.json
 #   prof LEG              rocprofv3 --kernel-trace --stats of one bench leg -> gpurun_out/prof_LEG/
 #                         LEG: data | cov | large | small | logistic | mlp (one bench leg each)
 #   pmc LEG               FETCH_SIZE and WRITE_SIZE passes (each its own run) of one leg,
@@ -22,10 +24,10 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 
 leg_args() {
-  local skip="--no-cpu --no-fit --no-cov --no-large --no-mlp --no-logistic --no-small"
+  local skip="--no-cpu --no-check --no-fit --no-cov --no-large --no-mlp --no-logistic --no-small"
   case "$1" in
     data)     echo "--steps 5 --warmup 1 ${skip}" ;;
-    cov)      echo "--workload cov --cov-steps 2000 --no-cpu --no-fit --no-large" ;;
+    cov)      echo "--workload cov --cov-steps 2000 --no-cpu --no-check --no-fit --no-large" ;;
     large)    echo "--no-data ${skip/--no-large/} --large-steps 200" ;;
     mlp)      echo "--no-data ${skip/--no-mlp/}" ;;
     logistic) echo "--no-data ${skip/--no-logistic/}" ;;
@@ -61,6 +63,11 @@ run_task() {
     bench)
       timeout -k 10 1100 python bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err; local rc=$?
       echo "bench rc=$rc"; cat gpurun_out/bench.json; grep -v amdgpu.ids gpurun_out/bench.err | tail -8; return $rc ;;
+    rehearse2)
+      MIDAGMA_BENCH_SAME_DEVICE=1 MIDAGMA_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 \
+        --steps 10 --warmup 2 "$@" > gpurun_out/rehearse2.json 2> gpurun_out/rehearse2.err; local rc=$?
+      echo "rehearse2 rc=$rc"; cat gpurun_out/rehearse2.json; grep -v amdgpu.ids gpurun_out/rehearse2.err | tail -8
+      return $rc ;;
     prof)
       local leg=$1 a
       a="$R/bench.py $(leg_args "$leg")" || return 2
