@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 5
+#define MIDAGMA_ABI_VERSION 6
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -225,6 +225,25 @@ int midagma_logdet_h_dev(const double* A, int64_t d, int64_t lda, double s, doub
 int64_t midagma_logdet_h_parts(int64_t d);
 int midagma_logdet_h_dev_part(const double* A, int64_t d, int64_t lda, double s, double* h_dev, double* Mt_dev,
                               int64_t ldm, void* stream, int64_t part);
+/* ABI 6: the h log-det of consecutive DagmaNonlinear.minimize steps (nonlinear.py:206-217, 85-86)
+ * with a warm start.  A handle holds the warm-start ring of one minimize call's A = sum fc1^2
+ * (d <= 256; larger d always runs the Gauss-Jordan chain).  A fast step (exact = 0) inverts
+ * (sI - A)^T by the product-form series from the last two steps' inverses and keeps the last
+ * exact h when that inverse converged and is entrywise >= 0 (then sI - A is a nonsingular
+ * M-matrix and h >= 0: the reference's h < 0 exit cannot fire); otherwise it runs the
+ * Gauss-Jordan chain on the device and takes its h.  An exact step (exact = 1: the steps whose
+ * objective the caller reads) always runs the chain.  Both write (sI - A)^-T to Mt and feed the
+ * ring.  midagma_ldfast_reset starts a call (the first step then runs the chain).  Parts as
+ * midagma_logdet_h_dev_part: issued in order on one stream; one step at a time per handle. */
+typedef struct midagma_ldfast midagma_ldfast;
+int midagma_ldfast_create(midagma_ldfast** out, int64_t d);
+void midagma_ldfast_destroy(midagma_ldfast* h);
+int midagma_ldfast_reset(midagma_ldfast* h);
+int64_t midagma_ldfast_parts(const midagma_ldfast* h, int exact);
+int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t lda, double s, double* h_dev, double* Mt_dev,
+                           int64_t ldm, void* stream, int exact, int64_t part);
+/* gate-open (Gauss-Jordan) steps and fast steps since the last reset (diagnostics; syncs) */
+int midagma_ldfast_stats(midagma_ldfast* h, int64_t* steps, int64_t* exact_steps);
 int midagma_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
                           double lambda1, double half_d, double inv_n, double* obj, void* stream);
 int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,

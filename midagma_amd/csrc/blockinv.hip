@@ -24,6 +24,7 @@
 //         (first slot of a minimize call, rho > 0.25, no convergence): the fast kernels
 //         then set ST_NEED_GJ and the host re-runs the slot on the slow path.
 #include <cstdlib>
+#include <type_traits>
 
 #include "binv_tile.h"
 #include "launch.h"
@@ -382,6 +383,43 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
                        bw.Q[(p - 1) & 1], bw.Y[p & 1], bw.Q[p & 1], bw.P, part + (p - 1) * PART_STRIDE,
                        part + p * PART_STRIDE, done, p, st, ext ? la[p - 1] : none);
   }
+}
+
+// One B2 x B2 block's product-form series with explicit buffers (the DagmaMLP log-det's fast
+// path, mlp.hip): the same kernels and arithmetic as an outer block of the fast blocked inverse.
+template <class F>
+static void with_series_l(int B2, F&& f) {
+  if (B2 == 256)
+    f(std::integral_constant<int, 16>{});
+  else if (B2 == 128)
+    f(std::integral_constant<int, 8>{});
+  else
+    throw std::invalid_argument("launch_series: B2 must be 128 or 256");
+}
+
+void launch_series_pass(int B2, const SeriesWork& w, State* st, int p, hipStream_t stream) {
+  if (p < 1 || p > NM_PASSES) throw std::invalid_argument("launch_series_pass: pass out of range");
+  const NmLA none{};
+  with_series_l(B2, [&](auto Lc) {
+    constexpr int L = decltype(Lc)::value;
+    const int nwg = (B2 / 16) * (B2 / 16);
+    hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, w.Y[(p - 1) & 1], w.Q[(p - 1) & 1],
+                       w.Y[p & 1], w.Q[p & 1], w.P, w.part + (p - 1) * PART_STRIDE, w.part + p * PART_STRIDE, w.done,
+                       p, st, none);
+  });
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_series(const double* S, int64_t lds, int B2, const SeriesWork& w, State* st, int passes,
+                   hipStream_t stream) {
+  with_series_l(B2, [&](auto Lc) {
+    constexpr int L = decltype(Lc)::value;
+    const int nwg = (B2 / 16) * (B2 / 16);
+    hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, S, lds, w.Pe, w.Po, w.Y[0], w.Q[0],
+                       w.part, w.done, st);
+  });
+  HIP_TRY(hipGetLastError());
+  for (int p = 1; p <= passes; ++p) launch_series_pass(B2, w, st, p, stream);
 }
 
 // Experiment knob MIDAGMA_EXP_RESID_LA=1: the look-ahead residual (read at each enqueue, i.e.

@@ -95,6 +95,25 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes = NM_PASSES_RUN, const GemmSpec* fuse = nullptr);
 
+// One B2 x B2 block (B2 = 128 or 256) by the product-form series from the warm start in the
+// ring Pe / Po (the slot parity and the extrapolation rule of the blocked inverse: st->slots,
+// st->warm_run): nm_resid + `passes` pass launches.  On convergence the inverse is in P and
+// *done holds the converging pass; otherwise *done stays 0 or st->status becomes ST_NEED_GJ
+// (also at once when st->ckpt_pending).  part: (NM_PASSES + 1) x PART_STRIDE doubles.
+struct SeriesWork {
+  const double* Pe;
+  const double* Po;
+  double* Y[2];
+  double* Q[2];
+  double* P;
+  double* part;
+  int* done;
+};
+void launch_series(const double* S, int64_t lds, int B2, const SeriesWork& w, State* st, int passes,
+                   hipStream_t stream);
+// pass p (1 .. NM_PASSES) of that series alone
+void launch_series_pass(int B2, const SeriesWork& w, State* st, int p, hipStream_t stream);
+
 // --- dfinv.hip --------------------------------------------------------------
 // The fast slot's blocked inverse as one dataflow launch (tile tasks, host-planned order).
 constexpr int DF_MAX_K2 = 8;  // outer blocks of 256
@@ -216,6 +235,18 @@ void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA,
 // Mt (d x d, ldm; nullable) from the D x D log-det workspace Ws and h = -sum(piv[0:d]) + dls
 void launch_logdet_post(const double* piv, int64_t d, double dls, double* h, const double* Ws, int64_t D, double* Mt,
                         int64_t ldm, hipStream_t stream);
+// The h log-det's warm-started fast path (mlp.hip, DagmaNonlinear.minimize): the step's start
+// (ring parity, Gauss-Jordan gate reset; with build, (sI - A)^T into the B x B S), the series
+// result's certificate (Mt from P, gate opened when P did not converge or has an entry < 0 or
+// non-finite) and the step's end (h and Mt from the Gauss-Jordan chain when it ran, else h =
+// *hlast; the inverse into the ring; the ring state advanced).
+void launch_ldfast_begin(const double* A, int64_t lda, int64_t d, double s, double* S, int B, State* st, State* gjst,
+                         bool build, hipStream_t stream);
+void launch_ldfast_certify(const double* P, int B, int64_t d, double* Mt, int64_t ldm, const State* st,
+                           const int* done, State* gjst, hipStream_t stream);
+void launch_ldfast_post(const double* piv, int64_t d, double dls, double* h, const double* Wgj, int64_t Dgj, double* Mt,
+                        int64_t ldm, const double* P, int B, double* ring0, double* ring1, State* st,
+                        const State* gjst, double* hlast, bool exact, hipStream_t stream);
 // obj = mu (half_d log(inv_n ssq) + lambda1 sum(l1part)) + h and its backward
 void launch_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
                           double lambda1, double half_d, double inv_n, double* out, hipStream_t stream);

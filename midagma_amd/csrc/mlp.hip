@@ -323,3 +323,135 @@ void launch_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, do
 }
 
 }  // namespace midagma
+
+// ---- the h log-det's warm-started fast path (DagmaNonlinear.minimize, BASELINE config 5) -------
+// Between two Adam steps fc1 moves by ~lr, so (sI - A)^-T of the last two steps is a warm start
+// for this one: the product-form series of the blocked inverse (launch_series, blockinv.hip) on
+// the B x B identity-padded (sI - A)^T replaces the 32-block Gauss-Jordan's prologue and block
+// steps.  The log-det itself is needed only where the caller reads it (the checkpoint steps,
+// nonlinear.py:214-217 via the objective) and for the h < 0 exit (nonlinear.py:206-208): an
+// entrywise nonnegative inverse of the Z-matrix sI - A (A = sum fc1^2 >= 0) proves it a nonsingular
+// M-matrix, where h = sum_k tr((A/s)^k)/k >= 0 and the exit cannot fire, so such a step keeps the
+// last exactly computed h.  Every other step -- no convergence, a negative or non-finite entry,
+// no warm start yet (the first step of a call) -- runs the Gauss-Jordan chain, gated on the
+// device, and takes its pivots' h, as do the caller's exact (checkpoint) steps.
+namespace midagma {
+namespace {
+
+// (sI - A)^T into the B x B S (identity padding); one workgroup also opens the step: the
+// step index (the warm-start ring's parity) and the Gauss-Jordan gate reset to "skip".
+__global__ __launch_bounds__(NTHREADS) void ldfast_begin_kernel(const double* __restrict__ A, int64_t lda, int64_t d,
+                                                                double s, double* __restrict__ S, int B,
+                                                                State* __restrict__ st, State* __restrict__ gjst,
+                                                                int build) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->slots += 1;
+    gjst->status = ST_DONE;
+  }
+  if (!build) return;
+  const int64_t e = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  if (e >= (int64_t)B * B) return;
+  const int64_t r = e / B, c = e % B;  // S[r][c] = (sI - A)^T[r][c] = s delta - A[c][r]
+  double v;
+  if (r < d && c < d)
+    v = (r == c ? s : 0.0) - A[c * lda + r];
+  else
+    v = (r == c) ? 1.0 : 0.0;
+  S[e] = v;
+}
+
+// The series' inverse P (B x B, converged: *done != 0) is (sI - A)^-T: Mt (d x d) from it, and
+// the Gauss-Jordan gate opened (gjst->status = ST_RUNNING) when it did not converge or is not
+// entrywise >= 0 and finite on the d x d block.
+__global__ __launch_bounds__(NTHREADS) void ldfast_certify_kernel(const double* __restrict__ P, int B, int64_t d,
+                                                                  double* __restrict__ Mt, int64_t ldm,
+                                                                  const State* __restrict__ st,
+                                                                  const int* __restrict__ done,
+                                                                  State* __restrict__ gjst) {
+  const int64_t e = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  int bad = 0;
+  if (e < d * d) {
+    const int64_t i = e / d, j = e % d;
+    const double v = P[i * B + j];
+    Mt[i * ldm + j] = v;
+    bad = !(v >= 0.0) || !isfinite(v);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (st->status != ST_RUNNING || *done == 0)) bad = 1;
+  if (__syncthreads_or(bad) && threadIdx.x == 0)
+    __hip_atomic_store(&gjst->status, (int32_t)ST_RUNNING, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The step's end: if the Gauss-Jordan chain ran (exact step, or the gate opened), h from its
+// pivots (logdet_post's sum, bit for bit) and Mt from its workspace, else h = the last exact h;
+// the step's inverse into the warm-start ring (slot parity of st->slots); one workgroup then
+// advances the ring's state for the next step.
+__global__ __launch_bounds__(NTHREADS) void ldfast_post_kernel(const double* __restrict__ piv, int64_t d, double dls,
+                                                               double* __restrict__ h, const double* __restrict__ Wgj,
+                                                               int64_t Dgj, double* __restrict__ Mt, int64_t ldm,
+                                                               const double* __restrict__ P, int B,
+                                                               double* __restrict__ ring0, double* __restrict__ ring1,
+                                                               State* __restrict__ st, const State* __restrict__ gjst,
+                                                               double* __restrict__ hlast, int exact) {
+  const bool ran = exact || gjst->status == ST_RUNNING;
+  const int64_t slot = st->slots;
+  double* dst = (slot & 1) ? ring1 : ring0;
+  const int64_t e = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  if (e < (int64_t)B * B) {  // the ring (B = 0: no fast path, no ring)
+    const int64_t i = e / B, j = e % B;
+    dst[e] = ran ? ((i < Dgj && j < Dgj) ? Wgj[i * Dgj + j] : (i == j ? 1.0 : 0.0)) : P[e];
+  }
+  if (ran && e < d * d) {
+    const int64_t i = e / d, j = e % d;
+    Mt[i * ldm + j] = Wgj[i * Dgj + j];
+  }
+  if (blockIdx.x != 0) return;
+  __shared__ double red[NTHREADS];
+  double acc = 0.0;
+  if (ran)
+    for (int64_t k = threadIdx.x; k < d; k += NTHREADS) acc += piv[k];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s2 = NTHREADS / 2; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double hv = ran ? -red[0] + dls : hlast[0];
+    h[0] = hv;
+    if (ran) hlast[0] = hv;
+    st->warm_run = st->warm_run < 2 ? st->warm_run + 1 : 2;
+    st->ckpt_pending = 0;
+    st->status = ST_RUNNING;
+    st->iter += 1;                // diagnostics (midagma_ldfast_stats): steps,
+    if (ran) st->halvings += 1;   // and those that ran the Gauss-Jordan chain
+  }
+}
+
+}  // namespace
+
+void launch_ldfast_begin(const double* A, int64_t lda, int64_t d, double s, double* S, int B, State* st, State* gjst,
+                         bool build, hipStream_t stream) {
+  const unsigned blocks = build ? (unsigned)(((int64_t)B * B + NTHREADS - 1) / NTHREADS) : 1u;
+  hipLaunchKernelGGL(ldfast_begin_kernel, dim3(blocks), dim3(NTHREADS), 0, stream, A, lda, d, s, S, B, st, gjst,
+                     build ? 1 : 0);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_ldfast_certify(const double* P, int B, int64_t d, double* Mt, int64_t ldm, const State* st,
+                           const int* done, State* gjst, hipStream_t stream) {
+  const int64_t blocks = std::max<int64_t>(1, (d * d + NTHREADS - 1) / NTHREADS);
+  hipLaunchKernelGGL(ldfast_certify_kernel, dim3((unsigned)blocks), dim3(NTHREADS), 0, stream, P, B, d, Mt, ldm, st,
+                     done, gjst);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_ldfast_post(const double* piv, int64_t d, double dls, double* h, const double* Wgj, int64_t Dgj, double* Mt,
+                        int64_t ldm, const double* P, int B, double* ring0, double* ring1, State* st,
+                        const State* gjst, double* hlast, bool exact, hipStream_t stream) {
+  const unsigned blocks = (unsigned)((std::max<int64_t>((int64_t)B * B, d * d) + NTHREADS - 1) / NTHREADS);
+  hipLaunchKernelGGL(ldfast_post_kernel, dim3(blocks), dim3(NTHREADS), 0, stream, piv, d, dls, h, Wgj, Dgj, Mt, ldm,
+                     P, B, ring0, ring1, st, gjst, hlast, exact ? 1 : 0);
+  HIP_TRY(hipGetLastError());
+}
+
+}  // namespace midagma

@@ -1593,6 +1593,152 @@ extern "C" int midagma_logdet_h_dev(const double* A, int64_t d, int64_t lda, dou
 
 extern "C" int64_t midagma_logdet_h_parts(int64_t d) { return d < 1 ? 0 : (d + 31) / 32 + 2; }
 
+// ---- the h log-det's warm-started fast path (ABI 6; mlp.hip) -------------------------------------
+struct midagma_ldfast {
+  int device = 0;
+  int64_t d = 0, Dgj = 0;  // Gauss-Jordan workspace: 32-padded, as midagma_logdet_h_dev
+  int B = 0;               // series block: 128 or 256 (0: d > 256, every step exact)
+  DevBuf S, ring0, ring1, Y0, Y1, Q0, Q1, P, part, done, hlast;
+  DevBuf A, Pgj, Rgj, Cgj, piv;
+  State* st = nullptr;    // the ring's state (slots: step index; warm_run; status of the series)
+  State* gjst = nullptr;  // the Gauss-Jordan gate of a fast step (ST_RUNNING: run the chain)
+  std::string err;
+  ~midagma_ldfast() {
+    for (DevBuf* b : {&S, &ring0, &ring1, &Y0, &Y1, &Q0, &Q1, &P, &part, &done, &hlast, &A, &Pgj, &Rgj, &Cgj, &piv})
+      b->release();
+    if (st) (void)hipFree(st);
+    if (gjst) (void)hipFree(gjst);
+  }
+  GJWork gjw() const { return GJWork{Pgj.p, Rgj.p, Cgj.p, piv.p}; }
+  SeriesWork sw() const {
+    return SeriesWork{ring0.p, ring1.p, {Y0.p, Y1.p}, {Q0.p, Q1.p}, P.p, part.p, reinterpret_cast<int*>(done.p)};
+  }
+};
+
+extern "C" int midagma_ldfast_create(midagma_ldfast** out, int64_t d) {
+  if (!out || d < 1) return fail(nullptr, MIDAGMA_E_ARG, "ldfast_create: bad arguments");
+  auto* h = new midagma_ldfast();
+  int rc = guarded(nullptr, [&] {
+    setup_attributes_once();
+    HIP_TRY(hipGetDevice(&h->device));
+    h->d = d;
+    h->Dgj = (d + 31) / 32 * 32;
+    h->B = d <= 128 ? 128 : (d <= 256 ? 256 : 0);
+    const size_t DD = (size_t)h->Dgj * h->Dgj;
+    h->A.alloc(DD);
+    h->Pgj.alloc(64 * 64);
+    h->Rgj.alloc((size_t)64 * h->Dgj);
+    h->Cgj.alloc((size_t)h->Dgj * 64);
+    h->piv.alloc(h->Dgj);
+    h->hlast.alloc(1);
+    if (h->B) {
+      const size_t BB = (size_t)h->B * h->B;
+      for (DevBuf* b : {&h->S, &h->ring0, &h->ring1, &h->Y0, &h->Y1, &h->Q0, &h->Q1, &h->P}) b->alloc(BB);
+      h->part.alloc((size_t)(NM_PASSES + 1) * PART_STRIDE);
+      h->done.alloc(1);
+    }
+    HIP_TRY(hipMalloc(&h->st, sizeof(State)));
+    HIP_TRY(hipMalloc(&h->gjst, sizeof(State)));
+    return midagma_ldfast_reset(h);
+  });
+  if (rc != MIDAGMA_OK) {
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return MIDAGMA_OK;
+}
+
+extern "C" void midagma_ldfast_destroy(midagma_ldfast* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  delete h;
+}
+
+extern "C" int midagma_ldfast_reset(midagma_ldfast* h) {
+  if (!h) return fail(nullptr, MIDAGMA_E_ARG, "ldfast_reset: null handle");
+  return guarded(nullptr, [&] {
+    HIP_TRY(hipSetDevice(h->device));
+    State st{};
+    st.status = ST_RUNNING;
+    st.slots = -1;        // ldfast_begin opens step 0
+    st.ckpt_pending = 1;  // no warm start: the first step runs the Gauss-Jordan chain
+    State gj{};
+    gj.status = ST_DONE;
+    HIP_TRY(hipMemcpy(h->st, &st, sizeof(State), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->gjst, &gj, sizeof(State), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(h->hlast.p, 0, sizeof(double)));
+    if (h->done.p) HIP_TRY(hipMemset(h->done.p, 0, sizeof(double)));
+    return MIDAGMA_OK;
+  });
+}
+
+// fast: 0 begin + series residual, 1 .. 3 the passes, 4 certificate + the gated chain, 5 end;
+// exact: 0 begin + build + prologue, 1 .. Dgj/32 the block steps, last the end
+static constexpr int kLdfastPasses = 3;
+extern "C" int64_t midagma_ldfast_parts(const midagma_ldfast* h, int exact) {
+  if (!h) return 0;
+  return (exact || !h->B) ? h->Dgj / 32 + 2 : kLdfastPasses + 3;
+}
+
+extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t lda, double s, double* h_dev,
+                                      double* Mt_dev, int64_t ldm, void* stream, int exact, int64_t part) {
+  if (!h || !A || !h_dev || !Mt_dev || lda < h->d || ldm < h->d || !(s > 0.0) || part >= midagma_ldfast_parts(h, exact))
+    return fail(nullptr, MIDAGMA_E_ARG, "ldfast_enqueue: bad arguments");
+  return guarded(nullptr, [&] {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t d = h->d, D = h->Dgj;
+    const int K = (int)(D / 32);
+    const double dls = (double)d * std::log(s);
+    const bool ex = exact || !h->B;
+    auto want = [&](int64_t p) { return part < 0 || part == p; };
+    if (ex) {  // the Gauss-Jordan chain, ungated
+      if (want(0)) {
+        launch_ldfast_begin(A, lda, d, s, h->S.p, h->B, h->st, h->gjst, false, st);
+        launch_build_at(A, lda, false, h->A.p, D, d, s, nullptr, nullptr, st);
+        launch_gj_prologue(h->A.p, D, D, h->gjw(), nullptr, st);
+      }
+      for (int k = 0; k < K; ++k)
+        if (want(k + 1)) launch_gj_step(h->A.p, D, D, h->gjw(), nullptr, k, st);
+      if (want(K + 1))
+        launch_ldfast_post(h->piv.p, d, dls, h_dev, h->A.p, D, Mt_dev, ldm, h->P.p, h->B, h->ring0.p, h->ring1.p,
+                           h->st, h->gjst, h->hlast.p, true, st);
+      return MIDAGMA_OK;
+    }
+    const SeriesWork w = h->sw();
+    if (want(0)) {
+      launch_ldfast_begin(A, lda, d, s, h->S.p, h->B, h->st, h->gjst, true, st);
+      launch_series(h->S.p, h->B, h->B, w, h->st, 0, st);  // the residual launch only
+    }
+    // the passes one by one (each its own part: the caller interleaves them)
+    for (int p = 1; p <= kLdfastPasses; ++p)
+      if (want(p)) launch_series_pass(h->B, w, h->st, p, st);
+    if (want(kLdfastPasses + 1)) {
+      launch_ldfast_certify(h->P.p, h->B, d, Mt_dev, ldm, h->st, reinterpret_cast<const int*>(h->done.p), h->gjst, st);
+      launch_build_at(A, lda, false, h->A.p, D, d, s, nullptr, h->gjst, st);  // gated: opened by the certificate
+      launch_gj_inverse(h->A.p, D, D, h->gjw(), h->gjst, st);
+    }
+    if (want(kLdfastPasses + 2))
+      launch_ldfast_post(h->piv.p, d, dls, h_dev, h->A.p, D, Mt_dev, ldm, h->P.p, h->B, h->ring0.p, h->ring1.p, h->st,
+                         h->gjst, h->hlast.p, false, st);
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_ldfast_stats(midagma_ldfast* h, int64_t* steps, int64_t* exact_steps) {
+  if (!h) return fail(nullptr, MIDAGMA_E_ARG, "ldfast_stats: null handle");
+  return guarded(nullptr, [&] {
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
+    State st{};
+    HIP_TRY(hipMemcpy(&st, h->st, sizeof(State), hipMemcpyDeviceToHost));
+    if (steps) *steps = st.iter;
+    if (exact_steps) *exact_steps = st.halvings;
+    return MIDAGMA_OK;
+  });
+}
+
 extern "C" int midagma_logdet_h_dev_part(const double* A, int64_t d, int64_t lda, double s, double* h_dev,
                                          double* Mt_dev, int64_t ldm, void* stream, int64_t part) {
   if (!A || !h_dev || d < 1 || lda < d || !(s > 0.0) || (Mt_dev && ldm < d) || part < 0 ||

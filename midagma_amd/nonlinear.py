@@ -116,7 +116,7 @@ class _MLPObjective(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, X, W1, b1, w2, b2, d: int, m1: int, s: float, mu: float, lambda1: float,
-                overlap: bool = False):
+                overlap: bool = False, ld=None, exact: bool = True):
         L = _lib.lib()
         dev = X.device
         X, W1, b1, w2, b2 = X.contiguous(), W1.contiguous(), b1.contiguous(), w2.contiguous(), b2.contiguous()
@@ -151,7 +151,7 @@ class _MLPObjective(torch.autograd.Function):
                 ev_fc1 = torch.cuda.Event()
                 ev_fc1.record(main)
                 side.wait_event(ev_fc1)
-                chain = _SideLogdet(L, side, A, d, float(s), h, Mt)
+                chain = _SideLogdet(L, side, A, d, float(s), h, Mt, ld=ld, exact=exact)
                 chain.enqueue(1)
                 _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
                                                   _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
@@ -162,8 +162,11 @@ class _MLPObjective(torch.autograd.Function):
                 ctx.chain = chain
                 ctx.keep = (A, l1part)  # read on the side stream: alive until the join
             else:
-                _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None,
-                           "logdet_h_dev")
+                if ld is not None:
+                    ld.enqueue(A, d, float(s), h, Mt, stream, exact, -1)
+                else:
+                    _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None,
+                               "logdet_h_dev")
                 _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
                                                   _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
                 _lib.check(L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(h), float(mu),
@@ -212,28 +215,33 @@ class _MLPObjective(torch.autograd.Function):
                 ctx.chain = None
             _lib.check(L.midagma_fc1_terms_bwd(_vp(W1), d, m1, _vp(Mt), _vp(gh), _vp(gl1), _vp(lin), nlin,
                                                _vp(dW1), st), None, "fc1_terms_bwd")
-        return None, dW1, db1, dw2, db2, None, None, None, None, None, None
+        return None, dW1, db1, dw2, db2, None, None, None, None, None, None, None, None
 
 
 _SIDE: dict = {}
 
 
 class _SideLogdet:
-    """The h log-det (midagma_logdet_h_dev_part) enqueued part by part on a side stream, then the
-    scalar objective once the tail's ssq is ready (objective = (event, ssq, l1part, mu, lambda1,
-    half_d, inv_n, out))."""
+    """The h log-det (midagma_logdet_h_dev_part, or a warm-started LdFast step) enqueued part by
+    part on a side stream, then the scalar objective once the tail's ssq is ready (objective =
+    (event, ssq, l1part, mu, lambda1, half_d, inv_n, out))."""
 
-    def __init__(self, L, side, A, d, s, h, Mt):
+    def __init__(self, L, side, A, d, s, h, Mt, ld=None, exact=True):
         self.L, self.side, self.A, self.d, self.s, self.h, self.Mt = L, side, A, d, s, h, Mt
-        self.parts = int(L.midagma_logdet_h_parts(d))
+        self.ld, self.exact = ld, exact
+        self.parts = ld.parts(exact) if ld is not None else int(L.midagma_logdet_h_parts(d))
         self.next = 0
         self.objective = None
 
     def enqueue(self, k):
         ss = C.c_void_p(self.side.cuda_stream)
         while k > 0 and self.next < self.parts:
-            _lib.check(self.L.midagma_logdet_h_dev_part(_vp(self.A), self.d, self.d, self.s, _vp(self.h), _vp(self.Mt),
-                                                        self.d, ss, self.next), None, "logdet_h_dev_part")
+            if self.ld is not None:
+                self.ld.enqueue(self.A, self.d, self.s, self.h, self.Mt, self.side.cuda_stream, self.exact, self.next)
+            else:
+                _lib.check(self.L.midagma_logdet_h_dev_part(_vp(self.A), self.d, self.d, self.s, _vp(self.h),
+                                                            _vp(self.Mt), self.d, ss, self.next), None,
+                           "logdet_h_dev_part")
             self.next += 1
             k -= 1
 
@@ -247,6 +255,53 @@ class _SideLogdet:
         ev = torch.cuda.Event()
         ev.record(self.side)
         return ev
+
+
+class LdFast:
+    """The h log-det of consecutive minimize steps with a warm start (midagma_ldfast_*, ABI 6): a
+    fast step inverts sI - A by the product-form series from the last two steps' inverses and
+    keeps the last exact h when that inverse is entrywise >= 0 (sI - A is then a nonsingular
+    M-matrix and h >= 0, so the reference's h < 0 exit, nonlinear.py:206-208, cannot fire), else
+    it runs the Gauss-Jordan chain on the device; an exact step always runs the chain (the steps
+    whose objective the loop reads, nonlinear.py:214-217).  One per (model size, device)."""
+
+    def __init__(self, d: int, device: int):
+        self.L = _lib.lib()
+        self.d, self.device = int(d), int(device)
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.midagma_ldfast_create(C.byref(h), self.d), None, "ldfast_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.midagma_ldfast_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.midagma_ldfast_reset(self.h), None, "ldfast_reset")
+
+    def parts(self, exact: bool) -> int:
+        return int(self.L.midagma_ldfast_parts(self.h, 1 if exact else 0))
+
+    def enqueue(self, A, d, s, h, Mt, stream, exact: bool, part: int):
+        _lib.check(self.L.midagma_ldfast_enqueue(self.h, _vp(A), d, float(s), _vp(h), _vp(Mt), d,
+                                                 C.c_void_p(stream) if stream else None, 1 if exact else 0, part),
+                   None, "ldfast_enqueue")
+
+    def stats(self):
+        """(steps, steps that ran the Gauss-Jordan chain) since the last reset."""
+        a, b = C.c_int64(), C.c_int64()
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.midagma_ldfast_stats(self.h, C.byref(a), C.byref(b)), None, "ldfast_stats")
+        return int(a.value), int(b.value)
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -385,7 +440,8 @@ class DagmaNonlinear:
         n, d = target.shape
         return 0.5 * d * torch.log(1 / n * torch.sum((output - target) ** 2))
 
-    def _h_and_objective(self, mu: float, lambda1: float, s: float, overlap: bool = False):
+    def _h_and_objective(self, mu: float, lambda1: float, s: float, overlap: bool = False, ld=None,
+                         exact: bool = True):
         """(h, mu * (score + lambda1 * |fc1|_1) + h) (nonlinear.py:198-204): for a [d, m1, 1] MLP
         on the GPU through the fused kernels (fc1 terms, log-det, tail, scalar objective),
         otherwise the reference's expressions."""
@@ -395,7 +451,7 @@ class DagmaNonlinear:
             m1 = m.dims[1]
             fc = m.fc2[0]
             return _MLPObjective.apply(self.X, m.fc1.weight, m.fc1.bias, fc.weight, fc.bias, d, m1, s, mu, lambda1,
-                                       overlap)
+                                       overlap, ld, exact)
         h_val = m.h_func(s)
         return h_val, mu * (self._score() + lambda1 * m.fc1_l1_reg()) + h_val
 
@@ -487,11 +543,12 @@ class DagmaNonlinear:
         L = _lib.lib()
 
         seed = torch.ones((), dtype=torch.float64, device=dev)  # d obj / d obj: no fill node per step
+        ld = self._ldfast(dev)
 
-        def body(gate):
+        def body(gate, exact=True):
             for p in params:
                 p.grad = None
-            h_val, obj = self._h_and_objective(mu, lambda1, s, overlap=self.overlap)
+            h_val, obj = self._h_and_objective(mu, lambda1, s, overlap=self.overlap, ld=ld, exact=exact)
             obj.backward(seed)
             stream = torch.cuda.current_stream(dev).cuda_stream
             st = C.c_void_p(stream) if stream else None
@@ -521,13 +578,21 @@ class DagmaNonlinear:
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
-                for _ in range(2):
-                    body(no_step)
+                for exact in (True, False) if ld is not None else (True,):
+                    body(no_step, exact)
             torch.cuda.current_stream(dev).wait_stream(side)
             counter.zero_()
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 h_static, obj_static = body(None)
+            # the steps whose objective the loop does not read: the log-det's warm-started fast path
+            graph_fast = None
+            if ld is not None:
+                graph_fast = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph_fast):
+                    body(None, False)
+                torch.cuda.synchronize(dev)
+                ld.reset()
         except Exception as e:  # noqa: BLE001
             for p in params:
                 p.grad = None
@@ -535,8 +600,9 @@ class DagmaNonlinear:
         obj_prev = 1e16
         try:
             for i in range(max_iter):
-                graph.replay()
-                if i % self.checkpoint == 0 or i == max_iter - 1:
+                ck = i % self.checkpoint == 0 or i == max_iter - 1
+                (graph if ck or graph_fast is None else graph_fast).replay()
+                if ck:
                     h_host = h_static.item()
                     if h_host < 0:
                         self.vprint(f"Found h negative {h_host} at or before iter {i}")
@@ -555,7 +621,22 @@ class DagmaNonlinear:
             torch.cuda.current_stream(dev).synchronize()
             for p in params:
                 p.grad = None
-            del graph
+            del graph, graph_fast
+
+    def _ldfast(self, dev: torch.device):
+        """The warm-started log-det handle of this model's [d, m1, 1] objective (None: the fused
+        objective does not apply, d > 256, or MIDAGMA_NO_LDFAST=1 keeps every step exact)."""
+        m = self.model
+        if os.environ.get("MIDAGMA_NO_LDFAST") or not getattr(m, "fused_tail", lambda: False)():
+            return None
+        d = self.X.shape[1]
+        if d > 256:
+            return None
+        key = (d, dev.index)
+        if getattr(self, "_ld", None) is None or self._ld_key != key:
+            self._ld = LdFast(d, dev.index)
+            self._ld_key = key
+        return self._ld
 
     def fit(self, X, lambda1: float = .02, lambda2: float = .005, T: int = 4, mu_init: float = .1,
             mu_factor: float = .1, s: float = 1.0, warm_iter: int = 5e4, max_iter: int = 8e4, lr: float = .0002,

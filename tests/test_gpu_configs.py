@@ -143,3 +143,48 @@ def test_config5_logdet_side_stream_bit_identical(graph, monkeypatch):
         out[overlap] = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
     for k in out[True]:
         assert np.array_equal(out[True][k], out[False][k]), k
+
+
+def test_config5_ldfast_path_matches_oracle(parity):
+    """The h log-det's warm-started fast path (midagma_ldfast, nonlinear.LdFast): between the
+    checkpoint steps (every 100 here; each runs the Gauss-Jordan chain) the product-form series
+    from the last two steps' inverses, certified entrywise >= 0.  300 steps at dims [200, 10, 1]:
+    the fast path carries almost every step, and every parameter stays within 1e-9 of the
+    oracle's (torch CPU, slogdet) run; against the all-exact run (MIDAGMA_NO_LDFAST) to 1e-12."""
+    import os
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    from oracle.mlp_oracle import OracleMLP, load_params, nonlinear_minimize
+    d, n, K = 200, 1000, 300
+    X, _, _ = make_dataset(d, n, seed=2)
+    gen = torch.Generator().manual_seed(9)
+    ref = OracleMLP([d, 10, 1])
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(torch.randn(p.shape, generator=gen, dtype=torch.float64) * 0.05)
+        ref.fc1.weight.mul_(0.3 / np.sqrt(10 * d) / 0.05)
+    p0 = {k: v.detach().numpy().copy() for k, v in ref.state_dict().items() if k in KEYS}
+    out = {}
+    for exact_only in (False, True):
+        if exact_only:
+            os.environ["MIDAGMA_NO_LDFAST"] = "1"
+        try:
+            model = DagmaMLP(dims=[d, 10, 1], bias=True).to("cuda:0")
+            load_params(model, p0)
+            dn = DagmaNonlinear(model, device=0)
+            dn.X = torch.from_numpy(X).to("cuda:0")
+            dn.checkpoint = 100
+            assert dn.minimize(K, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
+            if not exact_only:
+                steps, exact = dn._ld.stats()
+                assert steps == K and exact <= 10, (steps, exact)   # 3 checkpoints + the last step
+            out[exact_only] = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items() if k in KEYS}
+        finally:
+            os.environ.pop("MIDAGMA_NO_LDFAST", None)
+    ok, it = nonlinear_minimize(ref, torch.from_numpy(X), K, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1, checkpoint=100)
+    assert ok and it == K
+    rd = ref.state_dict()
+    dev = max(np.abs(out[False][k] - rd[k].numpy()).max() / max(1.0, np.abs(rd[k].numpy()).max()) for k in KEYS)
+    parity("config5", dev, 1e-9, f"max|dparam|/max(1,|p|) K={K} (fast log-det path)")
+    assert dev <= 1e-9
+    for k in KEYS:
+        assert np.abs(out[False][k] - out[True][k]).max() <= 1e-12 * max(1.0, np.abs(out[True][k]).max()), k
