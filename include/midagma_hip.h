@@ -244,6 +244,22 @@ int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t lda, doub
                            int64_t ldm, void* stream, int exact, int64_t part);
 /* gate-open (Gauss-Jordan) steps and fast steps since the last reset (diagnostics; syncs) */
 int midagma_ldfast_stats(midagma_ldfast* h, int64_t* steps, int64_t* exact_steps);
+/* ABI 6: the [d, m1, 1] objective with the scalar objective's backward folded into its consumers
+ * (no mlp_sum / mlp_objective_bwd launches; bit-identical to the ABI-5 sequence): the tail forward
+ * leaves its n row partials (part), the objective sums them and, with a counter, advances the
+ * Adam table's step (counter += 1, nullable), the tail backward and the fc1 terms' backward take
+ * gobj = d loss / d obj and derive d obj / d ssq, d h = gobj, d l1part = (gobj mu) lambda1. */
+int midagma_mlp_tail_fwd_part(const double* Z, const double* b1, const double* w2, const double* b2, const double* X,
+                              int64_t n, int64_t d, int64_t m1, double* R, double* part, void* stream);
+int midagma_mlp_objective_part(const double* part, int64_t npart, const double* l1part, int64_t np, const double* h,
+                               double mu, double lambda1, double half_d, double inv_n, double* obj, int64_t* counter,
+                               void* stream);
+int midagma_mlp_tail_bwd_obj(const double* Z, const double* b1, const double* w2, const double* R, const double* part,
+                             const double* gobj, double mu, double half_d, double inv_n, int64_t n, int64_t d,
+                             int64_t m1, double* dZ, double* dw2, double* db2, double* db1, double* scratch,
+                             void* stream);
+int midagma_fc1_terms_bwd_obj(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gobj, double mu,
+                              double lambda1, const double* lin, int64_t nlin, double* dW1, void* stream);
 int midagma_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
                           double lambda1, double half_d, double inv_n, double* obj, void* stream);
 int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,

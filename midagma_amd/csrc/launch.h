@@ -221,17 +221,23 @@ void launch_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, co
                          int64_t n, int64_t d, int m1, double* R, double* scratch, double* ssq, hipStream_t stream);
 // g (device scalar) = d loss / d ssq -> dZ (n x d*m1), dw2 (d x m1), db2 (d)
 // (db1 nullable: also the column sums of dZ, the fc1 bias gradient)
+// (part nullable: then g = d loss / d ssq; else gobj = d loss / d obj and the backward takes ssq from
+// the forward's row partials part[n] and d obj / d ssq itself, mlp_objective_bwd's arithmetic)
 void launch_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R, const double* g,
                          int64_t n, int64_t d, int m1, double* dZ, double* dw2, double* db2, double* db1,
-                         double* scratch, hipStream_t stream);
+                         double* scratch, hipStream_t stream, const double* part = nullptr,
+                         const double* gobj = nullptr, double mu = 0.0, double half_d = 0.0, double inv_n = 0.0);
 
 // fc1 terms of the [d, m1, 1] DagmaMLP: A[i, j] = sum_m W1[j m1 + m, i]^2, |W1| partial sums
 // (fc1_terms_parts(d) of them); backward dW1 = 2 W1 gA^T + gl1part sign(W1)
 int64_t fc1_terms_parts(int64_t d);
 void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1part, hipStream_t stream);
 // (lin, nlin: nlin split-K chunks of another dW1 contribution to add; nullable / 0)
+// (gobj nullable: d obj; then gscale = gobj and gl1part = (gobj mu) lambda1 everywhere, the
+// objective's backward folded in)
 void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gscale,
-                          const double* gl1part, const double* lin, int nlin, double* dW1, hipStream_t stream);
+                          const double* gl1part, const double* lin, int nlin, double* dW1, hipStream_t stream,
+                          const double* gobj = nullptr, double mu = 0.0, double lambda1 = 0.0);
 // Mt (d x d, ldm; nullable) from the D x D log-det workspace Ws and h = -sum(piv[0:d]) + dls
 void launch_logdet_post(const double* piv, int64_t d, double dls, double* h, const double* Ws, int64_t D, double* Mt,
                         int64_t ldm, hipStream_t stream);
@@ -248,8 +254,10 @@ void launch_ldfast_post(const double* piv, int64_t d, double dls, double* h, con
                         int64_t ldm, const double* P, int B, double* ring0, double* ring1, State* st,
                         const State* gjst, double* hlast, bool exact, hipStream_t stream);
 // obj = mu (half_d log(inv_n ssq) + lambda1 sum(l1part)) + h and its backward
+// (part nullable: ssq from the tail's npart row partials instead; counter nullable: += 1)
 void launch_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
-                          double lambda1, double half_d, double inv_n, double* out, hipStream_t stream);
+                          double lambda1, double half_d, double inv_n, double* out, hipStream_t stream,
+                          const double* part = nullptr, int64_t npart = 0, int64_t* counter = nullptr);
 void launch_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,
                               double inv_n, double* gssq, double* gl1part, double* gh, hipStream_t stream);
 

@@ -68,6 +68,27 @@ __global__ __launch_bounds__(NTHREADS) void mlp_sum_kernel(const double* __restr
 
 // grid (column tiles of 256, row chunks of TAIL_ROWS): thread per column c = j m1 + m over
 // the chunk's rows: dZ, and the chunk's partials of dw2 (pw[chunk][c]) and db2 (pb[chunk][j])
+// The objective's backward for d obj = gobj (mlp_objective_bwd's arithmetic): d obj / d ssq, with
+// ssq the fixed-order sum of the forward's row partials (mlp_sum's order), computed by the
+// consumer itself instead of a launch of its own.
+struct ObjGrad {
+  const double* part;  // the forward's row partials (null: g already is d obj / d ssq)
+  int64_t np;
+  const double* gobj;
+  double mu, half_d, inv_n;
+};
+
+__device__ __forceinline__ double ssq_from_parts(const double* __restrict__ part, int64_t np, double* red) {
+  double a = 0.0;
+  for (int64_t i = threadIdx.x; i < np; i += NTHREADS) a += part[i];
+  return block_sum256(a, red);
+}
+
+__device__ __forceinline__ double gssq_of(double gv, double ssq, const ObjGrad& o) {
+  const double inner = gv * o.mu;
+  return ((inner * o.half_d) / (o.inv_n * ssq)) * o.inv_n;
+}
+
 __global__ __launch_bounds__(NTHREADS) void mlp_tail_bwd_kernel(const double* __restrict__ Z,
                                                                 const double* __restrict__ b1,
                                                                 const double* __restrict__ w2,
@@ -75,13 +96,20 @@ __global__ __launch_bounds__(NTHREADS) void mlp_tail_bwd_kernel(const double* __
                                                                 const double* __restrict__ g, int64_t n, int64_t d,
                                                                 int m1, double* __restrict__ dZ,
                                                                 double* __restrict__ pw, double* __restrict__ pb,
-                                                                double* __restrict__ pz) {
+                                                                double* __restrict__ pz, ObjGrad og) {
   const int64_t dm = d * m1;
+  double gs;
+  if (og.part) {  // every workgroup reduces the partials (before any thread leaves)
+    __shared__ double red[NTHREADS];
+    gs = gssq_of(og.gobj[0], ssq_from_parts(og.part, og.np, red), og);
+  } else {
+    gs = g[0];
+  }
   const int64_t c = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   if (c >= dm) return;
   const int64_t j = c / m1;
   const int m = (int)(c % m1);
-  const double w = w2[c], g2 = 2.0 * g[0], bias = b1 ? b1[c] : 0.0;
+  const double w = w2[c], g2 = 2.0 * gs, bias = b1 ? b1[c] : 0.0;
   const int64_t r0 = (int64_t)blockIdx.y * TAIL_ROWS, r1 = r0 + TAIL_ROWS < n ? r0 + TAIL_ROWS : n;
   double aw = 0.0, ab = 0.0, az = 0.0;
   for (int64_t row = r0; row < r1; ++row) {
@@ -144,19 +172,21 @@ void launch_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, co
   const size_t lds = (size_t)(d * m1 + NTHREADS) * sizeof(double);
   hipLaunchKernelGGL(mlp_tail_fwd_kernel, dim3((unsigned)n), dim3(NTHREADS), lds, stream, Z, b1, w2, b2, X, d, m1, R,
                      part);
-  hipLaunchKernelGGL(mlp_sum_kernel, dim3(1), dim3(NTHREADS), 0, stream, part, n, ssq);
+  if (ssq) hipLaunchKernelGGL(mlp_sum_kernel, dim3(1), dim3(NTHREADS), 0, stream, part, n, ssq);
   HIP_TRY(hipGetLastError());
 }
 
 void launch_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R, const double* g,
                          int64_t n, int64_t d, int m1, double* dZ, double* dw2, double* db2, double* db1,
-                         double* scratch, hipStream_t stream) {
+                         double* scratch, hipStream_t stream, const double* part, const double* gobj, double mu,
+                         double half_d, double inv_n) {
   const int64_t dm = d * m1, chunks = (n + TAIL_ROWS - 1) / TAIL_ROWS;
   double* pw = scratch;
   double* pb = scratch + chunks * dm;
   double* pz = db1 ? pb + chunks * d : nullptr;
   hipLaunchKernelGGL(mlp_tail_bwd_kernel, dim3((unsigned)((dm + NTHREADS - 1) / NTHREADS), (unsigned)chunks),
-                     dim3(NTHREADS), 0, stream, Z, b1, w2, R, g, n, d, m1, dZ, pw, pb, pz);
+                     dim3(NTHREADS), 0, stream, Z, b1, w2, R, g, n, d, m1, dZ, pw, pb, pz,
+                     ObjGrad{part, n, gobj, mu, half_d, inv_n});
   const int64_t cols = dm + d + (db1 ? dm : 0);
   hipLaunchKernelGGL(mlp_tail_dw_kernel, dim3((unsigned)((cols + NTHREADS - 1) / NTHREADS)), dim3(NTHREADS), 0,
                      stream, pw, pb, pz, chunks, d, m1, dw2, db2, db1);
@@ -202,11 +232,14 @@ __global__ __launch_bounds__(NTHREADS) void fc1_terms_bwd_kernel(const double* _
                                                                  const double* __restrict__ gscale,
                                                                  const double* __restrict__ gl1,
                                                                  const double* __restrict__ lin, int nlin,
-                                                                 double* __restrict__ dW1) {
+                                                                 double* __restrict__ dW1, const double* gobj,
+                                                                 double mu, double lambda1) {
   const int64_t t = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
   if (t >= d * d) return;
   const int64_t j = t / d, i = t % d, dd = d * m1 * d;
-  const double ga = gscale ? gscale[0] * gA[i * d + j] : gA[i * d + j], gl = gl1[blockIdx.x];
+  // gobj (nullable): d obj = gobj, so d h = gobj and d l1part = (gobj mu) lambda1 (mlp_objective_bwd)
+  const double ga = gobj ? gobj[0] * gA[i * d + j] : (gscale ? gscale[0] * gA[i * d + j] : gA[i * d + j]);
+  const double gl = gobj ? (gobj[0] * mu) * lambda1 : gl1[blockIdx.x];
   for (int m = 0; m < m1; ++m) {
     const int64_t e = (j * m1 + m) * d + i;
     const double w = W1[e];
@@ -251,8 +284,13 @@ __global__ __launch_bounds__(NTHREADS) void mlp_objective_kernel(const double* _
                                                                  const double* __restrict__ l1part, int64_t np,
                                                                  const double* __restrict__ h, double mu,
                                                                  double lambda1, double half_d, double inv_n,
-                                                                 double* __restrict__ out) {
+                                                                 double* __restrict__ out,
+                                                                 const double* __restrict__ part, int64_t npart,
+                                                                 int64_t* __restrict__ counter) {
   __shared__ double red[NTHREADS];
+  // part (nullable): ssq as the fixed-order sum of the tail's row partials (mlp_sum's order)
+  const double ssq_v = part ? ssq_from_parts(part, npart, red) : ssq[0];
+  if (counter && threadIdx.x == 0) *counter += 1;  // the Adam step table's index (one per step)
   double a = 0.0;
   for (int64_t k = threadIdx.x; k < np; k += NTHREADS) a += l1part[k];
   red[threadIdx.x] = a;
@@ -262,7 +300,7 @@ __global__ __launch_bounds__(NTHREADS) void mlp_objective_kernel(const double* _
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double score = half_d * log(inv_n * ssq[0]);
+    const double score = half_d * log(inv_n * ssq_v);
     out[0] = mu * (score + lambda1 * red[0]) + h[0];
   }
 }
@@ -294,9 +332,10 @@ void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1
 }
 
 void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gscale,
-                          const double* gl1part, const double* lin, int nlin, double* dW1, hipStream_t stream) {
+                          const double* gl1part, const double* lin, int nlin, double* dW1, hipStream_t stream,
+                          const double* gobj, double mu, double lambda1) {
   hipLaunchKernelGGL(fc1_terms_bwd_kernel, dim3((unsigned)fc1_terms_parts(d)), dim3(NTHREADS), 0, stream, W1, d, m1,
-                     gA, gscale, gl1part, lin, nlin, dW1);
+                     gA, gscale, gl1part, lin, nlin, dW1, gobj, mu, lambda1);
   HIP_TRY(hipGetLastError());
 }
 
@@ -309,9 +348,10 @@ void launch_logdet_post(const double* piv, int64_t d, double dls, double* h, con
 }
 
 void launch_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
-                          double lambda1, double half_d, double inv_n, double* out, hipStream_t stream) {
+                          double lambda1, double half_d, double inv_n, double* out, hipStream_t stream,
+                          const double* part, int64_t npart, int64_t* counter) {
   hipLaunchKernelGGL(mlp_objective_kernel, dim3(1), dim3(NTHREADS), 0, stream, ssq, l1part, np, h, mu, lambda1, half_d,
-                     inv_n, out);
+                     inv_n, out, part, npart, counter);
   HIP_TRY(hipGetLastError());
 }
 

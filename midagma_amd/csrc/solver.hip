@@ -1917,6 +1917,60 @@ extern "C" int midagma_mlp_objective_bwd(const double* g, const double* ssq, int
   });
 }
 
+// ABI 6: the [d, m1, 1] objective's step with the scalar objective's backward folded into its
+// consumers (no mlp_sum / mlp_objective_bwd launches): the tail forward leaves its n row partials,
+// the objective sums them (and advances the Adam table counter), the tail backward and the fc1
+// terms' backward derive d obj / d ssq, d h and d l1 from gobj themselves.  Bit-identical to the
+// ABI-5 sequence (the same sums in the same order, the same scalar arithmetic).
+extern "C" int midagma_mlp_tail_fwd_part(const double* Z, const double* b1, const double* w2, const double* b2,
+                                         const double* X, int64_t n, int64_t d, int64_t m1, double* R, double* part,
+                                         void* stream) {
+  if (!Z || !w2 || !b2 || !X || !R || !part || n < 1 || d < 1 || m1 < 1 || d * m1 > MLP_TAIL_MAX_DM)
+    return fail(nullptr, MIDAGMA_E_ARG, "mlp_tail_fwd_part: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_mlp_tail_fwd(Z, b1, w2, b2, X, n, d, (int)m1, R, part, nullptr, reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_mlp_tail_bwd_obj(const double* Z, const double* b1, const double* w2, const double* R,
+                                        const double* part, const double* gobj, double mu, double half_d,
+                                        double inv_n, int64_t n, int64_t d, int64_t m1, double* dZ, double* dw2,
+                                        double* db2, double* db1, double* scratch, void* stream) {
+  if (!Z || !w2 || !R || !part || !gobj || !dZ || !dw2 || !db2 || !scratch || n < 1 || d < 1 || m1 < 1 ||
+      d * m1 > MLP_TAIL_MAX_DM)
+    return fail(nullptr, MIDAGMA_E_ARG, "mlp_tail_bwd_obj: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_mlp_tail_bwd(Z, b1, w2, R, nullptr, n, d, (int)m1, dZ, dw2, db2, db1, scratch,
+                        reinterpret_cast<hipStream_t>(stream), part, gobj, mu, half_d, inv_n);
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_fc1_terms_bwd_obj(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gobj,
+                                         double mu, double lambda1, const double* lin, int64_t nlin, double* dW1,
+                                         void* stream) {
+  if (!W1 || !gA || !gobj || !dW1 || d < 1 || m1 < 1 || nlin < 0 || (nlin > 0 && !lin))
+    return fail(nullptr, MIDAGMA_E_ARG, "fc1_terms_bwd_obj: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_fc1_terms_bwd(W1, d, (int)m1, gA, nullptr, nullptr, lin, (int)nlin, dW1,
+                         reinterpret_cast<hipStream_t>(stream), gobj, mu, lambda1);
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_mlp_objective_part(const double* part, int64_t npart, const double* l1part, int64_t np,
+                                          const double* h, double mu, double lambda1, double half_d, double inv_n,
+                                          double* obj, int64_t* counter, void* stream) {
+  if (!part || npart < 1 || !l1part || !h || !obj || np < 1)
+    return fail(nullptr, MIDAGMA_E_ARG, "mlp_objective_part: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_mlp_objective(nullptr, l1part, np, h, mu, lambda1, half_d, inv_n, obj,
+                         reinterpret_cast<hipStream_t>(stream), part, npart, counter);
+    return MIDAGMA_OK;
+  });
+}
+
 extern "C" int midagma_adam_step(double* p, const double* g, double* m, double* v, int64_t n, double step_size,
                                  double w1, double beta2, double c2, double bc2_sqrt, double eps, double wd,
                                  const double* gate, void* stream) {

@@ -116,7 +116,7 @@ class _MLPObjective(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, X, W1, b1, w2, b2, d: int, m1: int, s: float, mu: float, lambda1: float,
-                overlap: bool = False, ld=None, exact: bool = True):
+                overlap: bool = False, ld=None, exact: bool = True, counter=None):
         L = _lib.lib()
         dev = X.device
         X, W1, b1, w2, b2 = X.contiguous(), W1.contiguous(), b1.contiguous(), w2.contiguous(), b2.contiguous()
@@ -130,22 +130,23 @@ class _MLPObjective(torch.autograd.Function):
         Mt = torch.empty((d, d), **f64)
         h = torch.empty((), **f64)
         R = torch.empty_like(X)
+        part = torch.empty(n, **f64)  # the tail's row partials of the squared residual sum
         scratch = torch.empty(int(L.midagma_mlp_tail_scratch(n, d, m1)), **f64)
-        ssq = torch.empty((), **f64)
         obj = torch.empty((), **f64)
+        ctr = _vp(counter) if counter is not None else None
         ctx.chain = None
         with torch.cuda.device(dev):
             _lib.check(L.midagma_fc1_terms(_vp(W1), d, m1, _vp(A), _vp(l1part), st), None, "fc1_terms")
             if overlap:
-                # The log-det chain (Gauss-Jordan block steps: latency-bound, ~40% of a config-5
-                # step) depends on fc1 only: it runs on a side stream beside the tail forward and
-                # the backward up to the weight gradient, which never read h or the objective's
-                # value; the side stream also forms the objective once the tail's ssq is ready,
-                # and backward joins before the fc1 terms' backward needs (sI - A)^-T.  Only for
-                # callers that run backward right away (DagmaNonlinear.minimize): the join is there.
-                # Its parts are enqueued between the main stream's launches (a replayed graph
-                # submits nodes in capture order, ~4 us each: a branch captured whole ahead of the
-                # other holds the other back by its whole submission time).
+                # The log-det chain (latency-bound) depends on fc1 only: it runs on a side stream
+                # beside the tail forward and the backward up to the weight gradient, which never
+                # read h or the objective's value; the side stream also forms the objective once the
+                # tail's partials are ready, and backward joins before the fc1 terms' backward needs
+                # (sI - A)^-T.  Only for callers that run backward right away
+                # (DagmaNonlinear.minimize): the join is there.  Its parts are enqueued between the
+                # main stream's launches (a replayed graph submits nodes in capture order, ~4 us
+                # each: a branch captured whole ahead of the other holds the other back by its
+                # whole submission time).
                 main = torch.cuda.current_stream(dev)
                 side = _side_stream(dev)
                 ev_fc1 = torch.cuda.Event()
@@ -153,12 +154,12 @@ class _MLPObjective(torch.autograd.Function):
                 side.wait_event(ev_fc1)
                 chain = _SideLogdet(L, side, A, d, float(s), h, Mt, ld=ld, exact=exact)
                 chain.enqueue(1)
-                _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
-                                                  _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
+                _lib.check(L.midagma_mlp_tail_fwd_part(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
+                                                       _vp(part), st), None, "mlp_tail_fwd_part")
                 ev_tail = torch.cuda.Event()
                 ev_tail.record(main)
                 chain.enqueue(2)
-                chain.objective = (ev_tail, ssq, l1part, float(mu), float(lambda1), 0.5 * d, 1 / n, obj)
+                chain.objective = (ev_tail, part, l1part, float(mu), float(lambda1), 0.5 * d, 1 / n, obj, ctr)
                 ctx.chain = chain
                 ctx.keep = (A, l1part)  # read on the side stream: alive until the join
             else:
@@ -167,19 +168,19 @@ class _MLPObjective(torch.autograd.Function):
                 else:
                     _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None,
                                "logdet_h_dev")
-                _lib.check(L.midagma_mlp_tail_fwd(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
-                                                  _vp(scratch), _vp(ssq), st), None, "mlp_tail_fwd")
-                _lib.check(L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(h), float(mu),
-                                                   float(lambda1), 0.5 * d, 1 / n, _vp(obj), st), None,
-                           "mlp_objective")
-        ctx.save_for_backward(X, W1, b1, w2, Z, R, Mt, ssq, scratch)
+                _lib.check(L.midagma_mlp_tail_fwd_part(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
+                                                       _vp(part), st), None, "mlp_tail_fwd_part")
+                _lib.check(L.midagma_mlp_objective_part(_vp(part), n, _vp(l1part), l1part.numel(), _vp(h),
+                                                        float(mu), float(lambda1), 0.5 * d, 1 / n, _vp(obj), ctr, st),
+                           None, "mlp_objective_part")
+        ctx.save_for_backward(X, W1, b1, w2, Z, R, Mt, part, scratch)
         ctx.consts = (n, d, m1, float(mu), float(lambda1), l1part.numel())
         ctx.set_materialize_grads(False)  # h's own gradient stays None (no zero fill and add)
         return h, obj
 
     @staticmethod
     def backward(ctx, gh_out, g):
-        X, W1, b1, w2, Z, R, Mt, ssq, scratch = ctx.saved_tensors
+        X, W1, b1, w2, Z, R, Mt, part, scratch = ctx.saved_tensors
         n, d, m1, mu, lambda1, np_ = ctx.consts
         L = _lib.lib()
         dev = X.device
@@ -187,20 +188,18 @@ class _MLPObjective(torch.autograd.Function):
         st = C.c_void_p(stream) if stream else None
         f64 = dict(dtype=torch.float64, device=dev)
         g = torch.zeros((), **f64) if g is None else g.contiguous()
-        gssq, gl1, gh = torch.empty((), **f64), torch.empty(np_, **f64), torch.empty((), **f64)
         dZ = torch.empty_like(Z)
         dw2, db2, db1 = torch.empty_like(w2), torch.empty((d, 1), **f64), torch.empty(d * m1, **f64)
         dW1 = torch.empty_like(W1)
         chain = ctx.chain
         with torch.cuda.device(dev):
-            _lib.check(L.midagma_mlp_objective_bwd(_vp(g), _vp(ssq), np_, mu, lambda1, 0.5 * d, 1 / n, _vp(gssq),
-                                                   _vp(gl1), _vp(gh), st), None, "mlp_objective_bwd")
             if chain is not None:
                 chain.enqueue(2)
-            if gh_out is not None:  # h is also an output (the Adam gate): its own gradient adds in
-                gh = gh + gh_out
-            _lib.check(L.midagma_mlp_tail_bwd(_vp(Z), _vp(b1), _vp(w2), _vp(R), _vp(gssq), n, d, m1, _vp(dZ),
-                                              _vp(dw2), _vp(db2), _vp(db1), _vp(scratch), st), None, "mlp_tail_bwd")
+            # the objective's backward (d ssq, d h, d l1) is derived from g inside the tail's and the
+            # fc1 terms' backward (midagma_*_obj): no launch of its own
+            _lib.check(L.midagma_mlp_tail_bwd_obj(_vp(Z), _vp(b1), _vp(w2), _vp(R), _vp(part), _vp(g), mu, 0.5 * d,
+                                                  1 / n, n, d, m1, _vp(dZ), _vp(dw2), _vp(db2), _vp(db1),
+                                                  _vp(scratch), st), None, "mlp_tail_bwd_obj")
             if chain is not None:
                 chain.enqueue(2)
             if n % 4 == 0 and n >= 64:
@@ -213,9 +212,17 @@ class _MLPObjective(torch.autograd.Function):
             if chain is not None:  # the rest of the chain and the objective, then join
                 torch.cuda.current_stream(dev).wait_event(chain.finish())
                 ctx.chain = None
-            _lib.check(L.midagma_fc1_terms_bwd(_vp(W1), d, m1, _vp(Mt), _vp(gh), _vp(gl1), _vp(lin), nlin,
-                                               _vp(dW1), st), None, "fc1_terms_bwd")
-        return None, dW1, db1, dw2, db2, None, None, None, None, None, None, None, None
+            if gh_out is None:
+                _lib.check(L.midagma_fc1_terms_bwd_obj(_vp(W1), d, m1, _vp(Mt), _vp(g), mu, lambda1, _vp(lin), nlin,
+                                                       _vp(dW1), st), None, "fc1_terms_bwd_obj")
+            else:  # h is also an output whose gradient adds in (not the minimize loop's case)
+                gl1, gh, gdummy = torch.empty(np_, **f64), torch.empty((), **f64), torch.empty((), **f64)
+                _lib.check(L.midagma_mlp_objective_bwd(_vp(g), _vp(part), np_, mu, lambda1, 0.5 * d, 1 / n,
+                                                       _vp(gdummy), _vp(gl1), _vp(gh), st), None, "mlp_objective_bwd")
+                gh = gh + gh_out
+                _lib.check(L.midagma_fc1_terms_bwd(_vp(W1), d, m1, _vp(Mt), _vp(gh), _vp(gl1), _vp(lin), nlin,
+                                                   _vp(dW1), st), None, "fc1_terms_bwd")
+        return None, dW1, db1, dw2, db2, None, None, None, None, None, None, None, None, None
 
 
 _SIDE: dict = {}
@@ -223,8 +230,8 @@ _SIDE: dict = {}
 
 class _SideLogdet:
     """The h log-det (midagma_logdet_h_dev_part, or a warm-started LdFast step) enqueued part by
-    part on a side stream, then the scalar objective once the tail's ssq is ready (objective =
-    (event, ssq, l1part, mu, lambda1, half_d, inv_n, out))."""
+    part on a side stream, then the scalar objective once the tail's row partials are ready (objective
+    = (event, part, l1part, mu, lambda1, half_d, inv_n, out, counter or None))."""
 
     def __init__(self, L, side, A, d, s, h, Mt, ld=None, exact=True):
         self.L, self.side, self.A, self.d, self.s, self.h, self.Mt = L, side, A, d, s, h, Mt
@@ -247,11 +254,11 @@ class _SideLogdet:
 
     def finish(self) -> torch.cuda.Event:
         self.enqueue(self.parts)
-        ev_tail, ssq, l1part, mu, lambda1, half_d, inv_n, out = self.objective
+        ev_tail, part, l1part, mu, lambda1, half_d, inv_n, out, ctr = self.objective
         self.side.wait_event(ev_tail)
-        _lib.check(self.L.midagma_mlp_objective(_vp(ssq), _vp(l1part), l1part.numel(), _vp(self.h), mu, lambda1,
-                                                half_d, inv_n, _vp(out), C.c_void_p(self.side.cuda_stream)), None,
-                   "mlp_objective")
+        _lib.check(self.L.midagma_mlp_objective_part(_vp(part), part.numel(), _vp(l1part), l1part.numel(),
+                                                     _vp(self.h), mu, lambda1, half_d, inv_n, _vp(out), ctr,
+                                                     C.c_void_p(self.side.cuda_stream)), None, "mlp_objective_part")
         ev = torch.cuda.Event()
         ev.record(self.side)
         return ev
@@ -441,7 +448,7 @@ class DagmaNonlinear:
         return 0.5 * d * torch.log(1 / n * torch.sum((output - target) ** 2))
 
     def _h_and_objective(self, mu: float, lambda1: float, s: float, overlap: bool = False, ld=None,
-                         exact: bool = True):
+                         exact: bool = True, counter=None):
         """(h, mu * (score + lambda1 * |fc1|_1) + h) (nonlinear.py:198-204): for a [d, m1, 1] MLP
         on the GPU through the fused kernels (fc1 terms, log-det, tail, scalar objective),
         otherwise the reference's expressions."""
@@ -451,7 +458,7 @@ class DagmaNonlinear:
             m1 = m.dims[1]
             fc = m.fc2[0]
             return _MLPObjective.apply(self.X, m.fc1.weight, m.fc1.bias, fc.weight, fc.bias, d, m1, s, mu, lambda1,
-                                       overlap, ld, exact)
+                                       overlap, ld, exact, counter)
         h_val = m.h_func(s)
         return h_val, mu * (self._score() + lambda1 * m.fc1_l1_reg()) + h_val
 
@@ -537,6 +544,11 @@ class DagmaNonlinear:
             if lr_decay and (i + 1) % 1000 == 0:
                 lr_cur = lr_cur * 0.8
         dev = params[0].device
+        # the fused objective advances the step counter itself (before the step's Adam launch),
+        # so its Adam launches read the table one entry later: a leading pad entry
+        fused = getattr(self.model, "fused_tail", lambda: False)()
+        if fused:
+            table = np.concatenate([np.zeros(2), table])
         table_d = torch.from_numpy(table).to(dev)
         counter = torch.zeros(1, dtype=torch.int64, device=dev)
         no_step = torch.full((), -1.0, dtype=torch.float64, device=dev)
@@ -548,7 +560,8 @@ class DagmaNonlinear:
         def body(gate, exact=True):
             for p in params:
                 p.grad = None
-            h_val, obj = self._h_and_objective(mu, lambda1, s, overlap=self.overlap, ld=ld, exact=exact)
+            h_val, obj = self._h_and_objective(mu, lambda1, s, overlap=self.overlap, ld=ld, exact=exact,
+                                               counter=counter if fused else None)
             obj.backward(seed)
             stream = torch.cuda.current_stream(dev).cuda_stream
             st = C.c_void_p(stream) if stream else None
@@ -569,7 +582,8 @@ class DagmaNonlinear:
                                                          p.numel(), C.c_void_p(table_d.data_ptr()),
                                                          C.c_void_p(counter.data_ptr()), 1 - beta1, beta2,
                                                          1 - beta2, eps, wd, g_ptr, st), None, "adam_step_table")
-            _lib.check(L.midagma_counter_advance(C.c_void_p(counter.data_ptr()), st), None, "counter_advance")
+            if not fused:
+                _lib.check(L.midagma_counter_advance(C.c_void_p(counter.data_ptr()), st), None, "counter_advance")
             return h_val, obj
 
         try:

@@ -1,0 +1,50 @@
+"""Config 5 step-time variants (development tool): DagmaNonlinear.minimize at dims [200, 10, 1],
+n = 1000, with the log-det on a side stream or not (MIDAGMA_NO_OVERLAP) and with the warm-started
+fast log-det or every step exact (MIDAGMA_NO_LDFAST); prints steps/s and the fast path's share.
+
+    python tools/probe_mlp.py [K]
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear  # noqa: E402
+from midagma_amd.simulate import make_dataset  # noqa: E402
+
+
+def run(K, overlap, fast):
+    for k in ("MIDAGMA_NO_OVERLAP", "MIDAGMA_NO_LDFAST"):
+        os.environ.pop(k, None)
+    if not overlap:
+        os.environ["MIDAGMA_NO_OVERLAP"] = "1"
+    if not fast:
+        os.environ["MIDAGMA_NO_LDFAST"] = "1"
+    d, n = 200, 1000
+    X, _, _ = make_dataset(d, n, seed=0)
+    torch.manual_seed(0)
+    model = DagmaMLP(dims=[d, 10, 1]).to("cuda:0")
+    with torch.no_grad():
+        model.fc1.weight.normal_(0, 0.3 / np.sqrt(10 * d))
+    dn = DagmaNonlinear(model, device=0)
+    dn.X = torch.from_numpy(X).to("cuda:0")
+    dn.checkpoint = 10 ** 9
+    dn.minimize(20, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dn.minimize(K, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = dn._ld.stats() if fast and getattr(dn, "_ld", None) is not None else None
+    print(f"overlap={int(overlap)} ldfast={int(fast)}: {K / dt:.0f} steps/s ({dt / K * 1e6:.1f} us/step)"
+          f"{'' if st is None else f'  steps {st[0]}, Gauss-Jordan {st[1]}'}", flush=True)
+
+
+if __name__ == "__main__":
+    K = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+    for overlap in (True, False):
+        for fast in (True, False):
+            run(K, overlap, fast)
