@@ -432,12 +432,69 @@ static bool resid_lookahead() {
   return knob("MIDAGMA_EXP_RESID_LA", 0) == 1;
 }
 
+// Fast slot at large D with the look-ahead: each outer step's trailing update in two launches,
+// the tiles in block g + 1's row and column bands (its series and panel read only those) and the
+// rest; the chain series(g+1) -> panel(g+1) -> band tiles(g+1) runs on the high-priority side
+// stream while rest(g) runs on `stream`, so the serial series / panel phases hide behind the
+// long trailing launches (classic LU look-ahead).  Dependencies: rest(g) after panel(g) and
+// rest(g-1); band tiles(g) after panel(g) and rest(g-1) (which wrote its inputs, and whose
+// inputs it overwrites); the last step's whole trailing update (with the fused score GEMM and the
+// domain check) after rest(K2-2).  Every tile is computed by the same body as launch_trail128.
+static bool blocked_inverse_lookahead(double* Mt, int64_t D, int B2, const BInvWork& bw, State* st,
+                                      hipStream_t stream, int passes, const GemmSpec* fuse,
+                                      const TrailLookAhead& la) {
+  const int K2 = (int)(D / B2), gb = B2 / NB, mb = (int)(D / NB) - gb;
+  double* bufs[2] = {binv_build_target(Mt, D, bw), nullptr};
+  bufs[1] = bufs[0] == Mt ? bw.Aalt : Mt;
+  hipEvent_t* ev = la.ev;  // [0] fork, [1 + 2g] panel(g), [2 + 2g] rest(g), [2 K2 + 1] join
+  hipStream_t side = la.side;
+  bool fused = false;
+  HIP_TRY(hipEventRecord(ev[0], stream));
+  HIP_TRY(hipStreamWaitEvent(side, ev[0], 0));
+  for (int g = 0; g < K2; ++g) {
+    double* Ain = bufs[g & 1];
+    double* Aout = bufs[(g + 1) & 1];
+    const int64_t G0 = (int64_t)g * B2;
+    double* Pe = bw.Pst + (int64_t)g * B2 * B2;
+    double* Po = bw.Pst1 + (int64_t)g * B2 * B2;
+    if (B2 == 256)
+      launch_neumann<16>(Ain, D, G0, bw, g, st, passes, true, nullptr, side);
+    else
+      launch_neumann<8>(Ain, D, G0, bw, g, st, passes, true, nullptr, side);
+    const int check = g == K2 - 1;
+    hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, side, Ain, Aout, D, B2, g,
+                       bw.P, (int64_t)B2, Pe, Po, bw.done + g, check, st, t32_pf(), nullptr, nullptr);
+    if (g < K2 - 1) {
+      HIP_TRY(hipEventRecord(ev[1 + 2 * g], side));
+      HIP_TRY(hipStreamWaitEvent(stream, ev[1 + 2 * g], 0));
+      launch_trail128_split(Ain, Aout, D, B2, g, 1, st, stream);  // rest(g)
+      HIP_TRY(hipEventRecord(ev[2 + 2 * g], stream));
+      if (g >= 1) HIP_TRY(hipStreamWaitEvent(side, ev[2 * g], 0));  // rest(g - 1)
+      launch_trail128_split(Ain, Aout, D, B2, g, 0, st, side);  // block g + 1's bands
+    } else {
+      if (g >= 1) HIP_TRY(hipStreamWaitEvent(side, ev[2 * g], 0));
+      if (fuse && gemm_trail_supported(*fuse)) {
+        launch_gemm_trail(*fuse, Ain, Aout, D, B2, g, true, st, t32_pf(), -1, side);
+        fused = true;
+      } else {
+        launch_trail128(Ain, Aout, D, B2, g, true, st, side);
+      }
+    }
+  }
+  HIP_TRY(hipEventRecord(ev[2 * K2 + 1], side));
+  HIP_TRY(hipStreamWaitEvent(stream, ev[2 * K2 + 1], 0));
+  HIP_TRY(hipGetLastError());
+  return fused;
+}
+
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
-                            hipStream_t stream, int passes, const GemmSpec* fuse) {
+                            hipStream_t stream, int passes, const GemmSpec* fuse, const TrailLookAhead* tla) {
   bool fused = false;
   const int B2 = binv_block(D);
   if (B2 == 0) throw std::invalid_argument("blocked inverse needs D >= 256, D % 128 == 0");
   const int K2 = (int)(D / B2), gb = B2 / NB, mb = (int)(D / NB) - gb;
+  if (fast && tla && K2 >= 2 && D - B2 >= TRAIL128_MIN && (B2 == 256 || B2 == 128))
+    return blocked_inverse_lookahead(Mt, D, B2, bw, st, stream, passes, fuse, *tla);
   double* bufs[2] = {binv_build_target(Mt, D, bw), nullptr};
   bufs[1] = bufs[0] == Mt ? bw.Aalt : Mt;
   // look-ahead residual (NmLA / TrailLA): fast path with 32 x 32 trailing updates

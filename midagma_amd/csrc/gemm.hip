@@ -337,7 +337,22 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
   const int per_slice = tiles_m * tiles_n;
   const int z = t / per_slice, rem = t % per_slice;
   int bm, bn;
-  if (tiles_n > 8) {
+  if (EPI == EPI_SUB_CROSS) {
+    // look-ahead part of a trailing update (launch_trail128_split): the tiles in the row or column
+    // band of the NEXT outer block, which sits right after the pivot band b = m_valid, nb =
+    // n_valid tiles wide; tiles_m = the trailing grid's edge (pivot band skipped)
+    const int b = (int)m_valid, nb = (int)n_valid, tm = tiles_m;
+    if (t < nb * tm) {
+      bm = b + t / tm;
+      bn = t % tm;
+    } else {
+      const int u = t - nb * tm, ri = u / nb;
+      bm = ri < b ? ri : ri + nb;
+      bn = b + u % nb;
+    }
+    bm += bm >= b ? nb : 0;  // skip the pivot band
+    bn += bn >= b ? nb : 0;
+  } else if (tiles_n > 8) {
     // grouped order: the 64 consecutive tiles one XCD holds resident (32 CUs x 2) form an
     // 8 x 8 block, so its L2 serves each A row panel and B column panel to 8 tiles (row-major
     // order put 40 different B panels in flight per XCD at d = 5000)
@@ -498,7 +513,7 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
 #undef GP_FRAG
 #undef GP_MMA
 #undef GP_SCHED
-  if (EPI == EPI_SUB_BAND) {  // C = C0 - acc, C0 passed as loss_part; slice_stride = check flags
+  if (EPI == EPI_SUB_BAND || EPI == EPI_SUB_CROSS) {  // C = C0 - acc, C0 as loss_part; slice_stride = check
     const double* C0 = loss_part;
     int flag = 0;
 #pragma unroll
@@ -690,6 +705,7 @@ void gemm_setup_attributes() {
   set_attr_pipe<1, B_PLAIN, EPI_SIGMOID>();
   set_attr_pipe<0, B_PLAIN, EPI_SIGMOID>();
   set_attr_pipe<0, B_PLAIN, EPI_SUB_BAND>();
+  set_attr_pipe<0, B_PLAIN, EPI_SUB_CROSS>();
   set_attr128<false, B_PLAIN, EPI_STORE>();
   set_attr128<false, B_IMINUS, EPI_STORE>();
   set_attr128<true, B_PLAIN, EPI_STORE>();
@@ -884,6 +900,29 @@ void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int
     hipLaunchKernelGGL((gemm128_kernel<false, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
                        kGemm128Lds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
                        (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
+  HIP_TRY(hipGetLastError());
+}
+
+// The trailing update of outer step g in two parts (the cov-mode look-ahead, blockinv.hip):
+// part 0 the tiles in the row / column band of block g + 1 (what its series and panel read),
+// part 1 the rest (both bands skipped).  The same tile bodies as launch_trail128.
+void launch_trail128_split(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, int part,
+                           const State* st, hipStream_t stream) {
+  if (D % 128 || B2 % 128 || (g + 2) * B2 > D) throw std::invalid_argument("launch_trail128_split: shape");
+  const int tm = (int)((D - B2) / 128), nb = (int)(B2 / 128);
+  const int64_t G0 = g * B2;
+  if (part == 0) {
+    const int n = nb * (2 * tm - nb);
+    hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_CROSS>), dim3((unsigned)n), dim3(NTHREADS), kGemmPipeLds,
+                       stream, B2, B2, tm, nb, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
+                       const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)nb, st);
+  } else {
+    const int tr = tm - nb;
+    if (tr <= 0) return;
+    hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tr * tr)), dim3(NTHREADS),
+                       kGemmPipeLds, stream, B2, B2, tr, tr, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
+                       const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(2 * nb), st);
+  }
   HIP_TRY(hipGetLastError());
 }
 

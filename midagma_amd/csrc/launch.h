@@ -92,8 +92,15 @@ double* binv_build_target(double* Mt, int64_t D, const BInvWork& bw);
 // fuse (nullable; fast path): a GEMM (EPI_STORE, split-K slices) that runs in the launch of the
 // last outer step's 32 x 32 trailing update (gemm.hip, launch_gemm_trail); false is returned
 // when that launch is not available for this D and the caller must launch the GEMM itself.
+// tla (nullable; fast path, 128-tile trailing updates): the look-ahead across two streams
+// (blocked_inverse_lookahead in blockinv.hip): a high-priority side stream and 2 K2 + 2 events.
+struct TrailLookAhead {
+  hipStream_t side;
+  hipEvent_t* ev;
+};
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
-                            hipStream_t stream, int passes = NM_PASSES_RUN, const GemmSpec* fuse = nullptr);
+                            hipStream_t stream, int passes = NM_PASSES_RUN, const GemmSpec* fuse = nullptr,
+                            const TrailLookAhead* tla = nullptr);
 
 // One B2 x B2 block (B2 = 128 or 256) by the product-form series from the warm start in the
 // ring Pe / Po (the slot parity and the extrapolation rule of the blocked inverse: st->slots,
@@ -306,7 +313,8 @@ void launch_sem_slab(const SemDev& g, const std::vector<int32_t>& level_off, int
 
 // --- gemm.hip ---------------------------------------------------------------
 enum GemmB : int { B_PLAIN = 0, B_IMINUS = 1 };
-enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1, EPI_SUB_BAND = 2 /* launch_trail128 only */ };
+enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1, EPI_SUB_BAND = 2 /* launch_trail128 only */,
+                     EPI_SUB_CROSS = 3 /* launch_trail128_split only */ };
 void gemm_setup_attributes();
 // C[M x N] = op(A) * op(B); op(A) = A ([m][k], lda) or, if a_trans, A stored [k][m] (lda);
 // op(B) = B or (I - B) ([k][n], ldb).  M, N, K multiples of 64.  With split > 1
@@ -322,6 +330,10 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
 // with `check`, ORs the domain flags of the outputs into st->flags.
 void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
                      hipStream_t stream);
+// The same update in two launches: part 0 the tiles in block g + 1's row and column bands, part 1
+// the rest (no domain check: the look-ahead runs on steps before the last).
+void launch_trail128_split(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, int part,
+                           const State* st, hipStream_t stream);
 // The GEMM gs (EPI_STORE) and the blocked inverse's 32 x 32 trailing update of outer step g
 // (n_trail tiles) in one launch.
 bool gemm_trail_supported(const GemmSpec& gs);

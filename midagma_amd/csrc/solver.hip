@@ -168,6 +168,7 @@ struct midagma_solver {
     if (side) (void)hipStreamDestroy(side);
     for (hipEvent_t e : {ev_fork, ev_join})
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : la_ev) (void)hipEventDestroy(e);
   }
 
   void destroy_graphs() {
@@ -202,6 +203,11 @@ struct midagma_solver {
   // cov mode at large D (the 128-tile trailing update): the score GEMM beside the inverse
   // (experiment knob MIDAGMA_EXP_COV_FORK: 1 on, 0 off)
   bool cov_fork = knob("MIDAGMA_EXP_COV_FORK", 0) != 0;
+  // cov mode at large D, fast slots: the trailing-update look-ahead on two streams (blockinv.hip
+  // blocked_inverse_lookahead; experiment knob MIDAGMA_EXP_COV_LA: 1 on, 0 off)
+  bool cov_la = knob("MIDAGMA_EXP_COV_LA", 0) != 0;
+  std::vector<hipEvent_t> la_ev;
+  bool cov_la_on() const { return cov_la && side != nullptr && mode == MIDAGMA_MODE_COV && blocked() && D - B2 >= 1792; }
   bool cov_fork_on() const {
     return cov_fork && side != nullptr && mode == MIDAGMA_MODE_COV && blocked() && D - B2 >= 1792 && !trek_on;
   }
@@ -284,6 +290,18 @@ struct midagma_solver {
 #endif
     launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state, stream,
                     IW.p);
+    if (fast && cov_la_on()) {
+      const int64_t K2 = D / B2;
+      if ((int64_t)la_ev.size() < 2 * K2 + 2) {
+        for (size_t i = la_ev.size(); i < (size_t)(2 * K2 + 2); ++i) {
+          hipEvent_t e = nullptr;
+          HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+          la_ev.push_back(e);
+        }
+      }
+      const TrailLookAhead tla{side, la_ev.data()};
+      return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse, &tla);
+    }
     return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse);
   }
   bool fuse_gemm = knob("MIDAGMA_EXP_FUSE_GEMM", 1) != 0;
@@ -596,7 +614,8 @@ struct midagma_solver {
     HIP_TRY(hipMalloc(&d_state, sizeof(State)));
     HIP_TRY(hipHostMalloc(&h_state, 2 * sizeof(State), hipHostMallocDefault));
     for (auto& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if ((mode == MIDAGMA_MODE_DATA && fork_inv) || (mode == MIDAGMA_MODE_COV && cov_fork && B2 > 0 && D - B2 >= 1792)) {
+    if ((mode == MIDAGMA_MODE_DATA && fork_inv) ||
+        (mode == MIDAGMA_MODE_COV && (cov_fork || cov_la) && B2 > 0 && D - B2 >= 1792)) {
       int lo = 0, hi = 0;  // hi: the greatest priority (numerically least)
       HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
       HIP_TRY(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, hi));

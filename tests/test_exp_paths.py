@@ -69,3 +69,28 @@ def test_blocked_lookahead_residual_experiment(monkeypatch, d):
     assert np.abs(W - Wr).max() <= 1e-9
     for c, (_, obj_r, _, h_r) in zip(res.checkpoints, tr.checkpoints):
         assert abs(c[1] - obj_r) <= 1e-10 * abs(obj_r) and abs(c[3] - h_r) <= 1e-9 * max(1.0, abs(h_r))
+
+
+@pytest.mark.parametrize("d", [2000, 2100])
+def test_cov_lookahead_bit_identical(monkeypatch, d):
+    """The trailing-update look-ahead across two streams (MIDAGMA_EXP_COV_LA=1: each outer step's
+    128-tile trailing update split into block g+1's bands and the rest, the series / panel chain on
+    the high-priority side stream) computes every tile with the same body: W, iterations and the
+    checkpoint objectives are bit-identical to the one-stream path, and match the oracle.  d=2000 ->
+    D=2048 (B2=256, 8 outer blocks), 2100 -> 2176 (B2=128, 17)."""
+    X, _, _ = make_dataset(d, 2 * d, seed=d + 1)
+    o = _oracle(X, 4)
+    K = 12
+    out = {}
+    for la in ("0", "1"):
+        monkeypatch.setenv("MIDAGMA_EXP_COV_LA", la)
+        s = _solver(d, o.cov)
+        W = np.zeros((d, d))
+        r = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=4, want_checkpoints=True)
+        s.close()
+        out[la] = (W, r)
+    (W0, r0), (W1, r1) = out["0"], out["1"]
+    assert r0.iters == r1.iters == K and np.array_equal(W0, W1)
+    assert [c[1] for c in r0.checkpoints] == [c[1] for c in r1.checkpoints]
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert np.abs(W1 - Wr).max() <= 1e-9

@@ -142,6 +142,14 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_COV_PAD_B2={f}", end=" ")
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_COV_PAD_B2")
+    if which == "covla":  # large D cov mode: the trailing-update look-ahead (MIDAGMA_EXP_COV_LA)
+        ds = [int(x) for x in sys.argv[2:]] or [2000, 5000]
+        for d in ds:
+            for f in ("0", "1"):
+                os.environ["MIDAGMA_EXP_COV_LA"] = f
+                print(f"MIDAGMA_EXP_COV_LA={f}", end=" ")
+                cov_case(d, 2 * d, 3, 200 if d <= 2500 else 60)
+        os.environ.pop("MIDAGMA_EXP_COV_LA")
     if which == "covfork":  # large D cov mode: score GEMM beside the inverse (MIDAGMA_EXP_COV_FORK)
         ds = [int(x) for x in sys.argv[2:]] or [2000, 5000]
         for d in ds:
