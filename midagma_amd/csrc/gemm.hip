@@ -340,7 +340,8 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
   if (EPI == EPI_SUB_CROSS) {
     // look-ahead part of a trailing update (launch_trail128_split): the tiles in the row or column
     // band of the NEXT outer block, which sits right after the pivot band b = m_valid, nb =
-    // n_valid tiles wide; tiles_m = the trailing grid's edge (pivot band skipped)
+    // n_valid tiles wide; tiles_m = the trailing grid's edge (pivot band skipped), tiles_n = 2 nb
+    // (so that tiles_m tiles_n covers the grid and z = 0)
     const int b = (int)m_valid, nb = (int)n_valid, tm = tiles_m;
     if (t < nb * tm) {
       bm = b + t / tm;
@@ -913,8 +914,9 @@ void launch_trail128_split(const double* Ain, double* Aout, int64_t D, int64_t B
   const int64_t G0 = g * B2;
   if (part == 0) {
     const int n = nb * (2 * tm - nb);
+    // (tiles_n = 2 nb: tiles_m tiles_n >= n, so every tile is in K slice 0)
     hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_CROSS>), dim3((unsigned)n), dim3(NTHREADS), kGemmPipeLds,
-                       stream, B2, B2, tm, nb, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
+                       stream, B2, B2, tm, 2 * nb, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
                        const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)nb, st);
   } else {
     const int tr = tm - nb;

@@ -48,3 +48,29 @@ def test_create_without_gpu_raises():
     from midagma_amd._lib import HipSolverError
     with pytest.raises(HipSolverError):
         HipSolver(8)
+
+
+def test_product_library_reads_no_experiment_knobs():
+    """The product library compiles every MIDAGMA_EXP_* experiment knob to its default
+    (csrc/knobs.h): no such variable name is in it, and the rejected one-launch inverse
+    (dfinv.hip) is not linked in; the experiments build has both."""
+    from midagma_amd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"MIDAGMA_EXP_" not in blob
+    assert b"midagma_debug_df_plan" not in blob and b"df_plan" not in blob
+    exp = os.path.join(os.path.dirname(_lib.LIB_PATH), "libmidagma_hip_exp.so")
+    if os.path.exists(exp):
+        eb = open(exp, "rb").read()
+        assert b"MIDAGMA_EXP_DF" in eb and b"midagma_debug_df_plan" in eb
+
+
+def test_ldfast_entry_points_validate_without_a_device():
+    """The ABI-6 warm-started log-det entries refuse bad arguments before touching a device."""
+    import ctypes as C
+    from midagma_amd import _lib
+    L = _lib.load()
+    assert L.midagma_ldfast_parts(None, 1) == 0
+    assert L.midagma_ldfast_enqueue(None, None, 10, 1.0, None, None, 10, None, 0, -1) == -3
+    out = C.c_void_p()
+    assert L.midagma_ldfast_create(C.byref(out), 0) == -3
+    assert L.midagma_ldfast_reset(None) == -3
