@@ -348,7 +348,24 @@ def bench_mlp(args, device, with_cpu):
                          "note": "steps of the timed call whose log-det ran the Gauss-Jordan chain (the first and the "
                                  "last, whose objective the loop reads, plus any whose warm-started inverse was not "
                                  "certified); the rest took the product-form series"}
-    out["_check"] = dict(params=params, X=X, calls=[20, K], final=final)
+    # Value check: the reference's MLP trajectory is itself chaotic past a few hundred steps (a
+    # 1e-15 relative change of the initial parameters moves them by 4e-4 at step 1020 and 6e-3 at
+    # 2020 in the oracle; tools/mlp_chaos.py, profiles/r03_mlp_chaos.log), so the 1e-9 comparison
+    # runs a separate 20 + 300-step replay of the same path (graphs, warm-started log-det) from
+    # the same parameters; the timed window's own deviation is reported beside it.
+    with torch.no_grad():
+        for k, v in model.state_dict().items():
+            if k in params:
+                v.copy_(torch.from_numpy(params[k]))
+    dn2 = DagmaNonlinear(model, device=device)
+    dn2.X = dn.X
+    dn2.checkpoint = 10 ** 9
+    dn2.minimize(20, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
+    dn2.minimize(300, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
+    torch.cuda.synchronize(device)
+    final_check = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items() if k in params}
+    out["_check"] = dict(params=params, X=X, calls=[20, 300], final=final_check, timed_calls=[20, K],
+                         timed_final=final)
     if with_cpu:
         best = None
         phys = host_cpus()["physical_cores"]
@@ -751,17 +768,29 @@ def value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world)
         c = mlp_res.pop("_check")
         inp = dict(c["params"], X=c["X"], d=c["X"].shape[1], calls=np.array(c["calls"]))
         out = oracle_run("mlp", inp, threads=16)
+
+        def pdev(fin, ref):
+            return {k: float(np.abs(fin[k] - ref[k]).max() / max(1.0, np.abs(ref[k]).max())) for k in fin}
         if out is None:
             mlp_res["value_check"] = {"ok": False, "error": "oracle run failed"}
         else:
-            dev = {k: float(np.abs(c["final"][k] - out[k]).max() / max(1.0, np.abs(out[k]).max()))
-                   for k in c["final"]}
+            dev = pdev(c["final"], out)
             worst = max(dev.values())
             mlp_res["value_check"] = {
                 "ok": bool(worst <= 1e-9), "max_dparam_rel": worst, "tol": 1e-9, "per_param": dev,
                 "steps": int(sum(c["calls"])), "calls": c["calls"],
                 "oracle": "oracle DagmaNonlinear.minimize (torch CPU, slogdet h_func), the same calls from the "
-                          "same parameters; |dp| / max(1, max|p|)"}
+                          "same parameters, replayed on the GPU after the timed run through the same path; "
+                          "|dp| / max(1, max|p|)"}
+            inp_t = dict(inp, calls=np.array(c["timed_calls"]))
+            out_t = oracle_run("mlp", inp_t, threads=16)
+            if out_t is not None:
+                dt_ = pdev(c["timed_final"], out_t)
+                mlp_res["value_check"]["timed_window"] = {
+                    "calls": c["timed_calls"], "max_dparam_rel": max(dt_.values()),
+                    "note": "not held to 1e-9: the reference's trajectory is chaotic here (a 1e-15 relative "
+                            "change of the start moves the oracle's parameters by 6e-3 at step 2020, "
+                            "profiles/r03_mlp_chaos.log)"}
     for lg in logi or []:
         c = lg.pop("_check", None)
         if c is None:
@@ -969,10 +998,12 @@ def main():
                     sample=f"oracle logistic Adam step (linear.py:246) at d={args.d}, n=10000 binary X: 2 steps "
                            f"per thread count after a warm step, threads {sorted(t)}, best shown")
                 logi[0]["vs_cpu"] = logi[0]["value"] / v
-    if rank == 0 and res is None and cov_res is None:   # --no-data --no-cov: a profiling run of the other legs
+    if rank == 0 and res is None and args.workload == "data":   # --no-data: a profiling run of the other legs
         out = {k: v for k, v in (large_res or {}).items() if k not in ("cov", "W_check")}
-        print(json.dumps({"config3": out, "full_fit": fit_res, "config5": mlp_res, "config1": small_res,
-                          "logistic": logi}), flush=True)
+        cov_out = None if cov_res is None else {k: v for k, v in cov_res.items()
+                                                if not isinstance(v, np.ndarray) and k not in ("cov", "_check")}
+        print(json.dumps({"cov_mode": cov_out, "config3": out, "full_fit": fit_res, "config5": mlp_res,
+                          "config1": small_res, "logistic": logi}), flush=True)
         return
     if rank == 0:
         d = args.d

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
   const int per_slice = tiles_m * tiles_n;
   const int z = t / per_slice, rem = t % per_slice;
   int bm = rem / tiles_n, bn = rem % tiles_n;
-  if (EPI == EPI_SUB_BAND) {
+  if (EPI == EPI_SUB_BAND || EPI == EPI_SUB_PRE) {
     // trailing update of the blocked inverse: the tile grid skips the pivot band
     // [m_valid, m_valid + n_valid) (in 128-tiles) in both rows and columns
     bm += bm >= (int)m_valid ? (int)n_valid : 0;
@@ -365,7 +365,7 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
     bm = rem / tiles_n;
     bn = rem % tiles_n;
   }
-  if (EPI == EPI_SUB_BAND) {
+  if (EPI == EPI_SUB_BAND || EPI == EPI_SUB_PRE) {
     // trailing update of the blocked inverse: the tile grid skips the pivot band
     // [m_valid, m_valid + n_valid) (in 128-tiles) in both rows and columns
     bm += bm >= (int)m_valid ? (int)n_valid : 0;
@@ -432,6 +432,10 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
       b0_ = (kg_ == ng_ ? 1.0 : 0.0) - b0_;                                                       \
       b1_ = (kg_ == ng_ + 1 ? 1.0 : 0.0) - b1_;                                                   \
     }                                                                                             \
+    if (EPI == EPI_SUB_PRE) {                                                                     \
+      b0_ = -b0_;                                                                                 \
+      b1_ = -b1_;                                                                                 \
+    }                                                                                             \
     _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                            \
       acc[i_][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(FA[i_], b0_, acc[i_][0], 0, 0, 0);         \
       acc[i_][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(FA[i_], b1_, acc[i_][1], 0, 0, 0);         \
@@ -468,6 +472,21 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
     GP_LOADA(k_begin)
 #pragma unroll
     for (int q = 0; q < 4; ++q) GP_LOADB1(k_begin, q)
+    if (EPI == EPI_SUB_PRE) {
+      // C = C0 + sum (-a) b: the accumulators start from C0 (loads issued behind the first
+      // operand tile, so they overlap the prologue instead of a load-then-store epilogue)
+      const double* C0 = loss_part;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const int64_t row = m0 + 16 * i + acc_row(lane, tt);
+          const int64_t col = nw + 2 * acc_col(lane);
+          const double2 c0 = *reinterpret_cast<const double2*>(C0 + row * ldc + col);
+          acc[i][0][tt] = c0.x;
+          acc[i][1][tt] = c0.y;
+        }
+    }
     GP_STOREA(As0)
     GP_LOADA((k_begin + 16 < k_end) ? k_begin + 16 : k_begin)
     __syncthreads();
@@ -514,6 +533,22 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
 #undef GP_FRAG
 #undef GP_MMA
 #undef GP_SCHED
+  if (EPI == EPI_SUB_PRE) {  // acc = C0 - A B already; slice_stride = check
+    int flag = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int64_t row = m0 + 16 * i + acc_row(lane, tt);
+        const int64_t col = nw + 2 * acc_col(lane);
+        const double2 v = double2{acc[i][0][tt], acc[i][1][tt]};
+        *reinterpret_cast<double2*>(C + row * ldc + col) = v;
+        flag |= (v.x + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v.x) ? 0 : 2);
+        flag |= (v.y + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v.y) ? 0 : 2);
+      }
+    if (slice_stride && flag) atomicOr(const_cast<int32_t*>(&st->flags), flag);
+    return;
+  }
   if (EPI == EPI_SUB_BAND || EPI == EPI_SUB_CROSS) {  // C = C0 - acc, C0 as loss_part; slice_stride = check
     const double* C0 = loss_part;
     int flag = 0;
@@ -707,6 +742,9 @@ void gemm_setup_attributes() {
   set_attr_pipe<0, B_PLAIN, EPI_SIGMOID>();
   set_attr_pipe<0, B_PLAIN, EPI_SUB_BAND>();
   set_attr_pipe<0, B_PLAIN, EPI_SUB_CROSS>();
+#ifdef MIDAGMA_EXPERIMENTS
+  set_attr_pipe<0, B_PLAIN, EPI_SUB_PRE>();
+#endif
   set_attr128<false, B_PLAIN, EPI_STORE>();
   set_attr128<false, B_IMINUS, EPI_STORE>();
   set_attr128<true, B_PLAIN, EPI_STORE>();
@@ -903,6 +941,22 @@ void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int
                        (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
   HIP_TRY(hipGetLastError());
 }
+
+#ifdef MIDAGMA_EXPERIMENTS
+// launch_trail128 with the accumulators preloaded from C0 (EPI_SUB_PRE; experiments build only:
+// measured no faster, tools/micro/trail_micro.hip)
+void launch_trail128_pre(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
+                         const State* st, hipStream_t stream) {
+  if (D % 128 || B2 % 128) throw std::invalid_argument("launch_trail128_pre: D, B2 must be multiples of 128");
+  const int tm = (int)((D - B2) / 128);
+  if (tm <= 0) return;
+  const int64_t G0 = g * B2;
+  hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_PRE>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
+                     kGemmPipeLds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
+                     (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
+  HIP_TRY(hipGetLastError());
+}
+#endif
 
 // The trailing update of outer step g in two parts (the cov-mode look-ahead, blockinv.hip):
 // part 0 the tiles in the row / column band of block g + 1 (what its series and panel read),

@@ -314,7 +314,8 @@ void launch_sem_slab(const SemDev& g, const std::vector<int32_t>& level_off, int
 // --- gemm.hip ---------------------------------------------------------------
 enum GemmB : int { B_PLAIN = 0, B_IMINUS = 1 };
 enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1, EPI_SUB_BAND = 2 /* launch_trail128 only */,
-                     EPI_SUB_CROSS = 3 /* launch_trail128_split only */ };
+                     EPI_SUB_CROSS = 3 /* launch_trail128_split only */,
+                     EPI_SUB_PRE = 4 /* EPI_SUB_BAND with C0 preloaded into the accumulators */ };
 void gemm_setup_attributes();
 // C[M x N] = op(A) * op(B); op(A) = A ([m][k], lda) or, if a_trans, A stored [k][m] (lda);
 // op(B) = B or (I - B) ([k][n], ldb).  M, N, K multiples of 64.  With split > 1
@@ -330,6 +331,11 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
 // with `check`, ORs the domain flags of the outputs into st->flags.
 void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
                      hipStream_t stream);
+#ifdef MIDAGMA_EXPERIMENTS
+// The same update with the accumulators preloaded from C0 (experiments build, tools/micro/trail_micro.hip)
+void launch_trail128_pre(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
+                         const State* st, hipStream_t stream);
+#endif
 // The same update in two launches: part 0 the tiles in block g + 1's row and column bands, part 1
 // the rest (no domain check: the look-ahead runs on steps before the last).
 void launch_trail128_split(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, int part,

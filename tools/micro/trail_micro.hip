@@ -1,0 +1,119 @@
+// Development micro-benchmark (not part of the library): the blocked inverse's 128-tile trailing
+// update (launch_trail128, C = C0 - A B with C0 read in the epilogue) against the variant whose
+// accumulators start from C0 (launch_trail128_pre) and the same tile grid with no C0 at all
+// (launch_gemm EPI_STORE), hipEvent-timed.
+//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DMIDAGMA_EXPERIMENTS
+//          -I../../midagma_amd/csrc trail_micro.hip ../../midagma_amd/csrc/gemm.hip -o trail_micro
+//   run  : ./trail_micro [D ...]   (default 2048 3072 5120; B2 = 256, outer step g = 1)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "launch.h"
+
+using namespace midagma;
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(2);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+__global__ void fill_kernel(double* p, int64_t n, uint64_t seed, double scale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    p[i] = scale * ((double)(z >> 11) * (1.0 / 9007199254740992.0) - 0.5);
+  }
+}
+
+__global__ void reldiff_kernel(const double* a, const double* b, int64_t n, unsigned long long* out) {
+  double m = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmax(m, fabs(a[i] - b[i]) / fmax(1e-300, fabs(b[i])));
+  atomicMax(out, (unsigned long long)__double_as_longlong(m));
+}
+
+static double reldiff(const double* a, const double* b, int64_t n) {
+  unsigned long long* d;
+  CK(hipMalloc(&d, 8));
+  CK(hipMemset(d, 0, 8));
+  hipLaunchKernelGGL(reldiff_kernel, dim3(4096), dim3(256), 0, 0, a, b, n, d);
+  unsigned long long h = 0;
+  CK(hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost));
+  CK(hipFree(d));
+  double r;
+  memcpy(&r, &h, 8);
+  return r;
+}
+
+template <class F>
+static double time_us(F&& f, int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  f();
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(a, 0));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return 1e3 * ms / reps;
+}
+
+int main(int argc, char** argv) {
+  std::vector<int64_t> Ds;
+  for (int i = 1; i < argc; ++i) Ds.push_back(atoll(argv[i]));
+  if (Ds.empty()) Ds = {2048, 3072, 5120};
+  gemm_setup_attributes();
+  const int64_t B2 = 256, g = 1;
+  const int reps = 50;
+  for (int64_t D : Ds) {
+    double *Ain, *Aout, *Aout2, *C;
+    CK(hipMalloc(&Ain, sizeof(double) * D * D));
+    CK(hipMalloc(&Aout, sizeof(double) * D * D));
+    CK(hipMalloc(&Aout2, sizeof(double) * D * D));
+    CK(hipMalloc(&C, sizeof(double) * D * D));
+    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, Ain, D * D, 1, 2.0);
+    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, Aout, D * D, 2, 2.0);
+    CK(hipMemcpy(Aout2, Aout, sizeof(double) * D * D, hipMemcpyDeviceToDevice));
+    CK(hipDeviceSynchronize());
+    const int64_t t = D - B2;
+    const double f = 2.0 * t * t * B2;
+    const double us_lib = time_us([&] { launch_trail128(Ain, Aout, D, B2, g, false, nullptr, 0); }, reps);
+    const double us_pre = time_us([&] { launch_trail128_pre(Ain, Aout2, D, B2, g, false, nullptr, 0); }, reps);
+    CK(hipDeviceSynchronize());
+    const double rd = reldiff(Aout2, Aout, D * D);
+    const double us_st = time_us([&] {
+      launch_gemm(t, t, B2, Ain, D, false, Aout, D, B_PLAIN, C, D, EPI_STORE, 1, 0, nullptr, 0, 0, nullptr, 0);
+    }, reps);
+    // in place (Aout = Ain: the whole matrix is one 8 D^2-byte buffer, which fits the 256 MB
+    // Infinity Cache up to D ~ 5600; timing only: the column band is read while other tiles write)
+    const double us_ip = time_us([&] { launch_trail128(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
+    const double us_ip_pre = time_us([&] { launch_trail128_pre(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
+    const int tiles = (int)((t / 128) * (t / 128));
+    printf("D=%5ld tiles=%5d (%.2f rounds of 512)  lib %8.2f us %5.1f TF | pre %8.2f us %5.1f TF | "
+           "no-C0 store %8.2f us %5.1f TF | in place %8.2f / pre %8.2f us | max rel diff pre vs lib %.2e\n",
+           (long)D, tiles, tiles / 512.0, us_lib, f / us_lib / 1e6, us_pre, f / us_pre / 1e6, us_st, f / us_st / 1e6,
+           us_ip, us_ip_pre, rd);
+    fflush(stdout);
+    CK(hipFree(Ain));
+    CK(hipFree(Aout));
+    CK(hipFree(Aout2));
+    CK(hipFree(C));
+  }
+  return 0;
+}

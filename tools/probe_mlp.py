@@ -3,6 +3,8 @@ n = 1000, with the log-det on a side stream or not (MIDAGMA_NO_OVERLAP) and with
 fast log-det or every step exact (MIDAGMA_NO_LDFAST); prints steps/s and the fast path's share.
 
     python tools/probe_mlp.py [K]
+    python tools/probe_mlp.py K pre    # the fast variant after each of the bench's earlier legs' solvers
+                                       # (cov d=1000, cov d=5000, data d=1000 n=1e5) in the same process
 """
 import os
 import sys
@@ -43,8 +45,53 @@ def run(K, overlap, fast):
           f"{'' if st is None else f'  steps {st[0]}, Gauss-Jordan {st[1]}'}", flush=True)
 
 
+def pre_leg(kind):
+    """One of the bench's earlier solvers, run and closed in this process."""
+    from midagma_amd.solver import HipSolver
+    if kind.startswith("cov"):
+        d = int(kind[3:])
+        X, _, _ = make_dataset(d, 2 * d, seed=0)
+        X -= X.mean(0)
+        s = HipSolver(d, "l2", "cov")
+        s.set_cov(X.T @ X / X.shape[0])
+        K = 2000 if d <= 1000 else 20
+    else:
+        d, n = 1000, 100_000
+        X = np.random.default_rng(0).standard_normal((n, d))
+        s = HipSolver(d, "l2", "data")
+        s.set_data(X, n_global=n)
+        K = 20
+    s.begin(np.zeros((d, d)), 1.0, K + 10, 1.0, 3e-4, tol=-1.0)
+    s.run_slots(K)
+    s.sync()
+    s.close()
+    torch.cuda.synchronize()
+    print(f"-- after {kind}:", flush=True)
+
+
 if __name__ == "__main__":
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+    if len(sys.argv) > 2 and sys.argv[2] == "queues":
+        # the log-det side stream created after 0..7 other streams (HIP maps streams onto
+        # GPU_MAX_HW_QUEUES hardware queues round-robin)
+        import midagma_amd.nonlinear as nl
+        keep = []
+        for extra in range(8):
+            nl._SIDE.clear()
+            print(f"-- side stream created after {extra} extra streams:", flush=True)
+            run(K, True, True)
+            keep.append(torch.cuda.Stream())
+        sys.exit(0)
+    if len(sys.argv) > 2 and sys.argv[2] == "fast":
+        run(K, True, True)
+        sys.exit(0)
+    if len(sys.argv) > 2 and sys.argv[2] == "pre":
+        run(K, True, True)
+        for kind in ("cov1000", "cov5000", "data"):
+            pre_leg(kind)
+            run(K, True, True)
+            run(K, False, True)
+        sys.exit(0)
     for overlap in (True, False):
         for fast in (True, False):
             run(K, overlap, fast)
