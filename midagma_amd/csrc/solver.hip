@@ -207,6 +207,16 @@ struct midagma_solver {
   // blocked_inverse_lookahead; experiment knob MIDAGMA_EXP_COV_LA: 1 on, 0 off)
   bool cov_la = knob("MIDAGMA_EXP_COV_LA", 0) != 0;
   std::vector<hipEvent_t> la_ev;
+  // blocked slots enqueued launch by launch instead of replayed graphs (experiment knob
+  // MIDAGMA_EXP_EAGER: at large D the host runs far ahead of a multi-ms slot, and cross-stream
+  // waits are plain queue barriers instead of graph edges)
+  bool eager = knob("MIDAGMA_EXP_EAGER", 0) != 0;
+  void run_eager(bool fast, int passes, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) {
+      enqueue_part1(fast, passes);
+      enqueue_part2(fast);
+    }
+  }
   bool cov_la_on() const { return cov_la && side != nullptr && mode == MIDAGMA_MODE_COV && blocked() && D - B2 >= 1792; }
   bool cov_fork_on() const {
     return cov_fork && side != nullptr && mode == MIDAGMA_MODE_COV && blocked() && D - B2 >= 1792 && !trek_on;
@@ -616,9 +626,12 @@ struct midagma_solver {
     for (auto& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if ((mode == MIDAGMA_MODE_DATA && fork_inv) ||
         (mode == MIDAGMA_MODE_COV && (cov_fork || cov_la) && B2 > 0 && D - B2 >= 1792)) {
-      int lo = 0, hi = 0;  // hi: the greatest priority (numerically least)
-      HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIP_TRY(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, hi));
+      // Default priority: a fork / join between a high-priority stream and another one left the
+      // process's later two-stream work ~5x slower (the config-5 step after a data-mode solver:
+      // 7.5k -> 1.3k steps/s, also after a plain torch fork / join; tools/probe_after_data.py),
+      // and the forked inverse hides just as well without it (config 4: 17.46 vs 17.50 steps/s
+      // at n = 1e6, 133.8 vs 133.5 at the 8-GPU shard n = 125k)
+      HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     }
@@ -803,11 +816,16 @@ struct midagma_solver {
         static const int32_t running = ST_RUNNING;
         HIP_TRY(hipMemcpyAsync(&d_state->status, &running, sizeof(int32_t), hipMemcpyHostToDevice, stream));
       }
-      if (p.slow) HIP_TRY(hipGraphLaunch(g_full, stream));  // pivots + fresh warm starts
-      // (a hand-back inside a group turns the group's later slots into no-op launches)
-      hipGraphExec_t one = p.two_pass ? g_fast2 : g_fast, grp = p.two_pass ? g_fastN2 : g_fastN;
-      for (int64_t b = 0; b < p.groups; ++b) HIP_TRY(hipGraphLaunch(grp, stream));
-      for (int64_t b = 0; b < p.singles; ++b) HIP_TRY(hipGraphLaunch(one, stream));
+      if (eager) {
+        if (p.slow) run_eager(false, NM_PASSES_RUN, 1);
+        run_eager(true, p.two_pass ? 2 : NM_PASSES_RUN, p.groups * fast_group + p.singles);
+      } else {
+        if (p.slow) HIP_TRY(hipGraphLaunch(g_full, stream));  // pivots + fresh warm starts
+        // (a hand-back inside a group turns the group's later slots into no-op launches)
+        hipGraphExec_t one = p.two_pass ? g_fast2 : g_fast, grp = p.two_pass ? g_fastN2 : g_fastN;
+        for (int64_t b = 0; b < p.groups; ++b) HIP_TRY(hipGraphLaunch(grp, stream));
+        for (int64_t b = 0; b < p.singles; ++b) HIP_TRY(hipGraphLaunch(one, stream));
+      }
       HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
       cur = view(h_state[1]);

@@ -150,6 +150,16 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_COV_LA={f}", end=" ")
                 cov_case(d, 2 * d, 3, 200 if d <= 2500 else 60)
         os.environ.pop("MIDAGMA_EXP_COV_LA")
+    if which == "eagerla":  # large D cov mode: eager launches (MIDAGMA_EXP_EAGER) with / without the look-ahead
+        ds = [int(x) for x in sys.argv[2:]] or [2000, 3000, 5000]
+        for d in ds:
+            for e, la in (("0", "0"), ("1", "0"), ("1", "1")):
+                os.environ["MIDAGMA_EXP_EAGER"] = e
+                os.environ["MIDAGMA_EXP_COV_LA"] = la
+                print(f"MIDAGMA_EXP_EAGER={e} MIDAGMA_EXP_COV_LA={la}", end=" ")
+                cov_case(d, 2 * d, 3, 200 if d <= 2500 else 60)
+        os.environ.pop("MIDAGMA_EXP_EAGER")
+        os.environ.pop("MIDAGMA_EXP_COV_LA")
     if which == "covfork":  # large D cov mode: score GEMM beside the inverse (MIDAGMA_EXP_COV_FORK)
         ds = [int(x) for x in sys.argv[2:]] or [2000, 5000]
         for d in ds:
