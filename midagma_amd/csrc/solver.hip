@@ -203,6 +203,7 @@ struct midagma_solver {
   // cov mode at large D (the 128-tile trailing update): the score GEMM beside the inverse
   // (experiment knob MIDAGMA_EXP_COV_FORK: 1 on, 0 off)
   bool cov_fork = knob("MIDAGMA_EXP_COV_FORK", 0) != 0;
+  bool cov_fork_all = knob("MIDAGMA_EXP_COV_FORK", 0) == 2;  // 2: at every blocked D, not only large D
   // cov mode at large D, fast slots: the trailing-update look-ahead on two streams (blockinv.hip
   // blocked_inverse_lookahead; experiment knob MIDAGMA_EXP_COV_LA: 1 on, 0 off)
   bool cov_la = knob("MIDAGMA_EXP_COV_LA", 0) != 0;
@@ -219,7 +220,8 @@ struct midagma_solver {
   }
   bool cov_la_on() const { return cov_la && side != nullptr && mode == MIDAGMA_MODE_COV && blocked() && D - B2 >= 1792; }
   bool cov_fork_on() const {
-    return cov_fork && side != nullptr && mode == MIDAGMA_MODE_COV && blocked() && D - B2 >= 1792 && !trek_on;
+    return cov_fork && side != nullptr && mode == MIDAGMA_MODE_COV && blocked() && (D - B2 >= 1792 || cov_fork_all) &&
+           !trek_on;
   }
   bool data_binv = !knob_set("MIDAGMA_EXP_DATA_FLAT_GJ");
   bool data_binv_on() const { return data_binv && mode == MIDAGMA_MODE_DATA && binv_block(D) > 0; }
@@ -625,7 +627,7 @@ struct midagma_solver {
     HIP_TRY(hipHostMalloc(&h_state, 2 * sizeof(State), hipHostMallocDefault));
     for (auto& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if ((mode == MIDAGMA_MODE_DATA && fork_inv) ||
-        (mode == MIDAGMA_MODE_COV && (cov_fork || cov_la) && B2 > 0 && D - B2 >= 1792)) {
+        (mode == MIDAGMA_MODE_COV && (cov_fork || cov_la) && B2 > 0 && (D - B2 >= 1792 || cov_fork_all))) {
       // Default priority: a fork / join between a high-priority stream and another one left the
       // process's later two-stream work ~5x slower (the config-5 step after a data-mode solver:
       // 7.5k -> 1.3k steps/s, also after a plain torch fork / join; tools/probe_after_data.py),

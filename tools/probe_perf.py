@@ -160,6 +160,14 @@ if __name__ == "__main__":
                 cov_case(d, 2 * d, 3, 200 if d <= 2500 else 60)
         os.environ.pop("MIDAGMA_EXP_EAGER")
         os.environ.pop("MIDAGMA_EXP_COV_LA")
+    if which == "covforkall":  # cov mode at any blocked D: score GEMM on the main stream beside the inverse
+        ds = [int(x) for x in sys.argv[2:]] or [300, 1000, 1400, 2000]
+        for d in ds:
+            for f in ("0", "2"):
+                os.environ["MIDAGMA_EXP_COV_FORK"] = f
+                print(f"MIDAGMA_EXP_COV_FORK={f}", end=" ")
+                cov_case(d, 2 * d, 10, 2000 if d <= 1000 else (1000 if d <= 1500 else 300))
+        os.environ.pop("MIDAGMA_EXP_COV_FORK")
     if which == "covfork":  # large D cov mode: score GEMM beside the inverse (MIDAGMA_EXP_COV_FORK)
         ds = [int(x) for x in sys.argv[2:]] or [2000, 5000]
         for d in ds:
