@@ -12,7 +12,7 @@ __device__ __forceinline__ int xcd_spread(int w, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
 }
 
-// acc += A[0:32, 0:K] B[0:K, 0:32] (global operands, K <= 256), 32-deep chunks through double-
+// acc += A[0:32, 0:K] B[0:K, 0:32] (global operands, K = 32 NK), 32-deep chunks through double-
 // buffered LDS images; the register loads run PF chunks ahead of the MFMAs (the operands were
 // written by the previous launch on other XCDs: each chunk is a MALL round trip).  One barrier
 // per chunk.
@@ -67,6 +67,8 @@ __device__ __forceinline__ void tile32_gemm_any(int pf, const double* __restrict
       tile32_gemm_pf<2, 4>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
     else
       tile32_gemm_pf<1, 4>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
+  } else if (K == 512) {  // 512-wide outer blocks
+    tile32_gemm_pf<3, 16>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
   } else if (pf == 3) {
     tile32_gemm_pf<3, 8>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
   } else if (pf == 2) {

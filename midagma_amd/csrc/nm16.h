@@ -40,6 +40,21 @@ __device__ __forceinline__ double splitk_sum(const dbl4& part, double* red) {
   return ((red[tid] + red[256 + tid]) + red[512 + tid]) + red[768 + tid];
 }
 
+// The same for NW waves splitting K (NW x 256 doubles of red); NW = 4 sums in splitk_sum's
+// order.  Threads >= 256 return 0 (the tile has 256 elements); every thread passes the barrier.
+template <int NW>
+__device__ __forceinline__ double splitk_sum_w(const dbl4& part, double* red) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) red[w * 256 + t * 64 + lane] = part[t];
+  __syncthreads();
+  if (tid >= 256) return 0.0;
+  double s = red[tid];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) s += red[k * 256 + tid];
+  return s;
+}
+
 __device__ __forceinline__ void tile_elem(int e, int& row, int& col) {
   const int t = e >> 6, lane = e & 63;
   row = acc_row(lane, t);
@@ -52,6 +67,18 @@ __device__ __forceinline__ float block_max(float v, float* red4) {
   if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
   __syncthreads();
   return fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
+}
+// the same over NW waves (redn: NW floats)
+template <int NW>
+__device__ __forceinline__ float block_max_w(float v, float* redn) {
+  if (NW == 4) return block_max(v, redn);
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) redn[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float m = redn[0];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) m = fmaxf(m, redn[k]);
+  return m;
 }
 
 __device__ __forceinline__ double abs_or_inf(double v) { return isfinite(v) ? fabs(v) : INFINITY; }
@@ -81,25 +108,29 @@ __device__ __forceinline__ double row_sum16(double a) {
 // ||Q||_inf from the row partials (row r's NT = B2 / 16 tile partials at rowpart[r NT + t]),
 // one row per thread (B2 = 512: two); load(i) returns rowpart[i].  Non-finite propagates as
 // inf/nan; widened by 1e-6 against the float max.
-template <int B2, class Load>
+template <int B2, int NTH = NTHREADS, class Load>
 __device__ __forceinline__ double inf_norm_rows(Load&& load, float* red4) {
   constexpr int NT = B2 / 16;
-  constexpr int RPT = B2 > NTHREADS ? B2 / NTHREADS : 1;  // rows per thread
+  constexpr int RPT = B2 > NTH ? B2 / NTH : 1;  // rows per thread
   float f = 0.0f;
 #pragma unroll
   for (int h = 0; h < RPT; ++h) {
-    const int row = (int)threadIdx.x + h * NTHREADS;
+    const int row = (int)threadIdx.x + h * NTH;
     double r = 0.0;
     if (row < B2) {
-      double v[NT];  // all loads in flight before the (ordered) sum
+      constexpr int CH = NT < 16 ? NT : 16;  // loads in flight per chunk (registers)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) v[t] = load(row * NT + t);
+      for (int c0 = 0; c0 < NT; c0 += CH) {
+        double v[CH];  // a chunk's loads in flight before its (ordered) sum
 #pragma unroll
-      for (int t = 0; t < NT; ++t) r += v[t];
+        for (int t = 0; t < CH; ++t) v[t] = load(row * NT + c0 + t);
+#pragma unroll
+        for (int t = 0; t < CH; ++t) r += v[t];
+      }
     }
     f = fmaxf(f, isfinite(r) ? (float)(r * (1.0 + 1e-6)) : INFINITY);
   }
-  return (double)block_max(f, red4);
+  return (double)block_max_w<NTH / 64>(f, red4);
 }
 
 }  // namespace midagma

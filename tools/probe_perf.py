@@ -162,12 +162,21 @@ if __name__ == "__main__":
         os.environ.pop("MIDAGMA_EXP_COV_LA")
     if which == "covforkall":  # cov mode at any blocked D: score GEMM on the main stream beside the inverse
         ds = [int(x) for x in sys.argv[2:]] or [300, 1000, 1400, 2000]
+        splits = os.environ.pop("PROBE_SPLITS", "").split(",") if os.environ.get("PROBE_SPLITS") else [None]
         for d in ds:
             for f in ("0", "2"):
-                os.environ["MIDAGMA_EXP_COV_FORK"] = f
-                print(f"MIDAGMA_EXP_COV_FORK={f}", end=" ")
-                cov_case(d, 2 * d, 10, 2000 if d <= 1000 else (1000 if d <= 1500 else 300))
+                for sp in (splits if f == "2" else [None]):
+                    os.environ["MIDAGMA_EXP_COV_FORK"] = f
+                    if sp:
+                        os.environ["MIDAGMA_EXP_COV_SPLIT"] = sp
+                    print(f"MIDAGMA_EXP_COV_FORK={f} split={sp}", end=" ")
+                    cov_case(d, 2 * d, 10, 2000 if d <= 1000 else (1000 if d <= 1500 else 300))
+                    os.environ.pop("MIDAGMA_EXP_COV_SPLIT", None)
         os.environ.pop("MIDAGMA_EXP_COV_FORK")
+    if which == "b2_512":  # cov mode: 512-wide outer blocks where 512 divides D (run with MIDAGMA_EXP_B2_512=0 / 1)
+        for d in [int(x) for x in sys.argv[2:]] or [1000, 2000]:
+            print(f"MIDAGMA_EXP_B2_512={os.environ.get('MIDAGMA_EXP_B2_512', '0')}", end=" ")
+            cov_case(d, 2 * d, 10, 2000 if d <= 1000 else 300)
     if which == "covfork":  # large D cov mode: score GEMM beside the inverse (MIDAGMA_EXP_COV_FORK)
         ds = [int(x) for x in sys.argv[2:]] or [2000, 5000]
         for d in ds:
