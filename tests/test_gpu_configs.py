@@ -11,6 +11,8 @@
   steps against the CPU oracle (oracle/mlp_oracle.py, pinned to the reference's own
   trajectories in tests/test_mlp_oracle.py).
 Config 1 (d=20) and config 4 (d=1000, n=1e6) are covered in test_gpu_parity.py."""
+import os
+
 import numpy as np
 import pytest
 
@@ -188,3 +190,21 @@ def test_config5_ldfast_path_matches_oracle(parity):
     assert dev <= 1e-9
     for k in KEYS:
         assert np.abs(out[False][k] - out[True][k]).max() <= 1e-12 * max(1.0, np.abs(out[True][k]).max()), k
+
+
+def test_config5_rate_after_a_data_mode_solver():
+    """Regression: a fork / join across a high-priority stream (the data-mode solver's forked
+    inverse had one until round 3) left every later two-stream workload of the process ~5x
+    slower: the config-5 step fell from ~7.5k to 1.3-2.2k steps/s when the MLP ran after a
+    config-4 solver in one process.  In a fresh process: a data-mode solver
+    (run and closed), then the bench's config-5 leg; its timed rate must stay near a fresh
+    process's (healthy 6.7-7.6k across boxes, degraded 1.3-2.2k)."""
+    import re
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "probe_after_data.py"), "solver_small"],
+                       capture_output=True, text=True, timeout=240)
+    m = re.search(r"config5 leg: (\d+) steps/s", r.stdout)
+    assert r.returncode == 0 and m, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert int(m.group(1)) >= 3000, r.stdout
