@@ -563,7 +563,7 @@ def test_mlp_h_func(hip, golden, d, s):
 @pytest.mark.parametrize("d,n", [(300, 2000), (1000, 4000), (300, 20000)])
 def test_data_mode_shard_inverse_paths(hip, d, n):
     """Data-mode shards of <= 16384 rows run the cov-mode slot structure (the warm-started fast
-    blocked inverse in sequence with the GEMMs; pivoted slots at the first step, checkpoints and
+    blocked inverse, forked beside the GEMMs; pivoted slots at the first step, checkpoints and
     hand-backs); larger shards fork the pivoted blocked inverse beside the GEMMs (n=20000).  l2
     against the oracle's reference-algorithm steps (K=130, checkpoints every 40: iterations, W
     and the checkpoint objectives)."""

@@ -177,6 +177,15 @@ if __name__ == "__main__":
         for d in [int(x) for x in sys.argv[2:]] or [1000, 2000]:
             print(f"MIDAGMA_EXP_B2_512={os.environ.get('MIDAGMA_EXP_B2_512', '0')}", end=" ")
             cov_case(d, 2 * d, 10, 2000 if d <= 1000 else 300)
+    if which == "smallshard":  # logistic / l2 data mode at n = 1e4: the in-sequence fast inverse or the fork
+        for loss in ("logistic", "l2"):
+            for rows, ff in (("16384", "0"), ("0", "0"), ("16384", "1")):
+                os.environ["MIDAGMA_EXP_DATA_FAST_ROWS"] = rows
+                os.environ["MIDAGMA_EXP_DATA_FORK_FAST"] = ff
+                print(f"MIDAGMA_EXP_DATA_FAST_ROWS={rows} FORK_FAST={ff}", end=" ")
+                data_case(1000, 10000, 5, 200, loss)
+        os.environ.pop("MIDAGMA_EXP_DATA_FAST_ROWS")
+        os.environ.pop("MIDAGMA_EXP_DATA_FORK_FAST")
     if which == "covfork":  # large D cov mode: score GEMM beside the inverse (MIDAGMA_EXP_COV_FORK)
         ds = [int(x) for x in sys.argv[2:]] or [2000, 5000]
         for d in ds:
