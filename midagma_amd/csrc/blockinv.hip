@@ -102,6 +102,20 @@ struct TrailLA {  // trailing-launch extra tiles
   int gn;
 };
 
+// Tile of workgroup wg in a series launch over an nt x nt grid of 16 x 16 tiles.  xmap (256-wide
+// blocks, nt = 16): the 32 workgroups the dispatcher puts on one XCD (wg, wg + 8, ...) take a
+// 4 x 8 block of tiles, so that XCD's L2 serves 4 row bands and 8 column bands of the operands
+// instead of all 16 row bands (row-major order: every XCD read the whole of Y and Q)
+__device__ __forceinline__ void nm_tile(int wg, int nt, int xmap, int& m0, int& n0) {
+  int t = wg;
+  if (xmap && nt == 16) {
+    const int x = wg & 7, l = wg >> 3;
+    t = (4 * (x >> 1) + (l >> 3)) * 16 + 8 * (x & 1) + (l & 7);
+  }
+  m0 = (t / nt) * 16;
+  n0 = (t % nt) * 16;
+}
+
 // X0 = the warm start of this block: with two consecutive stored slots (st->warm_run >= 2)
 // the linear extrapolation 2 P1 - P2 of the last two inverses (P1 = slot k-1's, P2 = slot
 // k-2's, by the parity of k = st->slots), else P1.  Adam moves W smoothly (beta1 = 0.99), so
@@ -116,7 +130,8 @@ __global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restr
                                                            const double* __restrict__ Pe,
                                                            const double* __restrict__ Po, double* __restrict__ Y0,
                                                            double* __restrict__ Q0, double* __restrict__ part0,
-                                                           int* __restrict__ done, State* __restrict__ st) {
+                                                           int* __restrict__ done, State* __restrict__ st,
+                                                           int xmap) {
   if (st->status != ST_RUNNING) return;
   if (st->ckpt_pending) {  // a log-det is due: pivots come from the slow path only
     if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
@@ -125,7 +140,8 @@ __global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restr
   constexpr int B2 = 4 * NW * L;
   __shared__ double red[NW * 256];
   const int nt = B2 / 16, wg = blockIdx.x;
-  const int m0 = (wg / nt) * 16, n0 = (wg % nt) * 16;
+  int m0, n0;
+  nm_tile(wg, nt, xmap, m0, n0);
   if (wg == 0 && threadIdx.x == 0) *done = 0;
   const bool odd = (st->slots & 1) != 0;
   const double* P1 = odd ? Pe : Po;  // slot k-1
@@ -164,7 +180,7 @@ __global__ __launch_bounds__(64 * NW) void nm_pass_kernel(const double* __restri
                                                           double* __restrict__ Qn, double* __restrict__ P,
                                                           const double* __restrict__ part_prev,
                                                           double* __restrict__ part_next, int* __restrict__ done,
-                                                          int pass, State* __restrict__ st, NmLA la) {
+                                                          int pass, State* __restrict__ st, NmLA la, int xmap) {
   if (st->status != ST_RUNNING) return;
   constexpr int B2 = 4 * NW * L;
   __shared__ double red[NW * 256];
@@ -190,7 +206,8 @@ __global__ __launch_bounds__(64 * NW) void nm_pass_kernel(const double* __restri
   const int dn = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (dn != 0 && dn < pass) return;
   const int wg = blockIdx.x;
-  const int m0 = (wg / nt) * 16, n0 = (wg % nt) * 16;
+  int m0, n0;
+  nm_tile(wg, nt, xmap, m0, n0);
   // operands first: their latency overlaps the rho reduction (Y, Q are complete: the
   // previous launch wrote them)
   double aY[L], aQ[L], bQ[L];
@@ -709,6 +726,12 @@ static void launch_neumann5(double* Ain, int64_t D, int64_t G0, const BInvWork& 
 
 #endif
 
+// series tiles XCD-blocked (nm_tile; experiment knob MIDAGMA_EXP_NM_XCD=0: row-major)
+static int nm_xmap() {
+  static const int x = knob("MIDAGMA_EXP_NM_XCD", 1) != 0 ? 1 : 0;
+  return x;
+}
+
 template <int L, int NW = 4>
 static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& bw, int g, State* st, int passes,
                            bool resid, const NmLA* la, hipStream_t stream) {
@@ -720,7 +743,7 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
   double* part = bw.part + (int64_t)g * (NM_PASSES + 1) * PART_STRIDE;  // per block: kept for diagnostics
   if (resid)  // else the previous block's launches left X0, R and its row partials (look-ahead)
     hipLaunchKernelGGL((nm_resid_kernel<L, NW>), dim3(nwg), dim3(64 * NW), 0, stream, Ain + G0 * D + G0, D, Pe, Po,
-                       bw.Y[0], bw.Q[0], part, done, st);
+                       bw.Y[0], bw.Q[0], part, done, st, nm_xmap());
   const NmLA none{};
   for (int p = 1; p <= passes && p <= NM_PASSES; ++p) {
     const double* Y = bw.Y[(p - 1) & 1];  // pass 1: X0 from nm_resid (or the look-ahead)
@@ -729,7 +752,7 @@ static void launch_neumann(double* Ain, int64_t D, int64_t G0, const BInvWork& b
     const bool ext = la != nullptr && p <= 2;
     hipLaunchKernelGGL((nm_pass_kernel<L, NW>), dim3(ext ? 2 * nwg : nwg), dim3(64 * NW), 0, stream, Y,
                        bw.Q[(p - 1) & 1], bw.Y[p & 1], bw.Q[p & 1], bw.P, part + (p - 1) * PART_STRIDE,
-                       part + p * PART_STRIDE, done, p, st, ext ? la[p - 1] : none);
+                       part + p * PART_STRIDE, done, p, st, ext ? la[p - 1] : none, nm_xmap());
   }
 }
 
@@ -753,7 +776,7 @@ void launch_series_pass(int B2, const SeriesWork& w, State* st, int p, hipStream
     const int nwg = (B2 / 16) * (B2 / 16);
     hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, w.Y[(p - 1) & 1], w.Q[(p - 1) & 1],
                        w.Y[p & 1], w.Q[p & 1], w.P, w.part + (p - 1) * PART_STRIDE, w.part + p * PART_STRIDE, w.done,
-                       p, st, none);
+                       p, st, none, nm_xmap());
   });
   HIP_TRY(hipGetLastError());
 }
@@ -764,7 +787,7 @@ void launch_series(const double* S, int64_t lds, int B2, const SeriesWork& w, St
     constexpr int L = decltype(Lc)::value;
     const int nwg = (B2 / 16) * (B2 / 16);
     hipLaunchKernelGGL(nm_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, S, lds, w.Pe, w.Po, w.Y[0], w.Q[0],
-                       w.part, w.done, st);
+                       w.part, w.done, st, nm_xmap());
   });
   HIP_TRY(hipGetLastError());
   for (int p = 1; p <= passes; ++p) launch_series_pass(B2, w, st, p, stream);

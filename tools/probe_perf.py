@@ -173,6 +173,9 @@ if __name__ == "__main__":
                     cov_case(d, 2 * d, 10, 2000 if d <= 1000 else (1000 if d <= 1500 else 300))
                     os.environ.pop("MIDAGMA_EXP_COV_SPLIT", None)
         os.environ.pop("MIDAGMA_EXP_COV_FORK")
+    if which == "covds":  # cov mode at the given d (knobs read once per process: set them in the environment)
+        for d in [int(x) for x in sys.argv[2:]] or [1000]:
+            cov_case(d, 10 * d, 200, 4000 if d <= 1000 else (1000 if d <= 2000 else 100))
     if which == "b2_512":  # cov mode: 512-wide outer blocks where 512 divides D (run with MIDAGMA_EXP_B2_512=0 / 1)
         for d in [int(x) for x in sys.argv[2:]] or [1000, 2000]:
             print(f"MIDAGMA_EXP_B2_512={os.environ.get('MIDAGMA_EXP_B2_512', '0')}", end=" ")
