@@ -9,8 +9,11 @@
 // forward and backward.  Every Z access is coalesced (consecutive threads on consecutive
 // columns c = j m1 + m); sums over rows run in a fixed order (deterministic).
 #include <algorithm>
+#include <stdexcept>
+#include <utility>
 
 #include "launch.h"
+#include "mfma64.h"
 
 namespace midagma {
 namespace {
@@ -276,6 +279,32 @@ __global__ __launch_bounds__(NTHREADS) void fc1_terms_bwd_kernel(const double* _
   }
 }
 
+// fc1_terms_bwd_kernel's arithmetic with a thread per element of dW1 (c = j m1 + m, i): the
+// linear layer's nlin split-K slices are read in parallel by d m1 d threads instead of in a loop
+// over m by d d threads (config 5: 8 slices of 3.2 MB, 25 -> ~7 us)
+__global__ __launch_bounds__(NTHREADS) void fc1_terms_bwd_elem_kernel(const double* __restrict__ W1, int64_t d, int m1,
+                                                                      const double* __restrict__ gA,
+                                                                      const double* __restrict__ gscale,
+                                                                      const double* __restrict__ gl1,
+                                                                      const double* __restrict__ lin, int nlin,
+                                                                      double* __restrict__ dW1, const double* gobj,
+                                                                      double mu, double lambda1) {
+  const int64_t e = (int64_t)blockIdx.x * NTHREADS + threadIdx.x, dd = d * m1 * d;
+  if (e >= dd) return;
+  const int64_t c = e / d, i = e % d, j = c / m1;
+  const double ga = gobj ? gobj[0] * gA[i * d + j] : (gscale ? gscale[0] * gA[i * d + j] : gA[i * d + j]);
+  const double gl = gobj ? (gobj[0] * mu) * lambda1 : gl1[(j * d + i) / NTHREADS];
+  const double w = W1[e];
+  const double sg = w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : 0.0);
+  double v = ga * (2.0 * w) + gl * sg;
+  if (nlin > 0) {
+    double a = lin[e];
+    for (int q = 1; q < nlin; ++q) a += lin[q * dd + e];
+    v = a + v;
+  }
+  dW1[e] = v;
+}
+
 // the log-det's epilogue in one launch: Mt (d x d, ldm) from the D x D workspace, and
 // workgroup 0: h = -(sum of the pivot logs) + d log s (the reference's h_func, nonlinear.py:85-86)
 __global__ __launch_bounds__(NTHREADS) void logdet_post_kernel(const double* __restrict__ piv, int64_t d, double dls,
@@ -356,8 +385,14 @@ void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1
 void launch_fc1_terms_bwd(const double* W1, int64_t d, int m1, const double* gA, const double* gscale,
                           const double* gl1part, const double* lin, int nlin, double* dW1, hipStream_t stream,
                           const double* gobj, double mu, double lambda1) {
-  hipLaunchKernelGGL(fc1_terms_bwd_kernel, dim3((unsigned)fc1_terms_parts(d)), dim3(NTHREADS), 0, stream, W1, d, m1,
-                     gA, gscale, gl1part, lin, nlin, dW1, gobj, mu, lambda1);
+  if (nlin > 1) {
+    const int64_t dd = d * m1 * d;
+    hipLaunchKernelGGL(fc1_terms_bwd_elem_kernel, dim3((unsigned)((dd + NTHREADS - 1) / NTHREADS)), dim3(NTHREADS), 0,
+                       stream, W1, d, m1, gA, gscale, gl1part, lin, nlin, dW1, gobj, mu, lambda1);
+  } else {
+    hipLaunchKernelGGL(fc1_terms_bwd_kernel, dim3((unsigned)fc1_terms_parts(d)), dim3(NTHREADS), 0, stream, W1, d, m1,
+                       gA, gscale, gl1part, lin, nlin, dW1, gobj, mu, lambda1);
+  }
   HIP_TRY(hipGetLastError());
 }
 
@@ -513,6 +548,359 @@ void launch_ldfast_post(const double* piv, int64_t d, double dls, double* h, con
   const unsigned blocks = (unsigned)((std::max<int64_t>((int64_t)B * B, d * d) + NTHREADS - 1) / NTHREADS);
   hipLaunchKernelGGL(ldfast_post_kernel, dim3(blocks), dim3(NTHREADS), 0, stream, piv, d, dls, h, Wgj, Dgj, Mt, ldm,
                      P, B, ring0, ring1, st, gjst, hlast, exact ? 1 : 0);
+  HIP_TRY(hipGetLastError());
+}
+
+}  // namespace midagma
+
+// ---- fc1 and the tail fused on the f64 MFMA (ABI 7; BASELINE config 5) -------------------------
+// Forward: Z = X W1^T (nonlinear.py:99-100, fc1 without its bias) in 64 x TC tiles, TC = 16 NCB a
+// multiple of m1 so that no node's m1 hidden units straddle two tiles; the epilogue stores Z (the
+// backward's operand) and runs the tail forward on the tile (mlp_tail_fwd_kernel's arithmetic):
+// S w2 = sigmoid(Z + b1) w2 summed over each node's m1 units, R = (that + b2) - X, and one partial
+// of sum R^2 per workgroup.  It replaces rocBLAS's Z GEMM, the Z round trip through HBM and the
+// tail forward launch.
+// Backward: lin_z = dZ^T X over the z-th 128-row split, with dZ = 2 gs R w2 S (1 - S)
+// (mlp_tail_bwd_kernel's arithmetic) formed while the operand chunk is staged in LDS, never
+// stored; the staging threads also keep the dw2 / db2 / db1 partials of their column.  It
+// replaces the tail backward, the dZ round trip and the split-K bmm.
+namespace midagma {
+namespace {
+
+// development probe only (tools/micro/mlp_micro.hip): bit 0 skips the forward's MFMAs, bit 1 its
+// epilogue; bit 2 the backward's MFMAs; bit 4 the forward's S stores, bit 5 its node sums
+#ifndef MLP_FUSED_PROBE
+#define MLP_FUSED_PROBE 0
+#endif
+constexpr int FK = 32;      // k depth of one LDS chunk
+constexpr int FS = FK + 2;  // image row stride: 34 = 2 mod 32, conflict-free ds_read_b64 fragments
+constexpr int FBR = 128;    // rows per split of the fused backward
+constexpr int FFK = 40;     // the forward's k chunk (d = 200: five, no zero steps)
+constexpr int FFS = 66;     // its image stride (2 mod 32)
+
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int NCB>
+__global__ __launch_bounds__(NTHREADS, 2) void mlp_fc1_tail_fwd_kernel(
+    const double* __restrict__ X, const double* __restrict__ W1, const double* __restrict__ b1,
+    const double* __restrict__ w2, const double* __restrict__ b2, int64_t n, int64_t d, int m1,
+    double* __restrict__ S, double* __restrict__ R, double* __restrict__ part) {
+  constexpr int TC = 16 * NCB;
+  constexpr int NOPS = (64 + TC) * FFS, NSTG = 4 * 16 * (TC + 1);
+  // at least 56 KB: at most two workgroups per CU (three would share a SIMD's matrix pipe
+  // three ways on some CUs while others idle)
+  constexpr int NL = NOPS > NSTG ? NOPS : NSTG, NCAP = 7 * 1024;
+  __shared__ __attribute__((aligned(16))) double lds[NL > NCAP ? NL : NCAP];
+  __shared__ double red[4];
+  double* As = lds;             // [64 rows][FFS]: X
+  double* Bs = lds + 64 * FFS;  // [TC columns][FFS]: W1 (op(B) = W1^T read [n][k])
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, kq = lane >> 4;
+  const int64_t dm = d * m1, row0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * TC;
+  constexpr int XA = (64 * FFK + NTHREADS - 1) / NTHREADS, XB = (TC * FFK + NTHREADS - 1) / NTHREADS;
+  double xa[XA], xb[XB];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int it = 0; it < XA; ++it) {  // consecutive threads on consecutive k: 256-B row runs
+      const int e = it * NTHREADS + tid, rr = e / FFK, kk = e % FFK;
+      const int64_t gr = row0 + rr, gk = k0 + kk;
+      xa[it] = (rr < 64 && gr < n && gk < d) ? X[gr * d + gk] : 0.0;
+    }
+#pragma unroll
+    for (int it = 0; it < XB; ++it) {
+      const int e = it * NTHREADS + tid, cc = e / FFK, kk = e % FFK;
+      const int64_t gc = c0 + cc, gk = k0 + kk;
+      xb[it] = (cc < TC && gc < dm && gk < d) ? W1[gc * d + gk] : 0.0;
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int it = 0; it < XA; ++it) {
+      const int e = it * NTHREADS + tid;
+      if (e < 64 * FFK) As[(e / FFK) * FFS + e % FFK] = xa[it];
+    }
+#pragma unroll
+    for (int it = 0; it < XB; ++it) {
+      const int e = it * NTHREADS + tid;
+      if (e < TC * FFK) Bs[(e / FFK) * FFS + e % FFK] = xb[it];
+    }
+  };
+  dbl4 acc[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) acc[cb] = dbl4{0.0, 0.0, 0.0, 0.0};
+  // the epilogue's per-column operands, loaded up front (a load per element there left every
+  // sigmoid waiting on its own round trip)
+  double eb[NCB], ew[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int64_t gc = c0 + 16 * cb + (lane & 15);
+    eb[cb] = (gc < dm && b1) ? b1[gc] : 0.0;
+    ew[cb] = gc < dm ? w2[gc] : 0.0;
+  }
+  load(0);
+  for (int64_t k0 = 0; k0 < d; k0 += FFK) {
+    stage();
+    __syncthreads();
+    if (k0 + FFK < d) load(k0 + FFK);  // the next chunk's loads fly under this chunk's MFMAs
+    // k steps of this chunk that hold any k < d (d = 200: five full chunks of 40)
+    const int steps = (int)((d - k0 < FFK ? d - k0 : FFK) + 3) / 4;
+#pragma unroll 2
+    for (int s = 0; s < ((MLP_FUSED_PROBE & 1) ? 0 : steps); ++s) {
+      const double a = As[(16 * w + r) * FFS + 4 * s + kq];
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const double b = Bs[(16 * cb + r) * FFS + 4 * s + kq];
+        acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[cb], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  if (MLP_FUSED_PROBE & 2) {
+    double a = 0.0;
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) a += (acc[cb][0] + acc[cb][1]) + (acc[cb][2] + acc[cb][3]);
+    if (a == 12345.0) part[0] = a;
+    return;
+  }
+  // epilogue: S, then S w2 per wave through LDS (the operand images are dead)
+  double* sg = lds + w * 16 * (TC + 1);
+  const int64_t rw = row0 + 16 * w;
+  // every sigmoid first (independent chains the scheduler interleaves: two waves per SIMD do not
+  // hide one chain's latency), then the stores
+  double sv[NCB][4];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) sv[cb][t] = sigmoid(b1 ? acc[cb][t] + eb[cb] : acc[cb][t]);
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int rl = acc_row(lane, t), cl = 16 * cb + acc_col(lane);
+      const int64_t gr = rw + rl, gc = c0 + cl;
+      if (!(MLP_FUSED_PROBE & 16) && gr < n && gc < dm) S[gr * dm + gc] = sv[cb][t];
+      sg[rl * (TC + 1) + cl] = gc < dm ? sv[cb][t] * ew[cb] : 0.0;
+    }
+  __syncthreads();
+  if (MLP_FUSED_PROBE & 32) {
+    if (tid == 0) part[0] = sg[lane];
+    return;
+  }
+  const int nn = TC / m1;
+  const int64_t j0 = c0 / m1;
+  double r2 = 0.0;
+  for (int e = lane; e < 16 * nn; e += 64) {
+    const int rl = e / nn, q = e % nn;
+    const int64_t gr = rw + rl, j = j0 + q;
+    if (gr < n && j < d) {
+      double acc1 = 0.0;
+      for (int m = 0; m < m1; ++m) acc1 += sg[rl * (TC + 1) + q * m1 + m];
+      const double rv = (acc1 + b2[j]) - X[gr * d + j];
+      R[gr * d + j] = rv;
+      r2 += rv * rv;
+    }
+  }
+  r2 = wave_sum64(r2);
+  if (lane == 0) red[w] = r2;
+  __syncthreads();
+  if (tid == 0) part[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// grid (ceil(dm / 64), ceil(n / FBR)), 512 threads: wave w owns columns c0 + 16 (w & 3) + [0, 16)
+// of dZ^T and half (w >> 2) of X's NIB 16-wide column blocks (d <= 16 NIB): two waves per SIMD,
+// so one wave's LDS reads and staging overlap the other's MFMAs
+constexpr int BT = 512;
+template <int NIB>
+__global__ __launch_bounds__(BT, 1) void mlp_tail_bwd_lin_kernel(
+    const double* __restrict__ S, const double* __restrict__ w2,
+    const double* __restrict__ R, const double* __restrict__ X, int64_t n, int64_t d, int m1, ObjGrad og,
+    double* __restrict__ lin, double* __restrict__ pw, double* __restrict__ pb, double* __restrict__ pz) {
+  constexpr int NI = 16 * NIB, H0 = (NIB + 1) / 2;  // blocks of half 0; half 1 has NIB - H0
+  __shared__ __attribute__((aligned(16))) double As[64 * FS];  // [c][r]: dZ^T of the chunk
+  __shared__ __attribute__((aligned(16))) double Bs[NI * FS];  // [i][r]: X^T of the chunk
+  __shared__ double red[BT];
+  double g2;
+  {
+    double a = 0.0;
+    for (int64_t q = threadIdx.x; q < og.np; q += BT) a += og.part[q];
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int s2 = BT / 2; s2 > 0; s2 >>= 1) {
+      if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+      __syncthreads();
+    }
+    g2 = 2.0 * gssq_of(og.gobj[0], red[0], og);
+    __syncthreads();
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, kq = lane >> 4;
+  const int cb = w & 3, half = w >> 2, ib0 = half ? H0 : 0, nib = half ? NIB - H0 : H0;
+  const int64_t dm = d * m1, c0 = (int64_t)blockIdx.x * 64, rs0 = (int64_t)blockIdx.y * FBR;
+  const int64_t rs1 = rs0 + FBR < n ? rs0 + FBR : n;
+  // the staging thread's column (fixed) and rows tid / 64 + 8 q of each chunk
+  const int cc = tid & 63;
+  const int64_t gc = c0 + cc;
+  const bool cv = gc < dm;
+  const int64_t j = cv ? gc / m1 : 0;
+  const bool mz = cv && gc % m1 == 0;
+  const double wv = cv ? w2[gc] : 0.0;
+  double aw = 0.0, ab = 0.0, az = 0.0;
+  constexpr int XB = FK * NI / BT;  // X values per thread per chunk (NI / 16)
+  double rv[4], zv[4], xb[XB];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t gr = k0 + (tid >> 6) + 8 * q;
+      const bool ok = cv && gr < rs1;
+      rv[q] = ok ? R[gr * d + j] : 0.0;
+      zv[q] = ok ? S[gr * dm + gc] : 0.0;
+    }
+#pragma unroll
+    for (int it = 0; it < XB; ++it) {
+      const int e = it * BT + tid, rr = e / NI, i = e % NI;
+      const int64_t gr = k0 + rr;
+      xb[it] = (gr < rs1 && i < d) ? X[gr * d + i] : 0.0;
+    }
+  };
+  dbl4 acc[H0];
+#pragma unroll
+  for (int ib = 0; ib < H0; ++ib) acc[ib] = dbl4{0.0, 0.0, 0.0, 0.0};
+  load(rs0);
+  for (int64_t k0 = rs0; k0 < rs1; k0 += FK) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = (tid >> 6) + 8 * q;
+      double dz = 0.0;
+      if (cv && k0 + rr < rs1) {
+        const double dxh = g2 * rv[q];
+        const double sv = zv[q];
+        dz = dxh * wv * (sv * (1.0 - sv));
+        aw += dxh * sv;
+        ab += dxh;
+        az += dz;
+      }
+      As[cc * FS + rr] = dz;
+    }
+#pragma unroll
+    for (int it = 0; it < XB; ++it) {
+      const int e = it * BT + tid;
+      Bs[(e % NI) * FS + e / NI] = xb[it];
+    }
+    __syncthreads();
+    if (k0 + FK < rs1) load(k0 + FK);
+#pragma unroll
+    for (int s = 0; s < ((MLP_FUSED_PROBE & 4) ? 0 : FK / 4); ++s) {
+      const double a = As[(16 * cb + r) * FS + 4 * s + kq];
+#pragma unroll
+      for (int ib = 0; ib < H0; ++ib) {
+        if (ib < nib) {
+          const double b = Bs[(16 * (ib0 + ib) + r) * FS + 4 * s + kq];
+          acc[ib] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[ib], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  double* out = lin + (int64_t)blockIdx.y * dm * d;
+#pragma unroll
+  for (int ib = 0; ib < H0; ++ib)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int64_t c = c0 + 16 * cb + acc_row(lane, t), i = 16 * (ib0 + ib) + acc_col(lane);
+      if (ib < nib && c < dm && i < d) out[c * d + i] = acc[ib][t];
+    }
+  // the column partials of this split: the eight threads of a column in a fixed order
+  const int64_t zs = blockIdx.y;
+  double vals[3] = {aw, ab, az};
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    red[tid] = vals[f];
+    __syncthreads();
+    if (tid < 64 && cv) {
+      const double v = ((red[tid] + red[tid + 64]) + (red[tid + 128] + red[tid + 192])) +
+                       ((red[tid + 256] + red[tid + 320]) + (red[tid + 384] + red[tid + 448]));
+      if (f == 0) pw[zs * dm + gc] = v;
+      if (f == 1 && mz) pb[zs * d + j] = v;
+      if (f == 2 && pz) pz[zs * dm + gc] = v;
+    }
+    __syncthreads();
+  }
+}
+
+template <int NCB>
+void launch_fwd_ncb(const double* X, const double* W1, const double* b1, const double* w2, const double* b2,
+                    int64_t n, int64_t d, int m1, double* S, double* R, double* part, hipStream_t stream) {
+  const int64_t dm = d * m1;
+  hipLaunchKernelGGL(mlp_fc1_tail_fwd_kernel<NCB>, dim3((unsigned)((n + 63) / 64), (unsigned)((dm + 16 * NCB - 1) / (16 * NCB))),
+                     dim3(NTHREADS), 0, stream, X, W1, b1, w2, b2, n, d, m1, S, R, part);
+}
+
+template <int NIB>
+void launch_bwd_nib(const double* S, const double* w2, const double* R, const double* X, int64_t n, int64_t d, int m1,
+                    const ObjGrad& og, double* lin, double* pw, double* pb, double* pz, hipStream_t stream) {
+  const int64_t dm = d * m1;
+  hipLaunchKernelGGL(mlp_tail_bwd_lin_kernel<NIB>, dim3((unsigned)((dm + 63) / 64), (unsigned)((n + FBR - 1) / FBR)),
+                     dim3(BT), 0, stream, S, w2, R, X, n, d, m1, og, lin, pw, pb, pz);
+}
+
+template <int... I>
+void dispatch_nib(std::integer_sequence<int, I...>, int nib, const double* S, const double* w2, const double* R,
+                  const double* X, int64_t n, int64_t d, int m1, const ObjGrad& og, double* lin, double* pw,
+                  double* pb, double* pz, hipStream_t stream) {
+  ((nib == I + 1 ? (launch_bwd_nib<I + 1>(S, w2, R, X, n, d, m1, og, lin, pw, pb, pz, stream), 0) : 0), ...);
+}
+
+}  // namespace
+
+// the 16-column blocks of a forward tile for m1 hidden units: the largest NCB <= 8 with 16 NCB a
+// multiple of m1 (0: the fused path does not take this m1)
+int mlp_fused_ncb(int64_t m1) {
+  for (int ncb = 8; ncb >= 1; --ncb)
+    if ((16 * ncb) % m1 == 0) return ncb;
+  return 0;
+}
+
+int64_t mlp_fused_parts(int64_t n, int64_t d, int64_t m1) {
+  const int ncb = (n >= 1 && d >= 1 && d <= 16 * MLP_FUSED_MAX_NIB && m1 >= 1) ? mlp_fused_ncb(m1) : 0;
+  if (ncb == 0) return 0;
+  return ((n + 63) / 64) * ((d * m1 + 16 * ncb - 1) / (16 * ncb));
+}
+
+int64_t mlp_fused_splits(int64_t n) { return (n + FBR - 1) / FBR; }
+
+void launch_mlp_fc1_tail_fwd(const double* X, const double* W1, const double* b1, const double* w2, const double* b2,
+                             int64_t n, int64_t d, int m1, double* S, double* R, double* part, hipStream_t stream) {
+  switch (mlp_fused_ncb(m1)) {
+    case 1: launch_fwd_ncb<1>(X, W1, b1, w2, b2, n, d, m1, S, R, part, stream); break;
+    case 2: launch_fwd_ncb<2>(X, W1, b1, w2, b2, n, d, m1, S, R, part, stream); break;
+    case 3: launch_fwd_ncb<3>(X, W1, b1, w2, b2, n, d, m1, S, R, part, stream); break;
+    case 4: launch_fwd_ncb<4>(X, W1, b1, w2, b2, n, d, m1, S, R, part, stream); break;
+    case 5: launch_fwd_ncb<5>(X, W1, b1, w2, b2, n, d, m1, S, R, part, stream); break;
+    case 6: launch_fwd_ncb<6>(X, W1, b1, w2, b2, n, d, m1, S, R, part, stream); break;
+    case 7: launch_fwd_ncb<7>(X, W1, b1, w2, b2, n, d, m1, S, R, part, stream); break;
+    case 8: launch_fwd_ncb<8>(X, W1, b1, w2, b2, n, d, m1, S, R, part, stream); break;
+    default: throw std::invalid_argument("mlp_fc1_tail_fwd: m1 not supported by the fused path");
+  }
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_mlp_tail_bwd_lin(const double* S, const double* w2, const double* R, const double* X,
+                             const double* part, int64_t npart, const double* gobj, double mu, double half_d,
+                             double inv_n, int64_t n, int64_t d, int m1, double* lin, double* dw2, double* db2,
+                             double* db1, double* scratch, hipStream_t stream) {
+  const int64_t dm = d * m1, ns = mlp_fused_splits(n);
+  const int nib = (int)((d + 15) / 16);
+  if (nib < 1 || nib > MLP_FUSED_MAX_NIB) throw std::invalid_argument("mlp_tail_bwd_lin: d above the fused path");
+  double* pw = scratch;
+  double* pb = scratch + ns * dm;
+  double* pz = db1 ? pb + ns * d : nullptr;
+  dispatch_nib(std::make_integer_sequence<int, MLP_FUSED_MAX_NIB>{}, nib, S, w2, R, X, n, d, m1,
+               ObjGrad{part, npart, gobj, mu, half_d, inv_n}, lin, pw, pb, pz, stream);
+  const int64_t cols = dm + d + (db1 ? dm : 0);
+  hipLaunchKernelGGL(mlp_tail_dw_kernel, dim3((unsigned)((cols + NTHREADS - 1) / NTHREADS)), dim3(NTHREADS), 0,
+                     stream, pw, pb, pz, ns, d, m1, dw2, db2, db1);
   HIP_TRY(hipGetLastError());
 }
 

@@ -2004,6 +2004,35 @@ extern "C" int midagma_mlp_tail_bwd_obj(const double* Z, const double* b1, const
   });
 }
 
+extern "C" int64_t midagma_mlp_fused_parts(int64_t n, int64_t d, int64_t m1) { return mlp_fused_parts(n, d, m1); }
+
+extern "C" int64_t midagma_mlp_fused_splits(int64_t n) { return n < 1 ? 0 : mlp_fused_splits(n); }
+
+extern "C" int midagma_mlp_fc1_tail_fwd(const double* X, const double* W1, const double* b1, const double* w2,
+                                        const double* b2, int64_t n, int64_t d, int64_t m1, double* S, double* R,
+                                        double* part, void* stream) {
+  if (!X || !W1 || !w2 || !b2 || !S || !R || !part || mlp_fused_parts(n, d, m1) < 1)
+    return fail(nullptr, MIDAGMA_E_ARG, "mlp_fc1_tail_fwd: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_mlp_fc1_tail_fwd(X, W1, b1, w2, b2, n, d, (int)m1, S, R, part, reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_mlp_tail_bwd_lin(const double* S, const double* w2, const double* R, const double* X,
+                                        const double* part, int64_t npart, const double* gobj, double mu,
+                                        double half_d, double inv_n, int64_t n, int64_t d, int64_t m1, double* lin,
+                                        double* dw2, double* db2, double* db1, double* scratch, void* stream) {
+  if (!S || !w2 || !R || !X || !part || npart < 1 || !gobj || !lin || !dw2 || !db2 || !scratch ||
+      mlp_fused_parts(n, d, m1) < 1)
+    return fail(nullptr, MIDAGMA_E_ARG, "mlp_tail_bwd_lin: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_mlp_tail_bwd_lin(S, w2, R, X, part, npart, gobj, mu, half_d, inv_n, n, d, (int)m1, lin, dw2, db2, db1,
+                            scratch, reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
 extern "C" int midagma_fc1_terms_bwd_obj(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gobj,
                                          double mu, double lambda1, const double* lin, int64_t nlin, double* dW1,
                                          void* stream) {

@@ -105,6 +105,21 @@ def _vp(t):
     return C.c_void_p(t.data_ptr())
 
 
+# fc1 and the tail forward / backward fused on the MFMA (midagma_mlp_fc1_tail_fwd,
+# midagma_mlp_tail_bwd_lin; ABI 7) where the library takes the model's d and m1; False runs the
+# ABI-6 sequence (fc1 as a library GEMM, the tail kernels, the split-K dZ^T X)
+FUSED_TAIL = False
+
+
+def _tail_fwd(L, fused, X, W1, b1, w2, b2, n, d, m1, Z, R, part, st):
+    if fused:
+        _lib.check(L.midagma_mlp_fc1_tail_fwd(_vp(X), _vp(W1), _vp(b1), _vp(w2), _vp(b2), n, d, m1, _vp(Z), _vp(R),
+                                              _vp(part), st), None, "mlp_fc1_tail_fwd")
+    else:
+        _lib.check(L.midagma_mlp_tail_fwd_part(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
+                                               _vp(part), st), None, "mlp_tail_fwd_part")
+
+
 class _MLPObjective(torch.autograd.Function):
     """(h, mu * (0.5 d log(1/n sum (model(X) - X)^2) + lambda1 |fc1|_1) + h) of a [d, m1, 1]
     DagmaMLP as one autograd node (nonlinear.py:68-86, 139-159, 198-204), so that no gradient is
@@ -124,13 +139,17 @@ class _MLPObjective(torch.autograd.Function):
         stream = torch.cuda.current_stream(dev).cuda_stream
         st = C.c_void_p(stream) if stream else None
         f64 = dict(dtype=torch.float64, device=dev)
-        Z = X @ W1.t()
+        npf = int(L.midagma_mlp_fused_parts(n, d, m1)) if FUSED_TAIL else 0
+        fused = npf > 0
+        # fused: fc1's GEMM and the tail forward in one MFMA launch (midagma_mlp_fc1_tail_fwd), Z then
+        # holds sigmoid(X W1^T + b1) (what the fused backward reads), else fc1's pre-activation X W1^T
+        Z = torch.empty((n, d * m1), **f64) if fused else X @ W1.t()
         A = torch.empty((d, d), **f64)
         l1part = torch.empty(int(L.midagma_fc1_terms_parts(d)), **f64)
         Mt = torch.empty((d, d), **f64)
         h = torch.empty((), **f64)
         R = torch.empty_like(X)
-        part = torch.empty(n, **f64)  # the tail's row partials of the squared residual sum
+        part = torch.empty(npf if fused else n, **f64)  # the tail's partials of the squared residual sum
         scratch = torch.empty(int(L.midagma_mlp_tail_scratch(n, d, m1)), **f64)
         obj = torch.empty((), **f64)
         ctr = _vp(counter) if counter is not None else None
@@ -154,8 +173,7 @@ class _MLPObjective(torch.autograd.Function):
                 side.wait_event(ev_fc1)
                 chain = _SideLogdet(L, side, A, d, float(s), h, Mt, ld=ld, exact=exact)
                 chain.enqueue(1)
-                _lib.check(L.midagma_mlp_tail_fwd_part(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
-                                                       _vp(part), st), None, "mlp_tail_fwd_part")
+                _tail_fwd(L, fused, X, W1, b1, w2, b2, n, d, m1, Z, R, part, st)
                 ev_tail = torch.cuda.Event()
                 ev_tail.record(main)
                 chain.enqueue(2)
@@ -168,13 +186,13 @@ class _MLPObjective(torch.autograd.Function):
                 else:
                     _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None,
                                "logdet_h_dev")
-                _lib.check(L.midagma_mlp_tail_fwd_part(_vp(Z), _vp(b1), _vp(w2), _vp(b2), _vp(X), n, d, m1, _vp(R),
-                                                       _vp(part), st), None, "mlp_tail_fwd_part")
-                _lib.check(L.midagma_mlp_objective_part(_vp(part), n, _vp(l1part), l1part.numel(), _vp(h),
+                _tail_fwd(L, fused, X, W1, b1, w2, b2, n, d, m1, Z, R, part, st)
+                _lib.check(L.midagma_mlp_objective_part(_vp(part), part.numel(), _vp(l1part), l1part.numel(), _vp(h),
                                                         float(mu), float(lambda1), 0.5 * d, 1 / n, _vp(obj), ctr, st),
                            None, "mlp_objective_part")
         ctx.save_for_backward(X, W1, b1, w2, Z, R, Mt, part, scratch)
         ctx.consts = (n, d, m1, float(mu), float(lambda1), l1part.numel())
+        ctx.fused = fused
         ctx.set_materialize_grads(False)  # h's own gradient stays None (no zero fill and add)
         return h, obj
 
@@ -188,7 +206,6 @@ class _MLPObjective(torch.autograd.Function):
         st = C.c_void_p(stream) if stream else None
         f64 = dict(dtype=torch.float64, device=dev)
         g = torch.zeros((), **f64) if g is None else g.contiguous()
-        dZ = torch.empty_like(Z)
         dw2, db2, db1 = torch.empty_like(w2), torch.empty((d, 1), **f64), torch.empty(d * m1, **f64)
         dW1 = torch.empty_like(W1)
         chain = ctx.chain
@@ -197,18 +214,30 @@ class _MLPObjective(torch.autograd.Function):
                 chain.enqueue(2)
             # the objective's backward (d ssq, d h, d l1) is derived from g inside the tail's and the
             # fc1 terms' backward (midagma_*_obj): no launch of its own
-            _lib.check(L.midagma_mlp_tail_bwd_obj(_vp(Z), _vp(b1), _vp(w2), _vp(R), _vp(part), _vp(g), mu, 0.5 * d,
-                                                  1 / n, n, d, m1, _vp(dZ), _vp(dw2), _vp(db2), _vp(db1),
-                                                  _vp(scratch), st), None, "mlp_tail_bwd_obj")
-            if chain is not None:
-                chain.enqueue(2)
-            if n % 4 == 0 and n >= 64:
-                r = n // 4
-                lin = torch.bmm(dZ.view(4, r, -1).transpose(1, 2), X.view(4, r, -1))  # (4, d m1, d)
-                nlin = 4
+            if ctx.fused:
+                # the tail's backward and dZ^T X in one MFMA launch (dZ never stored), row-split slices
+                nlin = int(L.midagma_mlp_fused_splits(n))
+                lin = torch.empty((nlin, d * m1, d), **f64)
+                _lib.check(L.midagma_mlp_tail_bwd_lin(_vp(Z), _vp(w2), _vp(R), _vp(X), _vp(part),
+                                                      part.numel(), _vp(g), mu, 0.5 * d, 1 / n, n, d, m1, _vp(lin),
+                                                      _vp(dw2), _vp(db2), _vp(db1), _vp(scratch), st), None,
+                           "mlp_tail_bwd_lin")
+                if chain is not None:
+                    chain.enqueue(2)
             else:
-                lin = (dZ.t() @ X).contiguous()
-                nlin = 1
+                dZ = torch.empty_like(Z)
+                _lib.check(L.midagma_mlp_tail_bwd_obj(_vp(Z), _vp(b1), _vp(w2), _vp(R), _vp(part), _vp(g), mu,
+                                                      0.5 * d, 1 / n, n, d, m1, _vp(dZ), _vp(dw2), _vp(db2),
+                                                      _vp(db1), _vp(scratch), st), None, "mlp_tail_bwd_obj")
+                if chain is not None:
+                    chain.enqueue(2)
+                if n % 4 == 0 and n >= 64:
+                    r = n // 4
+                    lin = torch.bmm(dZ.view(4, r, -1).transpose(1, 2), X.view(4, r, -1))  # (4, d m1, d)
+                    nlin = 4
+                else:
+                    lin = (dZ.t() @ X).contiguous()
+                    nlin = 1
             if chain is not None:  # the rest of the chain and the objective, then join
                 torch.cuda.current_stream(dev).wait_event(chain.finish())
                 ctx.chain = None

@@ -3,6 +3,7 @@ n = 1000, with the log-det on a side stream or not (MIDAGMA_NO_OVERLAP) and with
 fast log-det or every step exact (MIDAGMA_NO_LDFAST); prints steps/s and the fast path's share.
 
     python tools/probe_mlp.py [K]
+    python tools/probe_mlp.py K fused  # fc1 and the tail fused on the MFMA (ABI 7) against the ABI-6 sequence
     python tools/probe_mlp.py K pre    # the fast variant after each of the bench's earlier legs' solvers
                                        # (cov d=1000, cov d=5000, data d=1000 n=1e5) in the same process
 """
@@ -81,6 +82,18 @@ if __name__ == "__main__":
             print(f"-- side stream created after {extra} extra streams:", flush=True)
             run(K, True, True)
             keep.append(torch.cuda.Stream())
+        sys.exit(0)
+    if len(sys.argv) > 2 and sys.argv[2] == "fused":  # fc1 + tail on the MFMA (ABI 7) or the ABI-6 sequence
+        import midagma_amd.nonlinear as nl
+        for rep in range(2):
+            for f in (True, False):
+                nl.FUSED_TAIL = f
+                print(f"-- FUSED_TAIL={f}", flush=True)
+                run(K, True, True)
+                run(K, False, True)
+        sys.exit(0)
+    if len(sys.argv) > 2 and sys.argv[2] == "serial":  # one stream (the log-det in sequence)
+        run(K, False, True)
         sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[2] == "fast":
         run(K, True, True)
