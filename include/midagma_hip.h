@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 7
+#define MIDAGMA_ABI_VERSION 6
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -267,25 +267,6 @@ int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, do
 int midagma_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R, const double* g,
                          int64_t n, int64_t d, int64_t m1, double* dZ, double* dw2, double* db2, double* db1,
                          double* scratch, void* stream);
-/* ABI 7: fc1 and the tail of a [d, m1, 1] DagmaMLP fused on the f64 matrix cores (nonlinear.py:99-104,
- * 139-159; replaces Z = X W1^T as a library GEMM, midagma_mlp_tail_fwd_part, midagma_mlp_tail_bwd_obj
- * and the split-K dZ^T X).  midagma_mlp_fused_parts(n, d, m1): the forward's partials of sum R^2
- * (0: this d / m1 is not supported: d <= 256 and a multiple of 16 up to 128 that m1 divides).
- * fc1_tail_fwd: X (n x d), W1 (d*m1 x d) -> S = sigmoid(X W1^T + b1) (n x d*m1), R = Xhat - X
- * (n x d), part[midagma_mlp_fused_parts] (what midagma_mlp_objective_part sums).
- * tail_bwd_lin: S, R from the forward, gobj = d loss / d obj -> lin (midagma_mlp_fused_splits(n)
- * slices of d*m1 x d: the row-split partial sums of dZ^T X that midagma_fc1_terms_bwd_obj adds as
- * its nlin slices), dw2, db2 and, when given, db1; scratch: midagma_mlp_tail_scratch(n, d, m1)
- * doubles.  dZ is not stored. */
-int64_t midagma_mlp_fused_parts(int64_t n, int64_t d, int64_t m1);
-int64_t midagma_mlp_fused_splits(int64_t n);
-int midagma_mlp_fc1_tail_fwd(const double* X, const double* W1, const double* b1, const double* w2, const double* b2,
-                             int64_t n, int64_t d, int64_t m1, double* S, double* R, double* part, void* stream);
-int midagma_mlp_tail_bwd_lin(const double* S, const double* w2, const double* R, const double* X, const double* part,
-                             int64_t npart, const double* gobj, double mu, double half_d, double inv_n, int64_t n,
-                             int64_t d, int64_t m1, double* lin, double* dw2, double* db2, double* db1,
-                             double* scratch, void* stream);
-
 #ifdef __cplusplus
 }
 #endif

@@ -114,11 +114,6 @@ EXPORTED = {
     "midagma_fc1_terms_bwd_obj": (_int, [_vp, _i64, _i64, _vp, _vp, _d, _d, _vp, _i64, _vp, _vp]),
     "midagma_mlp_tail_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "midagma_mlp_tail_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "midagma_mlp_fused_parts": (_i64, [_i64, _i64, _i64]),
-    "midagma_mlp_fused_splits": (_i64, [_i64]),
-    "midagma_mlp_fc1_tail_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
-    "midagma_mlp_tail_bwd_lin": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _i64, _i64, _i64, _vp, _vp,
-                                        _vp, _vp, _vp, _vp]),
 }
 
 _lock = threading.Lock()

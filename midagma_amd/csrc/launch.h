@@ -220,7 +220,8 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
 
 // --- mlp.hip ----------------------------------------------------------------
 constexpr int64_t MLP_TAIL_MAX_DM = 7936;  // d * m1 the fused DagmaMLP tail stages per row in LDS
-// fc1 and the tail fused on the MFMA (ABI 7): d <= 16 MLP_FUSED_MAX_NIB, m1 with a multiple of 16 up to
+#ifdef MIDAGMA_EXPERIMENTS
+// fc1 and the tail fused on the MFMA (experiments build; measured slower): d <= 16 MLP_FUSED_MAX_NIB, m1 with a multiple of 16 up to
 // 128 that m1 divides; mlp_fused_parts = the forward's partials of sum R^2 (0: not supported)
 constexpr int MLP_FUSED_MAX_NIB = 16;
 int mlp_fused_ncb(int64_t m1);
@@ -232,6 +233,7 @@ void launch_mlp_tail_bwd_lin(const double* S, const double* w2, const double* R,
                              const double* part, int64_t npart, const double* gobj, double mu, double half_d,
                              double inv_n, int64_t n, int64_t d, int m1, double* lin, double* dw2, double* db2,
                              double* db1, double* scratch, hipStream_t stream);
+#endif
 // doubles of scratch the tail needs (both directions)
 int64_t mlp_tail_scratch(int64_t n, int64_t d, int64_t m1);
 // Z (n x d*m1) -> R = Xhat - X (n x d), *ssq = sum R^2

@@ -553,13 +553,17 @@ void launch_ldfast_post(const double* piv, int64_t d, double dls, double* h, con
 
 }  // namespace midagma
 
-// ---- fc1 and the tail fused on the f64 MFMA (ABI 7; BASELINE config 5) -------------------------
+#ifdef MIDAGMA_EXPERIMENTS
+// ---- fc1 and the tail fused on the f64 MFMA (experiments build; BASELINE config 5) -----------
 // Forward: Z = X W1^T (nonlinear.py:99-100, fc1 without its bias) in 64 x TC tiles, TC = 16 NCB a
 // multiple of m1 so that no node's m1 hidden units straddle two tiles; the epilogue stores Z (the
 // backward's operand) and runs the tail forward on the tile (mlp_tail_fwd_kernel's arithmetic):
 // S w2 = sigmoid(Z + b1) w2 summed over each node's m1 units, R = (that + b2) - X, and one partial
 // of sum R^2 per workgroup.  It replaces rocBLAS's Z GEMM, the Z round trip through HBM and the
 // tail forward launch.
+// Measured at config 5 and rejected: 136.8 vs 139.7 us a step with the
+// log-det in sequence, but 145 vs 123 us with the log-det on its side stream, whose kernels these
+// launches' LDS / VGPR footprint keeps off the CUs.
 // Backward: lin_z = dZ^T X over the z-th 128-row split, with dZ = 2 gs R w2 S (1 - S)
 // (mlp_tail_bwd_kernel's arithmetic) formed while the operand chunk is staged in LDS, never
 // stored; the staging threads also keep the dw2 / db2 / db1 partials of their column.  It
@@ -905,3 +909,5 @@ void launch_mlp_tail_bwd_lin(const double* S, const double* w2, const double* R,
 }
 
 }  // namespace midagma
+
+#endif  // MIDAGMA_EXPERIMENTS

@@ -2004,6 +2004,9 @@ extern "C" int midagma_mlp_tail_bwd_obj(const double* Z, const double* b1, const
   });
 }
 
+#ifdef MIDAGMA_EXPERIMENTS
+// fc1 and the tail fused on the MFMA (mlp.hip; measured slower at config 5):
+// not in the public header, bound by nonlinear.py when the loaded library has them
 extern "C" int64_t midagma_mlp_fused_parts(int64_t n, int64_t d, int64_t m1) { return mlp_fused_parts(n, d, m1); }
 
 extern "C" int64_t midagma_mlp_fused_splits(int64_t n) { return n < 1 ? 0 : mlp_fused_splits(n); }
@@ -2032,6 +2035,7 @@ extern "C" int midagma_mlp_tail_bwd_lin(const double* S, const double* w2, const
     return MIDAGMA_OK;
   });
 }
+#endif
 
 extern "C" int midagma_fc1_terms_bwd_obj(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gobj,
                                          double mu, double lambda1, const double* lin, int64_t nlin, double* dW1,

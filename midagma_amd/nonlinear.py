@@ -106,9 +106,29 @@ def _vp(t):
 
 
 # fc1 and the tail forward / backward fused on the MFMA (midagma_mlp_fc1_tail_fwd,
-# midagma_mlp_tail_bwd_lin; ABI 7) where the library takes the model's d and m1; False runs the
-# ABI-6 sequence (fc1 as a library GEMM, the tail kernels, the split-K dZ^T X)
+# midagma_mlp_tail_bwd_lin: experiments build only, measured slower at config 5 beside the
+# side-stream log-det).  True takes them where the loaded library has them and
+# takes the model's d and m1; the product path runs fc1 as a library GEMM, the tail kernels and
+# the split-K dZ^T X.
 FUSED_TAIL = False
+
+
+def _fused_parts(L, n, d, m1) -> int:
+    """The fused forward's partial count (0: not taken), binding the experiment entries once."""
+    if not FUSED_TAIL or not hasattr(L, "midagma_mlp_fused_parts"):
+        return 0
+    if not getattr(L, "_fused_bound", False):
+        vp, i64, dd = C.c_void_p, C.c_int64, C.c_double
+        for name, res, args in (
+                ("midagma_mlp_fused_parts", i64, [i64, i64, i64]),
+                ("midagma_mlp_fused_splits", i64, [i64]),
+                ("midagma_mlp_fc1_tail_fwd", C.c_int, [vp, vp, vp, vp, vp, i64, i64, i64, vp, vp, vp, vp]),
+                ("midagma_mlp_tail_bwd_lin", C.c_int, [vp, vp, vp, vp, vp, i64, vp, dd, dd, dd, i64, i64, i64, vp,
+                                                       vp, vp, vp, vp, vp])):
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        L._fused_bound = True
+    return int(L.midagma_mlp_fused_parts(n, d, m1))
 
 
 def _tail_fwd(L, fused, X, W1, b1, w2, b2, n, d, m1, Z, R, part, st):
@@ -139,7 +159,7 @@ class _MLPObjective(torch.autograd.Function):
         stream = torch.cuda.current_stream(dev).cuda_stream
         st = C.c_void_p(stream) if stream else None
         f64 = dict(dtype=torch.float64, device=dev)
-        npf = int(L.midagma_mlp_fused_parts(n, d, m1)) if FUSED_TAIL else 0
+        npf = _fused_parts(L, n, d, m1)
         fused = npf > 0
         # fused: fc1's GEMM and the tail forward in one MFMA launch (midagma_mlp_fc1_tail_fwd), Z then
         # holds sigmoid(X W1^T + b1) (what the fused backward reads), else fc1's pre-activation X W1^T

@@ -1,7 +1,7 @@
 // Development micro-benchmark (not part of the library): the fused DagmaMLP fc1 + tail forward
 // and backward (csrc/mlp.hip, ABI 7) at config 5's shape (n = 1000, d = 200, m1 = 10), hipEvent-
 // timed, with parts switched off by MLP_FUSED_PROBE (see mlp.hip) to locate the time.
-//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I../../midagma_amd/csrc
+//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DMIDAGMA_EXPERIMENTS -I../../midagma_amd/csrc
 //          -DMLP_FUSED_PROBE=<bits> mlp_micro.hip -o mlp_micro_<bits>
 #include <hip/hip_runtime.h>
 
