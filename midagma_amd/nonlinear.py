@@ -111,6 +111,9 @@ def _vp(t):
 # takes the model's d and m1; the product path runs fc1 as a library GEMM, the tail kernels and
 # the split-K dZ^T X.
 FUSED_TAIL = False
+# split-K count of the weight gradient dZ^T X (a batched library GEMM whose slices the fc1 terms'
+# backward sums per element)
+LIN_SPLIT = 4
 
 
 def _fused_parts(L, n, d, m1) -> int:
@@ -251,10 +254,11 @@ class _MLPObjective(torch.autograd.Function):
                                                       _vp(db1), _vp(scratch), st), None, "mlp_tail_bwd_obj")
                 if chain is not None:
                     chain.enqueue(2)
-                if n % 4 == 0 and n >= 64:
-                    r = n // 4
-                    lin = torch.bmm(dZ.view(4, r, -1).transpose(1, 2), X.view(4, r, -1))  # (4, d m1, d)
-                    nlin = 4
+                ks = LIN_SPLIT
+                if n % ks == 0 and n >= 16 * ks:
+                    r = n // ks
+                    lin = torch.bmm(dZ.view(ks, r, -1).transpose(1, 2), X.view(ks, r, -1))  # (ks, d m1, d)
+                    nlin = ks
                 else:
                     lin = (dZ.t() @ X).contiguous()
                     nlin = 1

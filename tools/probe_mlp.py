@@ -92,6 +92,14 @@ if __name__ == "__main__":
                 run(K, True, True)
                 run(K, False, True)
         sys.exit(0)
+    if len(sys.argv) > 2 and sys.argv[2] == "linsplit":  # split-K count of dZ^T X
+        import midagma_amd.nonlinear as nl
+        for rep in range(2):
+            for ks in (4, 8, 2):
+                nl.LIN_SPLIT = ks
+                print(f"-- LIN_SPLIT={ks}", flush=True)
+                run(K, True, True)
+        sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[2] == "serial":  # one stream (the log-det in sequence)
         run(K, False, True)
         sys.exit(0)
