@@ -121,7 +121,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
   const int per_slice = tiles_m * tiles_n;
   const int z = t / per_slice, rem = t % per_slice;
   int bm = rem / tiles_n, bn = rem % tiles_n;
-  if (EPI == EPI_SUB_BAND || EPI == EPI_SUB_PRE) {
+  if (EPI == EPI_SUB_BAND || EPI == EPI_SUB_PRE || EPI == EPI_SUB_MID) {
     // trailing update of the blocked inverse: the tile grid skips the pivot band
     // [m_valid, m_valid + n_valid) (in 128-tiles) in both rows and columns
     bm += bm >= (int)m_valid ? (int)n_valid : 0;
@@ -365,7 +365,7 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
     bm = rem / tiles_n;
     bn = rem % tiles_n;
   }
-  if (EPI == EPI_SUB_BAND || EPI == EPI_SUB_PRE) {
+  if (EPI == EPI_SUB_BAND || EPI == EPI_SUB_PRE || EPI == EPI_SUB_MID) {
     // trailing update of the blocked inverse: the tile grid skips the pivot band
     // [m_valid, m_valid + n_valid) (in 128-tiles) in both rows and columns
     bm += bm >= (int)m_valid ? (int)n_valid : 0;
@@ -492,10 +492,63 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
     __syncthreads();
     GP_FRAG(fa0, As0, 0)
   }
+  // EPI_SUB_MID (K = 256 exactly, 16 K-tiles): C0 is read in 16 half-blocks (8 rows x 16
+  // columns of each of a lane's two accumulator columns) over the 16 K-tiles, each loaded one K-tile ahead of its fold
+  // acc -= C0 (8 extra VGPRs), so the C0 traffic overlaps the MFMAs instead of the epilogue's
+  // burst of every resident tile at once; acc ends as A B - C0 and is stored negated
+  const int nit = EPI == EPI_SUB_MID ? 16 : (int)((k_end - k_begin + 15) / 16);
+  const double* C0m = loss_part;
+  double2 c0r[2];
+  // (addresses: a wave-uniform row base (SGPRs) plus one per-lane 32-bit offset, so the 32 loads
+  // of the unrolled loop hold no 64-bit address registers)
+  const int64_t nwu = n0 + 32 * __builtin_amdgcn_readfirstlane(w);
+  const int c0lane = acc_row(lane, 0) * (int)ldc + 2 * acc_col(lane);
+  const int c0dt = acc_row(lane, 1) - acc_row(lane, 0);  // row step of accumulator element tt
+#define GP_C0LOAD(H)                                                                              \
+  {                                                                                               \
+    _Pragma("unroll") for (int u_ = 0; u_ < 2; ++u_) c0r[u_] = *reinterpret_cast<const double2*>(  \
+        C0m + ((m0 + 16 * ((H) >> 1) + c0dt * (2 * ((H) & 1) + u_)) * ldc + nwu) + c0lane);       \
+  }
+#define GP_C0FOLD(H)                                                                              \
+  {                                                                                               \
+    _Pragma("unroll") for (int u_ = 0; u_ < 2; ++u_) {                                            \
+      acc[(H) >> 1][0][2 * ((H) & 1) + u_] -= c0r[u_].x;                                          \
+      acc[(H) >> 1][1][2 * ((H) & 1) + u_] -= c0r[u_].y;                                          \
+    }                                                                                             \
+  }
+  // (the MID loop is unrolled over its fixed 16 K-tiles, so every fold and load index is a
+  // constant and acc stays in registers; a run-time switch over the folds spilled it)
+  constexpr int kUnroll = EPI == EPI_SUB_MID ? 16 : 1;
+  const int nit_loop = EPI == EPI_SUB_MID ? 16 : nit;
   __builtin_amdgcn_s_setprio(3);
-  for (int64_t kt = k_begin; kt < k_end; kt += 16) {
+#pragma unroll kUnroll
+  for (int it = 0; it < nit_loop; ++it) {
+    const int64_t kt = k_begin + 16 * (int64_t)it;
     const int64_t k1 = kt + 16 < k_end ? kt + 16 : kt;
     const int64_t k2 = kt + 32 < k_end ? kt + 32 : k1;
+    if (EPI == EPI_SUB_MID) {
+      const int h = it - (nit - 16) - 1;  // half-block folded in this K-tile (15: after the loop)
+      switch (h) {
+        case 0: GP_C0FOLD(0) break;
+        case 1: GP_C0FOLD(1) break;
+        case 2: GP_C0FOLD(2) break;
+        case 3: GP_C0FOLD(3) break;
+        case 4: GP_C0FOLD(4) break;
+        case 5: GP_C0FOLD(5) break;
+        case 6: GP_C0FOLD(6) break;
+        case 7: GP_C0FOLD(7) break;
+        case 8: GP_C0FOLD(8) break;
+        case 9: GP_C0FOLD(9) break;
+        case 10: GP_C0FOLD(10) break;
+        case 11: GP_C0FOLD(11) break;
+        case 12: GP_C0FOLD(12) break;
+        case 13: GP_C0FOLD(13) break;
+        case 14: GP_C0FOLD(14) break;
+        default: break;
+      }
+      if (h >= -1 && h < 15) GP_C0LOAD(h + 1)
+      __builtin_amdgcn_sched_barrier(0);
+    }
     GP_FRAG(fa1, As0, 1)  // k-step 0
     GP_MMA(fa0, kt, 0)
     GP_LOADB1(k1, 0)
@@ -533,6 +586,25 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
 #undef GP_FRAG
 #undef GP_MMA
 #undef GP_SCHED
+  if (EPI == EPI_SUB_MID) {  // acc = A B - C0 once the last half-block is folded; slice_stride = check
+    GP_C0FOLD(15)
+    int flag = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int64_t row = m0 + 16 * i + acc_row(lane, tt);
+        const int64_t col = nw + 2 * acc_col(lane);
+        const double2 v = double2{-acc[i][0][tt], -acc[i][1][tt]};
+        *reinterpret_cast<double2*>(C + row * ldc + col) = v;
+        flag |= (v.x + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v.x) ? 0 : 2);
+        flag |= (v.y + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v.y) ? 0 : 2);
+      }
+    if (slice_stride && flag) atomicOr(const_cast<int32_t*>(&st->flags), flag);
+    return;
+  }
+#undef GP_C0LOAD
+#undef GP_C0FOLD
   if (EPI == EPI_SUB_PRE) {  // acc = C0 - A B already; slice_stride = check
     int flag = 0;
 #pragma unroll
@@ -676,11 +748,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_trail_kernel(GemmTrailArgs a
   }
 }
 
+// experiment knob MIDAGMA_EXP_TRAIL_EPI=1: C0 read in the epilogue at every B2
+// (the 128-tile trailing updates; B2 = 256 otherwise folds it in during the K loop)
+static bool trail_mid() {
+  static const bool epi = knob_set("MIDAGMA_EXP_TRAIL_EPI");
+  return !epi;
+}
+
 // The same pairing at large D, where the trailing update itself runs on the 128-tile GEMM
 // (launch_trail128): the score GEMM's tiles, then the band-skipping C0 - A B tiles.
 struct Gemm2Args {
   GemmTrailArgs g;  // the score GEMM (its trailing-update fields unused)
   int tm2;          // trailing tiles per dimension: (D - B2) / 128
+  int mid;          // B2 = 256: C0 folded in during the K loop (EPI_SUB_MID, launch_trail128)
 };
 
 template <int AMODE, int BMODE>
@@ -694,10 +774,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_trail128_kernel(Gemm2Args a2
                                             a.C, a.ldc, a.slice_stride, nullptr, 0, 0, a.st, smem);
   } else {
     const int64_t G0 = (int64_t)a.g * a.B2;
-    gemm_pipe_tile<0, B_PLAIN, EPI_SUB_BAND>(xcd_remap(b - a.n_gemm, (int)gridDim.x - a.n_gemm), a.B2, a.B2, a2.tm2,
-                                             a2.tm2, a.Ain + G0, a.D, a.Aout + G0 * a.D, a.D, a.Aout, a.D,
-                                             (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, a.B2 / 128, a.st,
-                                             smem);
+    if (a2.mid)
+      gemm_pipe_tile<0, B_PLAIN, EPI_SUB_MID>(xcd_remap(b - a.n_gemm, (int)gridDim.x - a.n_gemm), a.B2, a.B2, a2.tm2,
+                                              a2.tm2, a.Ain + G0, a.D, a.Aout + G0 * a.D, a.D, a.Aout, a.D,
+                                              (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, a.B2 / 128,
+                                              a.st, smem);
+    else
+      gemm_pipe_tile<0, B_PLAIN, EPI_SUB_BAND>(xcd_remap(b - a.n_gemm, (int)gridDim.x - a.n_gemm), a.B2, a.B2, a2.tm2,
+                                               a2.tm2, a.Ain + G0, a.D, a.Aout + G0 * a.D, a.D, a.Aout, a.D,
+                                               (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, a.B2 / 128,
+                                               a.st, smem);
   }
 }
 
@@ -891,7 +977,7 @@ void launch_gemm_trail(const GemmSpec& gs, const double* Ain, double* Aout, int6
   a.st = st;
   if (n_trail < 0) {
     if (D % 128 || B2 % 128) throw std::invalid_argument("launch_gemm_trail: D, B2 must be multiples of 128");
-    Gemm2Args a2{a, (int)((D - B2) / 128)};
+    Gemm2Args a2{a, (int)((D - B2) / 128), (B2 == 256 && trail_mid()) ? 1 : 0};
     const dim3 grid2((unsigned)(a.n_gemm + a2.tm2 * a2.tm2));
 #define MIDAGMA_GT2(AM, BM) \
   hipLaunchKernelGGL((gemm_trail128_kernel<AM, BM>), grid2, dim3(NTHREADS), kGemmPipeLds, stream, a2)
@@ -922,27 +1008,42 @@ void launch_gemm_trail(const GemmSpec& gs, const double* Ain, double* Aout, int6
   HIP_TRY(hipGetLastError());
 }
 
-void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
-                     hipStream_t stream) {
+// B2 = 256 (16 K-tiles) folds C0 in during the K loop (EPI_SUB_MID; D = 5120: 219 -> 203 us, D =
+// 3072: 77.6 -> 68.9 us, tools/micro/trail_micro.hip), other B2 read it in the epilogue
+static void launch_trail128_epi(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
+                                const State* st, hipStream_t stream, bool mid) {
   if (D % 128 || B2 % 128) throw std::invalid_argument("launch_trail128: D, B2 must be multiples of 128");
   const int tm = (int)((D - B2) / 128);
   if (tm <= 0) return;
   const int64_t G0 = g * B2;
   // A = Ain[:, G] (lda D), B = Aout[G, :] (the row panel), C = Aout, C0 = Ain; K = B2
   static const bool no_pipe = knob_set("MIDAGMA_EXP_NO_PIPE");  // experiment knob
-  if (!no_pipe)
-    hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
-                       kGemmPipeLds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
-                       (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128),
-                       st);
+  const dim3 grid((unsigned)(tm * tm));
+  const int64_t chk = check ? 1 : 0, b0 = G0 / 128, nb = B2 / 128;
+  if (!no_pipe && mid && B2 == 256)
+    hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_MID>), grid, dim3(NTHREADS), kGemmPipeLds, stream, B2,
+                       B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D, chk, const_cast<double*>(Ain), b0, nb, st);
+  else if (!no_pipe)
+    hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_BAND>), grid, dim3(NTHREADS), kGemmPipeLds, stream, B2,
+                       B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D, chk, const_cast<double*>(Ain), b0, nb, st);
   else
-    hipLaunchKernelGGL((gemm128_kernel<false, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
-                       kGemm128Lds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
-                       (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
+    hipLaunchKernelGGL((gemm128_kernel<false, B_PLAIN, EPI_SUB_BAND>), grid, dim3(NTHREADS), kGemm128Lds, stream, B2,
+                       B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D, chk, const_cast<double*>(Ain), b0, nb, st);
   HIP_TRY(hipGetLastError());
 }
 
+void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
+                     hipStream_t stream) {
+  launch_trail128_epi(Ain, Aout, D, B2, g, check, st, stream, trail_mid());
+}
+
 #ifdef MIDAGMA_EXPERIMENTS
+// launch_trail128 with C0 read in the epilogue at every B2 (the micro-benchmark's baseline)
+void launch_trail128_band(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
+                          const State* st, hipStream_t stream) {
+  launch_trail128_epi(Ain, Aout, D, B2, g, check, st, stream, false);
+}
+
 // launch_trail128 with the accumulators preloaded from C0 (EPI_SUB_PRE; experiments build only:
 // measured no faster, tools/micro/trail_micro.hip)
 void launch_trail128_pre(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,

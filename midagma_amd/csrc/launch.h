@@ -329,7 +329,8 @@ void launch_sem_slab(const SemDev& g, const std::vector<int32_t>& level_off, int
 enum GemmB : int { B_PLAIN = 0, B_IMINUS = 1 };
 enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1, EPI_SUB_BAND = 2 /* launch_trail128 only */,
                      EPI_SUB_CROSS = 3 /* launch_trail128_split only */,
-                     EPI_SUB_PRE = 4 /* EPI_SUB_BAND with C0 preloaded into the accumulators */ };
+                     EPI_SUB_PRE = 4 /* EPI_SUB_BAND with C0 preloaded into the accumulators */,
+                     EPI_SUB_MID = 5 /* EPI_SUB_BAND with C0 folded in over the last 16 k-tiles */ };
 void gemm_setup_attributes();
 // C[M x N] = op(A) * op(B); op(A) = A ([m][k], lda) or, if a_trans, A stored [k][m] (lda);
 // op(B) = B or (I - B) ([k][n], ldb).  M, N, K multiples of 64.  With split > 1
@@ -346,6 +347,10 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
 void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
                      hipStream_t stream);
 #ifdef MIDAGMA_EXPERIMENTS
+// The same update with C0 read in the epilogue at every B2 (launch_trail128 folds it in during the
+// K loop at B2 = 256; experiments build, tools/micro/trail_micro.hip)
+void launch_trail128_band(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
+                          const State* st, hipStream_t stream);
 // The same update with the accumulators preloaded from C0 (experiments build, tools/micro/trail_micro.hip)
 void launch_trail128_pre(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
                          const State* st, hipStream_t stream);

@@ -1,7 +1,8 @@
 // Development micro-benchmark (not part of the library): the blocked inverse's 128-tile trailing
-// update (launch_trail128, C = C0 - A B with C0 read in the epilogue) against the variant whose
+// update with C0 read in the epilogue (launch_trail128_band, C = C0 - A B) against the variant whose
 // accumulators start from C0 (launch_trail128_pre) and the same tile grid with no C0 at all
-// (launch_gemm EPI_STORE), hipEvent-timed.
+// (launch_gemm EPI_STORE), and C0 folded in during the K loop (launch_trail128, the library's update at B2 = 256),
+// hipEvent-timed.
 //   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DMIDAGMA_EXPERIMENTS
 //          -I../../midagma_amd/csrc trail_micro.hip ../../midagma_amd/csrc/gemm.hip -o trail_micro
 //   run  : ./trail_micro [D ...]   (default 2048 3072 5120; B2 = 256, outer step g = 1)
@@ -82,37 +83,44 @@ int main(int argc, char** argv) {
   const int64_t B2 = 256, g = 1;
   const int reps = 50;
   for (int64_t D : Ds) {
-    double *Ain, *Aout, *Aout2, *C;
+    double *Ain, *Aout, *Aout2, *Aout3, *C;
     CK(hipMalloc(&Ain, sizeof(double) * D * D));
     CK(hipMalloc(&Aout, sizeof(double) * D * D));
     CK(hipMalloc(&Aout2, sizeof(double) * D * D));
+    CK(hipMalloc(&Aout3, sizeof(double) * D * D));
     CK(hipMalloc(&C, sizeof(double) * D * D));
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, Ain, D * D, 1, 2.0);
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, Aout, D * D, 2, 2.0);
     CK(hipMemcpy(Aout2, Aout, sizeof(double) * D * D, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(Aout3, Aout, sizeof(double) * D * D, hipMemcpyDeviceToDevice));
     CK(hipDeviceSynchronize());
     const int64_t t = D - B2;
     const double f = 2.0 * t * t * B2;
-    const double us_lib = time_us([&] { launch_trail128(Ain, Aout, D, B2, g, false, nullptr, 0); }, reps);
+    const double us_lib = time_us([&] { launch_trail128_band(Ain, Aout, D, B2, g, false, nullptr, 0); }, reps);
     const double us_pre = time_us([&] { launch_trail128_pre(Ain, Aout2, D, B2, g, false, nullptr, 0); }, reps);
     CK(hipDeviceSynchronize());
+    const double us_mid = time_us([&] { launch_trail128(Ain, Aout3, D, B2, g, false, nullptr, 0); }, reps);
+    CK(hipDeviceSynchronize());
     const double rd = reldiff(Aout2, Aout, D * D);
+    const double rd_mid = reldiff(Aout3, Aout, D * D);
     const double us_st = time_us([&] {
       launch_gemm(t, t, B2, Ain, D, false, Aout, D, B_PLAIN, C, D, EPI_STORE, 1, 0, nullptr, 0, 0, nullptr, 0);
     }, reps);
     // in place (Aout = Ain: the whole matrix is one 8 D^2-byte buffer, which fits the 256 MB
     // Infinity Cache up to D ~ 5600; timing only: the column band is read while other tiles write)
-    const double us_ip = time_us([&] { launch_trail128(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
+    const double us_ip = time_us([&] { launch_trail128_band(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
     const double us_ip_pre = time_us([&] { launch_trail128_pre(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
     const int tiles = (int)((t / 128) * (t / 128));
     printf("D=%5ld tiles=%5d (%.2f rounds of 512)  lib %8.2f us %5.1f TF | pre %8.2f us %5.1f TF | "
-           "no-C0 store %8.2f us %5.1f TF | in place %8.2f / pre %8.2f us | max rel diff pre vs lib %.2e\n",
-           (long)D, tiles, tiles / 512.0, us_lib, f / us_lib / 1e6, us_pre, f / us_pre / 1e6, us_st, f / us_st / 1e6,
-           us_ip, us_ip_pre, rd);
+           "mid %8.2f us %5.1f TF | no-C0 store %8.2f us %5.1f TF | in place %8.2f / pre %8.2f us | max rel diff "
+           "pre %.2e mid %.2e vs lib\n",
+           (long)D, tiles, tiles / 512.0, us_lib, f / us_lib / 1e6, us_pre, f / us_pre / 1e6, us_mid, f / us_mid / 1e6,
+           us_st, f / us_st / 1e6, us_ip, us_ip_pre, rd, rd_mid);
     fflush(stdout);
     CK(hipFree(Ain));
     CK(hipFree(Aout));
     CK(hipFree(Aout2));
+    CK(hipFree(Aout3));
     CK(hipFree(C));
   }
   return 0;
