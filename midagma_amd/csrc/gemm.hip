@@ -337,7 +337,7 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
   const int per_slice = tiles_m * tiles_n;
   const int z = t / per_slice, rem = t % per_slice;
   int bm, bn;
-  if (EPI == EPI_SUB_CROSS) {
+  if (EPI == EPI_SUB_CROSS || EPI == EPI_SUB_CROSS_MID) {
     // look-ahead part of a trailing update (launch_trail128_split): the tiles in the row or column
     // band of the NEXT outer block, which sits right after the pivot band b = m_valid, nb =
     // n_valid tiles wide; tiles_m = the trailing grid's edge (pivot band skipped), tiles_n = 2 nb
@@ -496,7 +496,8 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
   // columns of each of a lane's two accumulator columns) over the 16 K-tiles, each loaded one K-tile ahead of its fold
   // acc -= C0 (8 extra VGPRs), so the C0 traffic overlaps the MFMAs instead of the epilogue's
   // burst of every resident tile at once; acc ends as A B - C0 and is stored negated
-  const int nit = EPI == EPI_SUB_MID ? 16 : (int)((k_end - k_begin + 15) / 16);
+  constexpr bool kFold = EPI == EPI_SUB_MID || EPI == EPI_SUB_CROSS_MID;
+  const int nit = kFold ? 16 : (int)((k_end - k_begin + 15) / 16);
   const double* C0m = loss_part;
   double2 c0r[2];
   // (addresses: a wave-uniform row base (SGPRs) plus one per-lane 32-bit offset, so the 32 loads
@@ -518,15 +519,15 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
   }
   // (the MID loop is unrolled over its fixed 16 K-tiles, so every fold and load index is a
   // constant and acc stays in registers; a run-time switch over the folds spilled it)
-  constexpr int kUnroll = EPI == EPI_SUB_MID ? 16 : 1;
-  const int nit_loop = EPI == EPI_SUB_MID ? 16 : nit;
+  constexpr int kUnroll = kFold ? 16 : 1;
+  const int nit_loop = kFold ? 16 : nit;
   __builtin_amdgcn_s_setprio(3);
 #pragma unroll kUnroll
   for (int it = 0; it < nit_loop; ++it) {
     const int64_t kt = k_begin + 16 * (int64_t)it;
     const int64_t k1 = kt + 16 < k_end ? kt + 16 : kt;
     const int64_t k2 = kt + 32 < k_end ? kt + 32 : k1;
-    if (EPI == EPI_SUB_MID) {
+    if (kFold) {
       const int h = it - (nit - 16) - 1;  // half-block folded in this K-tile (15: after the loop)
       switch (h) {
         case 0: GP_C0FOLD(0) break;
@@ -586,7 +587,7 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
 #undef GP_FRAG
 #undef GP_MMA
 #undef GP_SCHED
-  if (EPI == EPI_SUB_MID) {  // acc = A B - C0 once the last half-block is folded; slice_stride = check
+  if (kFold) {  // acc = A B - C0 once the last half-block is folded; slice_stride = check
     GP_C0FOLD(15)
     int flag = 0;
 #pragma unroll
@@ -828,6 +829,7 @@ void gemm_setup_attributes() {
   set_attr_pipe<0, B_PLAIN, EPI_SIGMOID>();
   set_attr_pipe<0, B_PLAIN, EPI_SUB_BAND>();
   set_attr_pipe<0, B_PLAIN, EPI_SUB_CROSS>();
+  set_attr_pipe<0, B_PLAIN, EPI_SUB_CROSS_MID>();
 #ifdef MIDAGMA_EXPERIMENTS
   set_attr_pipe<0, B_PLAIN, EPI_SUB_PRE>();
 #endif
@@ -1067,18 +1069,29 @@ void launch_trail128_split(const double* Ain, double* Aout, int64_t D, int64_t B
   if (D % 128 || B2 % 128 || (g + 2) * B2 > D) throw std::invalid_argument("launch_trail128_split: shape");
   const int tm = (int)((D - B2) / 128), nb = (int)(B2 / 128);
   const int64_t G0 = g * B2;
+  const bool mid = B2 == 256 && trail_mid();  // the tile bodies of launch_trail128 (bit-identical)
   if (part == 0) {
     const int n = nb * (2 * tm - nb);
     // (tiles_n = 2 nb: tiles_m tiles_n >= n, so every tile is in K slice 0)
-    hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_CROSS>), dim3((unsigned)n), dim3(NTHREADS), kGemmPipeLds,
-                       stream, B2, B2, tm, 2 * nb, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
-                       const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)nb, st);
+    if (mid)
+      hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_CROSS_MID>), dim3((unsigned)n), dim3(NTHREADS),
+                         kGemmPipeLds, stream, B2, B2, tm, 2 * nb, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
+                         const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)nb, st);
+    else
+      hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_CROSS>), dim3((unsigned)n), dim3(NTHREADS), kGemmPipeLds,
+                         stream, B2, B2, tm, 2 * nb, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
+                         const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)nb, st);
   } else {
     const int tr = tm - nb;
     if (tr <= 0) return;
-    hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tr * tr)), dim3(NTHREADS),
-                       kGemmPipeLds, stream, B2, B2, tr, tr, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
-                       const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(2 * nb), st);
+    if (mid)
+      hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_MID>), dim3((unsigned)(tr * tr)), dim3(NTHREADS),
+                         kGemmPipeLds, stream, B2, B2, tr, tr, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
+                         const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(2 * nb), st);
+    else
+      hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_BAND>), dim3((unsigned)(tr * tr)), dim3(NTHREADS),
+                         kGemmPipeLds, stream, B2, B2, tr, tr, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
+                         const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(2 * nb), st);
   }
   HIP_TRY(hipGetLastError());
 }
