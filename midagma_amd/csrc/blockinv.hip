@@ -50,6 +50,26 @@ __device__ __forceinline__ void splitk_load_b(const double* __restrict__ B, int6
   for (int q = 0; q < L; ++q) b[q] = bp[(int64_t)q * ldb];
 }
 
+// splitk_load_a of S = (sI - W∘W)^T[0:B2, 0:B2] (outer block 0) computed from W itself:
+// S[i][k] = (k == i ? s : 0) - W[k][i]^2, identity in the padding -- build_at's values, bit for bit
+// (build_at_tile), so block 0's residual can run in build_at's launch (build_resid0_kernel)
+template <int L>
+__device__ __forceinline__ void splitk_load_a_w(const double* __restrict__ W, int64_t ldw, int64_t d, double s,
+                                                int m0, double (&a)[L]) {
+  const int64_t i = m0 + (threadIdx.x & 15), k0 = splitk_k0<L>();
+#pragma unroll
+  for (int q = 0; q < L; ++q) {
+    const int64_t k = k0 + q;
+    if (i < d && k < d) {
+      const double x = W[k * ldw + i];
+      const double f = x * x;
+      a[q] = (k == i ? s : 0.0) - f;
+    } else {
+      a[q] = (k == i) ? 1.0 : 0.0;
+    }
+  }
+}
+
 // Row partial of |Q| over this tile's 16 columns -> rowpart[(m0 + row) * NT + tile column]
 __device__ __forceinline__ void store_row_partial(double a, double* __restrict__ rowpart, int m0, int n0, int NT) {
   a = row_sum16(a);
@@ -125,21 +145,25 @@ __device__ __forceinline__ void nm_tile(int wg, int nt, int xmap, int& m0, int& 
 // workgroup also writes its tile of X0 -> Y0 (the first pass's iterate).
 // NW waves split K (B2 = 4 NW L): NW = 4 for B2 <= 256; B2 = 512 runs NW = 8 with L = 16, so
 // the per-lane operand runs and registers stay those of the 256-wide kernel
-template <int L, int NW = 4>
-__global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restrict__ S, int64_t lds,
-                                                           const double* __restrict__ Pe,
-                                                           const double* __restrict__ Po, double* __restrict__ Y0,
-                                                           double* __restrict__ Q0, double* __restrict__ part0,
-                                                           int* __restrict__ done, State* __restrict__ st,
-                                                           int xmap) {
-  if (st->status != ST_RUNNING) return;
+// Body of the residual launch for workgroup wg; FROM_W: S from W (outer block 0, SW = {W, ldw,
+// d, s}) instead of the At block S (lds)
+struct SFromW {
+  const double* W;
+  int64_t ldw, d;
+  const Params* pr;
+};
+template <int L, int NW, bool FROM_W>
+__device__ __forceinline__ void nm_resid_body(int wg, const double* __restrict__ S, int64_t lds, const SFromW& sw,
+                                              const double* __restrict__ Pe, const double* __restrict__ Po,
+                                              double* __restrict__ Y0, double* __restrict__ Q0,
+                                              double* __restrict__ part0, int* __restrict__ done,
+                                              State* __restrict__ st, int xmap, double* red) {
   if (st->ckpt_pending) {  // a log-det is due: pivots come from the slow path only
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
+    if (wg == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
     return;
   }
   constexpr int B2 = 4 * NW * L;
-  __shared__ double red[NW * 256];
-  const int nt = B2 / 16, wg = blockIdx.x;
+  const int nt = B2 / 16;
   int m0, n0;
   nm_tile(wg, nt, xmap, m0, n0);
   if (wg == 0 && threadIdx.x == 0) *done = 0;
@@ -148,7 +172,10 @@ __global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restr
   const double* P2 = odd ? Po : Pe;  // slot k-2
   const bool extrap = st->warm_run >= 2;
   double a[L], b[L];
-  splitk_load_a<L>(S, lds, m0, a);
+  if (FROM_W)
+    splitk_load_a_w<L>(sw.W, sw.ldw, sw.d, sw.pr->s, m0, a);
+  else
+    splitk_load_a<L>(S, lds, m0, a);
   splitk_load_b<L>(P1, B2, n0, b);
   if (extrap) {
     double b2[L];
@@ -169,6 +196,41 @@ __global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restr
   const double r = (gi == gj ? 1.0 : 0.0) - sum;
   st_wt(Q0 + e, r);
   store_row_partial(abs_or_inf(r), part0, m0, n0, nt);
+}
+
+template <int L, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restrict__ S, int64_t lds,
+                                                           const double* __restrict__ Pe,
+                                                           const double* __restrict__ Po, double* __restrict__ Y0,
+                                                           double* __restrict__ Q0, double* __restrict__ part0,
+                                                           int* __restrict__ done, State* __restrict__ st,
+                                                           int xmap) {
+  if (st->status != ST_RUNNING) return;
+  __shared__ double red[NW * 256];
+  nm_resid_body<L, NW, false>(blockIdx.x, S, lds, SFromW{}, Pe, Po, Y0, Q0, part0, done, st, xmap, red);
+}
+
+// build_at and outer block 0's residual in one launch (fast slots, B2 = 256): workgroups
+// [0, (D/32)^2) build the At tiles, the next 256 the residual tiles with S read from W (the two
+// read W only and write disjoint buffers), one dependent launch fewer per slot
+__global__ __launch_bounds__(NTHREADS) void build_resid0_kernel(const double* __restrict__ W, int64_t ldw,
+                                                                double* __restrict__ At, int64_t D, int64_t d,
+                                                                const Params* __restrict__ pr,
+                                                                const double* __restrict__ Pe,
+                                                                const double* __restrict__ Po, double* __restrict__ Y0,
+                                                                double* __restrict__ Q0, double* __restrict__ part0,
+                                                                int* __restrict__ done, State* __restrict__ st,
+                                                                int xmap) {
+  if (st->status != ST_RUNNING) return;
+  const int kb = (int)(D / 32), nbuild = kb * kb;
+  if ((int)blockIdx.x < nbuild) {
+    __shared__ double tile[32][33];
+    build_at_tile<true, 32>((int)blockIdx.x / kb, (int)blockIdx.x % kb, W, ldw, At, D, d, pr->s, nullptr, tile);
+  } else {
+    __shared__ double red[4 * 256];
+    nm_resid_body<16, 4, true>((int)blockIdx.x - nbuild, nullptr, 0, SFromW{W, ldw, d, pr}, Pe, Po, Y0, Q0, part0,
+                               done, st, xmap, red);
+  }
 }
 
 // Pass p: rho = ||Q||_inf from the previous launch's row partials; converged -> P = Y + Y Q
@@ -867,8 +929,18 @@ static bool blocked_inverse_lookahead(double* Mt, int64_t D, int B2, const BInvW
   return fused;
 }
 
+void launch_build_resid0(const double* W, int64_t ldw, double* At, int64_t D, int64_t d, const Params* pr,
+                         const BInvWork& bw, State* st, hipStream_t stream) {
+  if (binv_block(D) != 256 || D % 32) throw std::invalid_argument("launch_build_resid0: needs B2 = 256");
+  const int kb = (int)(D / 32);
+  hipLaunchKernelGGL(build_resid0_kernel, dim3((unsigned)(kb * kb + 256)), dim3(NTHREADS), 0, stream, W, ldw, At, D, d,
+                     pr, bw.Pst, bw.Pst1, bw.Y[0], bw.Q[0], bw.part, bw.done, st, nm_xmap());
+  HIP_TRY(hipGetLastError());
+}
+
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
-                            hipStream_t stream, int passes, const GemmSpec* fuse, const TrailLookAhead* tla) {
+                            hipStream_t stream, int passes, const GemmSpec* fuse, const TrailLookAhead* tla,
+                            bool resid0_done) {
   bool fused = false;
   const int B2 = binv_block(D);
   if (B2 == 0) throw std::invalid_argument("blocked inverse needs D >= 256, D % 128 == 0");
@@ -899,7 +971,7 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
                     bw.part + (int64_t)(g + 1) * (NM_PASSES + 1) * PART_STRIDE, bw.done + g + 1, g + 1};
     }
     if (fast) {
-      const bool resid = !look || g == 0;
+      const bool resid = (!look || g == 0) && !(g == 0 && resid0_done);  // (block 0: launch_build_resid0)
 #ifdef MIDAGMA_EXPERIMENTS
       if (B2 == 512 && !ahead && resid && nm5_on())
         launch_neumann5(Ain, D, G0, bw, g, st, passes, stream);

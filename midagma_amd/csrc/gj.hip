@@ -42,8 +42,8 @@ __device__ unsigned long long g_stamps[256][16];
 constexpr int EPT = NB * NB / NTHREADS;   // elements per thread in the tile inversion (4)
 constexpr int TPR = NB / EPT;             // threads per tile row (8)
 
-// A^T tile builder: At[J][I] = (I == J ? s : 0) - f(X[I][J]) on the logical
-// d x d block (f = square for W, identity for a given A), identity padding.
+// A^T tile builder (build_at_tile, tile32.h): (D/32)^2 workgroups (1024 at D = 1024) keep
+// enough loads in flight
 template <bool SQUARE, int BT = 32>
 __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __restrict__ X, int64_t ldx,
                                                             double* __restrict__ At, int64_t D, int64_t d,
@@ -52,34 +52,8 @@ __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __rest
   if (st && st->status != ST_RUNNING) return;
   // s comes from device Params when given: graph replays must see each call's s
   const double s = pr ? pr->s : s_arg;
-  // 32 x 32 tiles: (D/32)^2 workgroups (1024 at D = 1024) keep enough loads in flight
   __shared__ double tile[BT][BT + 1];
-  const int bi = blockIdx.y, bj = blockIdx.x;  // source tile (rows bi, cols bj)
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int it = 0; it < BT * BT / NTHREADS; ++it) {
-    const int e = it * NTHREADS + tid;
-    const int r = e / BT, c = e % BT;
-    const int64_t I = (int64_t)bi * BT + r, J = (int64_t)bj * BT + c;
-    double v;
-    const double x = (I < d && J < d) ? X[I * ldx + J] : 0.0;
-    if (I < d && J < d) {
-      const double f = SQUARE ? x * x : x;
-      v = (I == J ? s : 0.0) - f;
-    } else {
-      v = (I == J) ? 1.0 : 0.0;
-    }
-    // I - X, the B operand of the data-mode score GEMM X (I - W) (identity in the padding)
-    if (IW) IW[I * D + J] = (I == J ? 1.0 : 0.0) - x;
-    tile[c][r] = v;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int it = 0; it < BT * BT / NTHREADS; ++it) {
-    const int e = it * NTHREADS + tid;
-    const int r = e / BT, c = e % BT;  // r: row of At tile (= source col)
-    At[((int64_t)bj * BT + r) * D + (int64_t)bi * BT + c] = tile[r][c];
-  }
+  build_at_tile<SQUARE, BT>(blockIdx.y, blockIdx.x, X, ldx, At, D, d, s, IW, tile);
 }
 
 // Reciprocal to ~1 ulp: hardware seed + two Newton steps (no IEEE division chain).

@@ -316,8 +316,14 @@ struct midagma_solver {
       return false;
     }
 #endif
-    launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state, stream,
-                    IW.p);
+    // fast slots at B2 = 256: outer block 0's residual rides in build_at's launch (one dependent
+    // launch fewer; the look-ahead experiment keeps its own residual launches)
+    const bool resid0 = fast && IW.p == nullptr && binv_block(D) == 256 && !cov_la_on() && build_resid0_on();
+    if (resid0)
+      launch_build_resid0(W.p, D, binv_build_target(Mt.p, D, binv()), D, d, d_params, binv(), d_state, stream);
+    else
+      launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
+                      stream, IW.p);
     if (fast && cov_la_on()) {
       const int64_t K2 = D / B2;
       if ((int64_t)la_ev.size() < 2 * K2 + 2) {
@@ -330,7 +336,12 @@ struct midagma_solver {
       const TrailLookAhead tla{side, la_ev.data()};
       return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse, &tla);
     }
-    return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse);
+    return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse, nullptr, resid0);
+  }
+  // experiment knob MIDAGMA_EXP_BUILD_RESID0=1: build_at and block 0's residual in one launch
+  static bool build_resid0_on() {
+    static const bool on = knob("MIDAGMA_EXP_BUILD_RESID0", 0) != 0;
+    return on;
   }
   bool fuse_gemm = knob("MIDAGMA_EXP_FUSE_GEMM", 1) != 0;
 
