@@ -210,6 +210,7 @@ __global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restr
   nm_resid_body<L, NW, false>(blockIdx.x, S, lds, SFromW{}, Pe, Po, Y0, Q0, part0, done, st, xmap, red);
 }
 
+#ifdef MIDAGMA_EXPERIMENTS
 // build_at and outer block 0's residual in one launch (fast slots, B2 = 256): workgroups
 // [0, (D/32)^2) build the At tiles, the next 256 the residual tiles with S read from W (the two
 // read W only and write disjoint buffers), one dependent launch fewer per slot
@@ -232,6 +233,8 @@ __global__ __launch_bounds__(NTHREADS) void build_resid0_kernel(const double* __
                                done, st, xmap, red);
   }
 }
+
+#endif
 
 // Pass p: rho = ||Q||_inf from the previous launch's row partials; converged -> P = Y + Y Q
 // (done = p), else Y' = Y + Y Q, Q' = Q Q and the row partials of |Q'|.  Far or diverging
@@ -929,6 +932,7 @@ static bool blocked_inverse_lookahead(double* Mt, int64_t D, int B2, const BInvW
   return fused;
 }
 
+#ifdef MIDAGMA_EXPERIMENTS
 void launch_build_resid0(const double* W, int64_t ldw, double* At, int64_t D, int64_t d, const Params* pr,
                          const BInvWork& bw, State* st, hipStream_t stream) {
   if (binv_block(D) != 256 || D % 32) throw std::invalid_argument("launch_build_resid0: needs B2 = 256");
@@ -937,6 +941,7 @@ void launch_build_resid0(const double* W, int64_t ldw, double* At, int64_t D, in
                      pr, bw.Pst, bw.Pst1, bw.Y[0], bw.Q[0], bw.part, bw.done, st, nm_xmap());
   HIP_TRY(hipGetLastError());
 }
+#endif
 
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes, const GemmSpec* fuse, const TrailLookAhead* tla,

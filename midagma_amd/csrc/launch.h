@@ -102,10 +102,13 @@ struct TrailLookAhead {
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes = NM_PASSES_RUN, const GemmSpec* fuse = nullptr,
                             const TrailLookAhead* tla = nullptr, bool resid0_done = false);
+#ifdef MIDAGMA_EXPERIMENTS
 // launch_build_at(W, ldw, square, binv_build_target(...), D, d, 0, pr, st, stream) and the fast
-// blocked inverse's outer block 0 residual (S read from W) in one launch; B2 = 256 only.
+// blocked inverse's outer block 0 residual (S read from W) in one launch; B2 = 256 only
+// (experiments build: measured slower).
 void launch_build_resid0(const double* W, int64_t ldw, double* At, int64_t D, int64_t d, const Params* pr,
                          const BInvWork& bw, State* st, hipStream_t stream);
+#endif
 
 // One B2 x B2 block (B2 = 128 or 256) by the product-form series from the warm start in the
 // ring Pe / Po (the slot parity and the extrapolation rule of the blocked inverse: st->slots,

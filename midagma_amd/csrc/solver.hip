@@ -316,12 +316,16 @@ struct midagma_solver {
       return false;
     }
 #endif
-    // fast slots at B2 = 256: outer block 0's residual rides in build_at's launch (one dependent
-    // launch fewer; the look-ahead experiment keeps its own residual launches)
+    // experiments build, MIDAGMA_EXP_BUILD_RESID0=1: outer block 0's residual rides in build_at's
+    // launch on fast slots at B2 = 256 (one dependent launch fewer, but measured slower: DESIGN 8)
+#ifdef MIDAGMA_EXPERIMENTS
     const bool resid0 = fast && IW.p == nullptr && binv_block(D) == 256 && !cov_la_on() && build_resid0_on();
     if (resid0)
       launch_build_resid0(W.p, D, binv_build_target(Mt.p, D, binv()), D, d, d_params, binv(), d_state, stream);
     else
+#else
+    const bool resid0 = false;
+#endif
       launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
                       stream, IW.p);
     if (fast && cov_la_on()) {
@@ -338,11 +342,13 @@ struct midagma_solver {
     }
     return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse, nullptr, resid0);
   }
+#ifdef MIDAGMA_EXPERIMENTS
   // experiment knob MIDAGMA_EXP_BUILD_RESID0=1: build_at and block 0's residual in one launch
   static bool build_resid0_on() {
     static const bool on = knob("MIDAGMA_EXP_BUILD_RESID0", 0) != 0;
     return on;
   }
+#endif
   bool fuse_gemm = knob("MIDAGMA_EXP_FUSE_GEMM", 1) != 0;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
