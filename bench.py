@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--no-cov", action="store_true")
     p.add_argument("--profile-reps", type=int, default=3)
     p.add_argument("--no-fit", action="store_true", help="skip the full-fit wall-clock leg (config 2)")
+    p.add_argument("--no-fit4", action="store_true", help="skip the config-4 full-fit leg (d=1000, n=1e6, cov mode "
+                                                          "from the device / sharded X)")
     p.add_argument("--no-data", action="store_true", help="skip the data-mode leg (profiling the other legs)")
     p.add_argument("--no-large", action="store_true", help="skip the config 3 leg (d=5000, n=5e4, cov mode)")
     p.add_argument("--no-mlp", action="store_true", help="skip the config 5 leg (DagmaNonlinear, dims [200,10,1])")
@@ -744,8 +746,15 @@ def logistic_check(c, threads=8):
             "oracle": "LinearOracle('logistic') and its 64-row blocked-sum variant (the reference's order envelope)"}
 
 
-def value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world):
+def value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world, fit4=None):
     """Every leg's value check (attached as `value_check`; `verified` requires it)."""
+    if fit4 is not None and "_check" in fit4:
+        c = fit4.pop("_check")
+        vc = check_l2(c["W"], c["cov"], c["K"], "oracle reference algorithm on the fit's device-Gram cov, "
+                      "the fit's first 1000 stage-1 Adam steps from W = 0", threads=16)
+        if c["iters"] != c["K"]:
+            vc["ok"] = False
+        fit4["value_check"] = vc
     if res is not None and rank == 0:
         res["value_check"] = check_l2(res["W"], res["cov"], res["steps_total"],
                                       "oracle reference algorithm (cov = X^T X / n of the same X from the device "
@@ -890,6 +899,64 @@ def bench_fit(args, device):
                 accuracy=acc, h_final=float(m.h_final), score_final=float(m.score_final))
 
 
+def bench_fit_config4(args, world, rank, local, data_ms_per_step=None):
+    """Full-fit wall-clock at the headline configuration (BASELINE metric, second half; VERDICT r03
+    item 1): X (d=1000, n=1e6) generated on the GPU(s) -- each rank only its rows --, then
+    DagmaLinear('l2').fit with the reference's defaults in cov mode: the centring and cov's Gram on
+    the device (one all-reduce of the column sums and one of the d x d Gram across ranks), then the
+    n-independent loop (linear.py:428, 441-453), replicated with no per-step communication.
+    The wall clock is split into generation, data preparation and the loop."""
+    import torch
+    import torch.distributed as dist
+    from midagma_amd import DagmaLinear
+    from midagma_amd.simulate import count_accuracy, simulate_er_dag, simulate_weights
+    from midagma_amd.solver import HipSolver
+    dev = torch.device("cuda", local)
+    d, n = args.d, args.n
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    X, n_k, t_gen = make_shard(d, n, world, rank, args.seed, dev)
+    m = DagmaLinear("l2", device=local)
+    t1 = time.perf_counter()
+    W = m.fit(X, lambda1=0.03, n_global=n if world > 1 else None)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    fit_wall = time.perf_counter() - t1
+    del X
+    torch.cuda.empty_cache()
+    ft = dict(m.fit_timing)
+    t = torch.tensor([wall, fit_wall, ft["prep_s"], ft["loop_s"]], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, fit_wall, prep_s, loop_s = (float(x) for x in t.cpu())
+    iters = [e["iters"] for e in m.minimize_log]
+    rng = np.random.default_rng(args.seed)          # make_shard's graph, drawn again
+    B_true = simulate_weights(simulate_er_dag(d, d, rng), rng) != 0
+    out = dict(wall_s=wall, fit_s=fit_wall, sem_gen_s=t_gen, prep_s=prep_s, loop_s=loop_s, final_s=ft["final_s"],
+               cov_on=ft["cov_on"], total_iters=int(sum(iters)), stage_iters=iters,
+               calls=[{k: e[k] for k in ("mu", "s", "lr", "iters", "success", "early_stop")} for e in m.minimize_log],
+               accuracy=count_accuracy(B_true, W != 0), h_final=float(m.h_final), score_final=float(m.score_final),
+               loop_steps_per_s=sum(iters) / loop_s if loop_s > 0 else None, n_per_gpu=n_k,
+               timing="wall_s = GPU SEM generation + fit(); prep_s = centring + Gram + all-reduces + set_cov; "
+                      "loop_s = the path-following loop; max over ranks")
+    if data_ms_per_step:
+        out["data_mode_projected_wall_s"] = out["total_iters"] * data_ms_per_step * 1e-3
+        out["data_mode_projection"] = ("projected, not run: the same total Adam steps at this run's data-mode "
+                                       "ms_per_step (two n x d x d GEMMs per step), i.e. what fit(score_mode='data') "
+                                       "would take")
+    if rank == 0 and not args.no_check:
+        # the fit's cov, 1000 Adam steps of stage 1 (mu=1, s=1, lr=3e-4) on the GPU, for the oracle
+        s = HipSolver(d, "l2", "cov", device=local)
+        s.set_cov(m.cov)
+        Wc = np.zeros((d, d))
+        r = s.minimize(Wc, 1.0, 1000, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=1000)
+        s.close()
+        out["_check"] = dict(W=Wc, cov=m.cov, K=1000, iters=r.iters)
+    m._solver.close()
+    return out
+
+
 def cpu_baseline(args, cov):
     """CPU oracle (numpy/scipy restatement of the reference, bit-identical at 1 thread) on the
     host cores, in child processes with no GPU:
@@ -991,8 +1058,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_logistic and args.workload == "data":
         logi = [bench_logistic(args, local, nn, args.logistic_steps if nn > 100_000 else 200)
                 for nn in (10_000, args.n)]
+    fit4 = None
+    if args.workload == "data" and not args.no_fit4:
+        fit4 = bench_fit_config4(args, world, rank, local, res["ms_per_step"] if res else None)
     if not args.no_check:
-        value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world)
+        value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world, fit4)
     for leg in (small_res, mlp_res, *(logi or [])):
         if leg is not None:
             leg.pop("_check", None)
@@ -1015,7 +1085,7 @@ def main():
         cov_out = None if cov_res is None else {k: v for k, v in cov_res.items()
                                                 if not isinstance(v, np.ndarray) and k not in ("cov", "_check")}
         print(json.dumps({"cov_mode": cov_out, "config3": out, "full_fit": fit_res, "config5": mlp_res,
-                          "config1": small_res, "logistic": logi}), flush=True)
+                          "config1": small_res, "logistic": logi, "full_fit_config4": fit4}), flush=True)
         return
     if rank == 0:
         d = args.d
@@ -1119,6 +1189,20 @@ def main():
             line["logistic"] = logi
         if small_res is not None:
             line["config1"] = small_res
+        if fit4 is not None:
+            f4 = dict(fit4)
+            f4.pop("_check", None)
+            f4["workload"] = (f"config4: DagmaLinear('l2').fit(X) defaults, d={d}, n={args.n}, X generated on the "
+                              f"GPU{'s' if world > 1 else ''} and {'row-sharded over ' + str(world) + ' ranks' if world > 1 else 'device-resident'}"
+                              f", cov mode (device centring + Gram, then the n-independent loop)")
+            f4["verified"] = bool(f4.get("value_check", {}).get("ok", True))
+            if cpu and "reference_algorithm" in cpu:
+                ref_v = cpu["reference_algorithm"]["value"]
+                f4["cpu_projected_wall_s"] = f4["total_iters"] / ref_v
+                f4["cpu_projection"] = ("GPU fit's total Adam steps / CPU reference-algorithm steps/s at d=1000 "
+                                        "(cov precomputed; the CPU's own X^T X at n=1e6 not included)")
+                f4["vs_cpu_projected"] = f4["cpu_projected_wall_s"] / f4["wall_s"]
+            line["full_fit_config4"] = f4
         if fit_res is not None:
             fr = dict(fit_res)
             fr["workload"] = f"config2: DagmaLinear('l2').fit(X) defaults, d={d}, n={args.cov_n}, 1 GPU (cov mode)"

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 6
+#define MIDAGMA_ABI_VERSION 7
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -98,6 +98,23 @@ int midagma_cov_from_zbuf(midagma_solver* s, double n);
 /* The solver's cov (d x d, ld) to the host: the `self.cov` attribute fit() keeps (linear.py:428)
  * when cov was built on the device from the ranks' shards. */
 int midagma_get_cov(midagma_solver* s, double* out, int64_t ld);
+/* ABI 7: fit()'s data preparation on the device (linear.py:406-428), for a device-resident or
+ * row-sharded X in either score mode.  All on `stream` (a hipStream_t, NULL = default).
+ * colsum_dev: out_dev[j] = sum_r X[r, j] (n x d, ldx; fixed summation order); returns after it
+ *   is written.  Sharded: all-reduce it, then center with n_global.
+ * center_dev: X[r, j] -= colsum_dev[j] / nrows in place (the l2 centring, linear.py:411); async.
+ * gram: G_dev (d x d, ldg, device) = X^T X (linear.py:428) for X (n x d, ldx) in device memory
+ *   (on_device != 0) or host memory, streamed in zero-padded row chunks through the 128 x 128
+ *   FP64 MFMA GEMM, chunk sums in a fixed order; MIDAGMA_E_ARG if X holds inf/nan.  Returns
+ *   after G is written.  Sharded: all-reduce G over ranks.
+ * set_cov_dev: the solver's cov = G_dev / divisor (divisor = n, float(self.n) in linear.py:428),
+ *   G_dev d x d (ldg) device memory complete before the call; MIDAGMA_E_ARG on inf/nan. */
+int midagma_colsum_dev(const double* X, int64_t n, int64_t d, int64_t ldx, double* out_dev, void* stream);
+int midagma_center_dev(double* X, int64_t n, int64_t d, int64_t ldx, const double* colsum_dev, double nrows,
+                       void* stream);
+int midagma_gram(const double* X, int64_t n, int64_t d, int64_t ldx, int on_device, double* G_dev, int64_t ldg,
+                 void* stream);
+int midagma_set_cov_dev(midagma_solver* s, const double* G_dev, int64_t ldg, double divisor);
 /* The d x d (+ tail) device buffer that carries the per-step score partial Z_k.
  * Bind an external buffer (e.g. a torch tensor that torch.distributed all-reduces). */
 int64_t midagma_zbuf_len(const midagma_solver* s);

@@ -67,6 +67,10 @@ EXPORTED = {
     "midagma_data_gram": (_int, [_vp]),
     "midagma_cov_from_zbuf": (_int, [_vp, _d]),
     "midagma_get_cov": (_int, [_vp, _dp, _i64]),
+    "midagma_colsum_dev": (_int, [_vp, _i64, _i64, _i64, _vp, _vp]),
+    "midagma_center_dev": (_int, [_vp, _i64, _i64, _i64, _vp, _d, _vp]),
+    "midagma_gram": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _vp]),
+    "midagma_set_cov_dev": (_int, [_vp, _vp, _i64, _d]),
     "midagma_zbuf_len": (_i64, [_vp]),
     "midagma_bind_zbuf": (_int, [_vp, _vp, _i64]),
     "midagma_minimize": (_int, [_vp, _dp, _d, _i64, _d, _d, _d, _d, _d, _d, _i64, C.POINTER(MidagmaResult)]),

@@ -382,6 +382,28 @@ void launch_sum_slices(const double* parts, int split, int64_t stride, int64_t c
 // out[0] = sum(v[0..n)) in a fixed order (one workgroup).
 void launch_sum_vector(const double* v, int64_t n, double* out, const State* st, hipStream_t stream);
 
+// --- gram.hip (fit()'s data preparation, linear.py:406-428) ------------------
+// column sums of X (n x d, ldx): colsum_parts(n) x d doubles of partials, then a fixed-order sum
+int64_t colsum_parts(int64_t n);
+void launch_colsum(const double* X, int64_t n, int64_t d, int64_t ldx, double* part, double* out,
+                   hipStream_t stream);
+// X[r, j] -= colsum[j] / nrows in place
+void launch_center(double* X, int64_t n, int64_t d, int64_t ldx, const double* colsum, double nrows,
+                   hipStream_t stream);
+// S (rpad x D) <- rows x d of X zero-padded; *flag |= 1 on a non-finite value
+void launch_stage_rows(const double* X, int64_t ldx, int64_t rows, int64_t d, double* S, int64_t D, int64_t rpad,
+                       int* flag, hipStream_t stream);
+void launch_nonfinite_or(const double* S, int64_t rows, int64_t cols, int64_t ld, int* flag, hipStream_t stream);
+// out (d x d, ldo) = in (ldi) / divisor; *flag |= 1 on a non-finite result
+void launch_div_block(const double* in, int64_t ldi, double divisor, int64_t d, double* out, int64_t ldo, int* flag,
+                      hipStream_t stream);
+// the chunked Gram's shape: padded D, split-K per chunk, chunk rows (a multiple of 256), chunks
+struct GramPlan {
+  int64_t D = 0, chunk = 0, nchunks = 0;
+  int split = 1;
+};
+GramPlan gram_plan(int64_t n, int64_t d, int64_t chunk_rows);
+
 // --- step.hip ---------------------------------------------------------------
 void launch_reduce_check(const double* Mt, const double* W, const double* Z, const Params* pr, State* st,
                          double* partials, int64_t d, int64_t D, hipStream_t stream);

@@ -1220,6 +1220,93 @@ int midagma_get_cov(midagma_solver* s, double* out, int64_t ld) {
   });
 }
 
+// ABI 7: fit()'s data preparation on device memory (linear.py:406-428), csrc/gram.hip.
+int midagma_colsum_dev(const double* X, int64_t n, int64_t d, int64_t ldx, double* out_dev, void* stream) {
+  if (n < 0 || d < 1 || ldx < d || !out_dev || (n > 0 && !X))
+    return fail(nullptr, MIDAGMA_E_ARG, "colsum_dev: bad arguments");
+  return guarded(nullptr, [&] {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    DevBuf part;
+    part.alloc((size_t)colsum_parts(n) * d);
+    launch_colsum(X, n, d, ldx, part.p, out_dev, st);
+    HIP_TRY(hipStreamSynchronize(st));  // the partials are freed on return
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_center_dev(double* X, int64_t n, int64_t d, int64_t ldx, const double* colsum_dev, double nrows,
+                       void* stream) {
+  if (n < 0 || d < 1 || ldx < d || !colsum_dev || (n > 0 && !X) || !(nrows > 0))
+    return fail(nullptr, MIDAGMA_E_ARG, "center_dev: bad arguments");
+  return guarded(nullptr, [&] {
+    launch_center(X, n, d, ldx, colsum_dev, nrows, reinterpret_cast<hipStream_t>(stream));
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_gram(const double* X, int64_t n, int64_t d, int64_t ldx, int on_device, double* G_dev, int64_t ldg,
+                 void* stream) {
+  if (n < 0 || d < 1 || ldx < d || !G_dev || ldg < d || (n > 0 && !X))
+    return fail(nullptr, MIDAGMA_E_ARG, "gram: bad arguments");
+  return guarded(nullptr, [&] {
+    setup_attributes_once();
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    static const int64_t chunk_rows = [] {
+      const char* e = getenv("MIDAGMA_GRAM_CHUNK_ROWS");
+      return e ? std::max<int64_t>(256, atoll(e)) : int64_t(262144);
+    }();
+    const GramPlan p = gram_plan(n, d, chunk_rows);
+    const int64_t D = p.D, DD = D * D;
+    DevBuf S, Z, fl;
+    S.alloc((size_t)p.chunk * D);
+    Z.alloc((size_t)(p.split + 2) * DD);  // [0] the running sum, [1..split] a chunk's slices, [split+1] the new sum
+    fl.alloc(1);
+    int* flag = reinterpret_cast<int*>(fl.p);
+    HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), st));
+    HIP_TRY(hipMemsetAsync(Z.p, 0, DD * sizeof(double), st));
+    if (!on_device) HIP_TRY(hipMemsetAsync(S.p, 0, (size_t)p.chunk * D * sizeof(double), st));
+    for (int64_t c = 0; c < p.nchunks; ++c) {
+      const int64_t r0 = c * p.chunk, rows = std::min(p.chunk, n - r0);
+      const int64_t rpad = (rows + 255) / 256 * 256;
+      if (on_device) {
+        launch_stage_rows(X + r0 * ldx, ldx, rows, d, S.p, D, rpad, flag, st);
+      } else {
+        if (rows < rpad) HIP_TRY(hipMemsetAsync(S.p + rows * D, 0, (rpad - rows) * D * sizeof(double), st));
+        HIP_TRY(hipMemcpy2DAsync(S.p, D * sizeof(double), X + r0 * ldx, ldx * sizeof(double), d * sizeof(double),
+                                 rows, hipMemcpyHostToDevice, st));
+        launch_nonfinite_or(S.p, rows, d, D, flag, st);
+      }
+      launch_gemm(D, D, rpad, S.p, D, true, S.p, D, B_PLAIN, Z.p + DD, D, EPI_STORE, p.split, DD, nullptr, 0, 0,
+                  nullptr, st);
+      launch_sum_slices(Z.p, p.split + 1, DD, DD, Z.p + (p.split + 1) * DD, nullptr, st);
+      HIP_TRY(hipMemcpyAsync(Z.p, Z.p + (p.split + 1) * DD, DD * sizeof(double), hipMemcpyDeviceToDevice, st));
+    }
+    HIP_TRY(hipMemcpy2DAsync(G_dev, ldg * sizeof(double), Z.p, D * sizeof(double), d * sizeof(double), d,
+                             hipMemcpyDeviceToDevice, st));
+    int bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (bad) throw std::invalid_argument(std::string("gram: ") + kNonFinite);
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_set_cov_dev(midagma_solver* s, const double* G_dev, int64_t ldg, double divisor) {
+  if (!s || !G_dev || ldg < s->d || !(divisor > 0)) return fail(s, MIDAGMA_E_ARG, "set_cov_dev: bad arguments");
+  return guarded(s, [&] {
+    // cov = (X^T X) / float(n), a division as in linear.py:428 (the caller all-reduced the Gram)
+    int* flag = reinterpret_cast<int*>(s->partials.p);
+    HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), s->stream));
+    launch_div_block(G_dev, ldg, divisor, s->d, s->cov.p, s->D, flag, s->stream);
+    int bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (bad) throw std::invalid_argument(std::string("set_cov_dev: ") + kNonFinite);
+    s->has_cov = true;
+    return MIDAGMA_OK;
+  });
+}
+
 int64_t midagma_zbuf_len(const midagma_solver* s) { return s ? s->D * s->D + 64 : 0; }
 
 int midagma_bind_zbuf(midagma_solver* s, void* dev_ptr, int64_t len) {

@@ -39,7 +39,7 @@ import numpy as np
 
 from .slog import LogConfig, StructuredLogger, build_default_logger, checkpoint_row
 from ._lib import HipSolverError
-from .solver import HipSolver, run_allreduce_minimize
+from .solver import HipSolver, is_device_tensor, run_allreduce_minimize
 
 __all__ = ["DagmaLinear"]
 
@@ -100,7 +100,8 @@ class DagmaLinear:
 
     # ------------------------------------------------------------------ helpers
     def _world(self):
-        if self.score_mode != "data":
+        # cov mode talks to the other ranks only while a sharded fit() prepares cov
+        if self.score_mode != "data" and not getattr(self, "_sharded", False):
             return 1, 0
         try:
             import torch.distributed as dist
@@ -136,15 +137,24 @@ class DagmaLinear:
             raise HipSolverError(f"data-parallel replicas diverged: (status, iters) ranges over ranks "
                                  f"[{-m[2]:.0f}, {m[0]:.0f}], [{-m[3]:.0f}, {m[1]:.0f}] (pin NCCL_ALGO=Ring)")
 
-    def _setup_solver(self, X_local=None, cov_on_device=False):
+    def _allreduce_tensor(self, t):
+        """Sum a fit-time tensor over the process group (a no-op on one rank)."""
+        world, _ = self._world()
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(t, group=self.process_group)
+        return t
+
+    def _setup_solver(self, s=None, X_local=None, cov_on_device=False, gram_device=False):
         world, rank = self._world()
-        s = self._solver_factory(self.d, self.loss_type, self.score_mode, device=self.device)
+        if s is None:
+            s = self._solver_factory(self.d, self.loss_type, self.score_mode, device=self.device)
         self._allreduce = None
         if self.score_mode == "data":
             if X_local is None:
                 lo, hi = _row_range(self.n, world, rank)
                 X_local = self.X[lo:hi]
-            s.set_data(np.ascontiguousarray(X_local), n_global=self.n)
+            s.set_data(X_local if is_device_tensor(X_local) else np.ascontiguousarray(X_local), n_global=self.n)
             if world > 1 or self.force_allreduce:
                 import torch.distributed as dist
                 zt, on_stream = s.torch_zbuf()
@@ -164,6 +174,13 @@ class DagmaLinear:
                 self.cov = s.get_cov()
             else:
                 s.set_cov(self.cov)
+        elif gram_device:
+            # cov = (sum_k X_k^T X_k) / n (linear.py:428): this rank's rows through the MFMA Gram,
+            # one all-reduce of the d x d sum over the ranks of a sharded fit, then the loop runs
+            # replicated with no per-step communication (cov is n-independent)
+            G = self._allreduce_tensor(s.gram(X_local if X_local is not None else self.X))
+            s.set_cov_gram(G, float(self.n))
+            self.cov = s.get_cov()
         else:
             s.set_cov(self.cov)
         tr = self.trek_reg
@@ -266,18 +283,40 @@ class DagmaLinear:
             beta_1: float = 0.99, beta_2: float = 0.999,
             exclude_edges: typing.Optional[typing.List[typing.Tuple[int, int]]] = None,
             include_edges: typing.Optional[typing.List[typing.Tuple[int, int]]] = None, *,
-            n_global: int | None = None) -> np.ndarray:
+            n_global: int | None = None, gram: str = "auto") -> np.ndarray:
         """Runs DAGMA and returns the thresholded weighted adjacency (linear.py:335-462).
-        n_global: X is this rank's row shard of an n_global-row matrix (data mode)."""
-        world, rank = self._world()
+
+        Keyword-only extras:
+        n_global: X is this rank's row shard of an n_global-row matrix.  In data mode the rank
+            keeps its rows on its GPU; in cov mode (l2) the ranks' Gram matrices are all-reduced
+            once and every rank runs the same n-independent loop (no per-step communication).
+        gram: where cov = X^T X / n (linear.py:428) is formed in cov mode: 'host' (the
+            reference's numpy product), 'device' (the GPU's MFMA Gram) or 'auto' (the device for
+            a device X, a shard, or n d^2 >= 1e11 flop-pairs, e.g. n = 1e5 at d = 1000).
+        X may be a float64 torch CUDA tensor (centred in place on the device)."""
+        if gram not in ("auto", "host", "device"):
+            raise ValueError("gram must be 'auto', 'host' or 'device'")
+        t_start = time.perf_counter()
         sharded = n_global is not None
-        if sharded and self.score_mode != "data":
-            raise ValueError("fit(X_shard, n_global=...) needs score_mode='data'")
+        self._sharded = sharded
+        world, rank = self._world()
+        on_dev = is_device_tensor(X)
         self.X, self.lambda1, self.checkpoint = X, lambda1, checkpoint
-        self.n, self.d = (int(n_global), X.shape[1]) if sharded else X.shape
+        self.n, self.d = (int(n_global), int(X.shape[1])) if sharded else (int(X.shape[0]), int(X.shape[1]))
         self.Id = np.eye(self.d).astype(self.dtype)
+        if on_dev and gram == "host":
+            raise ValueError("gram='host' needs a host X")
+        gram_device = self.score_mode == "cov" and (
+            gram == "device" or (gram == "auto" and (on_dev or sharded or
+                                                     float(X.shape[0]) * self.d * self.d >= 1e11)))
+        if sharded and self.score_mode == "cov" and not gram_device:
+            raise ValueError("fit(X_shard, n_global=...) in cov mode forms cov on the device (gram='device')")
+        solver = self._solver_factory(self.d, self.loss_type, self.score_mode, device=self.device)
         if self.loss_type == 'l2':
-            if sharded:  # the global column mean from the ranks' column sums
+            if on_dev:  # the centring on the device: column sums (all-reduced over shards), X -= mean
+                colsum = self._allreduce_tensor(solver.colsum(X)) if sharded else solver.colsum(X)
+                solver.center(X, colsum, float(self.n))
+            elif sharded:  # the global column mean from the ranks' column sums
                 colsum = X.sum(axis=0)
                 if world > 1:
                     colsum = self._allreduce_host(colsum)
@@ -298,14 +337,16 @@ class DagmaLinear:
                 self.inc_r, self.inc_c = zip(*include_edges)
             else:
                 ValueError("whitelist should be a tuple of edges, e.g., ((1,2), (2,3))")
-        # data mode over several ranks (or a shard): cov from the device Gram matrices, no rank
-        # multiplies another rank's rows; one rank keeps the reference's host product
-        cov_on_device = self.score_mode == "data" and (sharded or world > 1)
+        # data mode over several ranks (or a shard, or a device X): cov from the device Gram
+        # matrices, no rank multiplies another rank's rows; one host X keeps the reference's product
+        cov_on_device = self.score_mode == "data" and (sharded or world > 1 or on_dev)
         X_local = X if sharded else None
-        if not cov_on_device:
+        if not cov_on_device and not gram_device:
             self.cov = X.T @ X / float(self.n)
         self.W_est = np.zeros((self.d, self.d)).astype(self.dtype)
-        self._setup_solver(X_local=X_local, cov_on_device=cov_on_device)
+        self._setup_solver(solver, X_local=X_local, cov_on_device=cov_on_device, gram_device=gram_device)
+        self._sharded = False  # the loop itself: replicated in cov mode, no collective
+        t_prep = time.perf_counter()
         mu = mu_init
         if type(s) == list:
             if len(s) < T:
@@ -329,8 +370,14 @@ class DagmaLinear:
                         s[i] += 0.1
                 self.W_est = W_temp
                 mu *= mu_factor
+        t_loop = time.perf_counter()
         self.h_final, _ = self._h(self.W_est)
         self.score_final, _ = self._score(self.W_est)
+        # wall-clock split of this fit (not in the reference): data preparation (centring, cov or
+        # the data-mode upload), the path-following loop, and the final h / score
+        self.fit_timing = dict(prep_s=t_prep - t_start, loop_s=t_loop - t_prep,
+                               final_s=time.perf_counter() - t_loop, cov_on=("device" if (gram_device or cov_on_device)
+                                                                              else "host"))
         self.W_est[np.abs(self.W_est) < w_threshold] = 0
         self._slog.close()
         return self.W_est

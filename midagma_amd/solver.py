@@ -17,7 +17,8 @@ import numpy as np
 from . import _lib
 from ._lib import check, dptr
 
-__all__ = ["HipSolver", "MinimizeResult", "CheckpointRecord", "run_allreduce_minimize", "device_count"]
+__all__ = ["HipSolver", "MinimizeResult", "CheckpointRecord", "run_allreduce_minimize", "device_count",
+           "colsum_dev", "center_dev", "gram"]
 
 
 CheckpointRecord = namedtuple("CheckpointRecord", [f for f, _ in _lib.MidagmaCkpt._fields_])
@@ -53,6 +54,62 @@ def device_count() -> int:
 
 def _as_f64(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def is_device_tensor(X) -> bool:
+    """True for a torch CUDA (HIP) tensor."""
+    return hasattr(X, "data_ptr") and getattr(getattr(X, "device", None), "type", None) == "cuda"
+
+
+def _rows(X):
+    """(n, d, ld) of a row-major float64 matrix (host ndarray or device tensor)."""
+    if hasattr(X, "data_ptr"):
+        import torch
+        if X.dtype != torch.float64 or X.dim() != 2 or X.stride(1) != 1:
+            raise ValueError("X must be a 2-d float64 tensor with unit column stride")
+        return int(X.shape[0]), int(X.shape[1]), int(X.stride(0))
+    if X.dtype != np.float64 or X.ndim != 2 or X.strides[1] != 8:
+        raise ValueError("X must be a 2-d float64 array with unit column stride")
+    return int(X.shape[0]), int(X.shape[1]), int(X.strides[0] // 8)
+
+
+def _cur_stream(dev):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def colsum_dev(X):
+    """Column sums of a device X (fixed order; `X.mean(axis=0)` of linear.py:411 is this / n),
+    on torch's current stream.  Returns a float64 device tensor of length d."""
+    import torch
+    n, d, ld = _rows(X)
+    out = torch.empty(d, dtype=torch.float64, device=X.device)
+    check(_lib.lib().midagma_colsum_dev(C.c_void_p(X.data_ptr()), n, d, ld, C.c_void_p(out.data_ptr()),
+                                        _cur_stream(X.device)), None, "colsum_dev")
+    return out
+
+
+def center_dev(X, colsum, nrows: float):
+    """X -= colsum / nrows in place on the device (the l2 centring, linear.py:411)."""
+    n, d, ld = _rows(X)
+    assert colsum.numel() == d and colsum.device == X.device
+    check(_lib.lib().midagma_center_dev(C.c_void_p(X.data_ptr()), n, d, ld, C.c_void_p(colsum.data_ptr()),
+                                        float(nrows), _cur_stream(X.device)), None, "center_dev")
+
+
+def gram(X, device: int | None = None):
+    """G = X^T X (linear.py:428 before the division) on the GPU, for X on the device or on the
+    host (streamed through the device in row chunks).  Returns a d x d float64 device tensor."""
+    import torch
+    n, d, ld = _rows(X)
+    on_dev = is_device_tensor(X)
+    dev = X.device if on_dev else torch.device("cuda", 0 if device is None else device)
+    G = torch.empty((d, d), dtype=torch.float64, device=dev)
+    src = C.c_void_p(X.data_ptr()) if on_dev else X.ctypes.data_as(C.c_void_p)
+    with torch.cuda.device(dev):
+        check(_lib.lib().midagma_gram(src, n, d, ld, 1 if on_dev else 0, C.c_void_p(G.data_ptr()), d,
+                                      _cur_stream(dev)), None, "gram")
+    return G
 
 
 class HipSolver:
@@ -146,6 +203,23 @@ class HipSolver:
             n_local = X.shape[0]
             check(self.L.midagma_set_data(self.h, X.ctypes.data_as(C.c_void_p), n_local,
                                           int(n_global or n_local), 0), self.h, "set_data")
+
+    # fit()'s device data preparation (linear.py:406-428; the CPU test doubles override these)
+    def colsum(self, X):
+        return colsum_dev(X)
+
+    def center(self, X, colsum, nrows: float):
+        center_dev(X, colsum, nrows)
+
+    def gram(self, X):
+        return gram(X, self.device)
+
+    def set_cov_gram(self, G, n: float):
+        """cov = G / n on the device (G: the (all-reduced) d x d Gram matrix, a device tensor)."""
+        import torch
+        assert G.shape == (self.d, self.d) and G.is_contiguous()
+        torch.cuda.current_stream(G.device).synchronize()
+        check(self.L.midagma_set_cov_dev(self.h, C.c_void_p(G.data_ptr()), self.d, float(n)), self.h, "set_cov_dev")
 
     def data_gram(self):
         check(self.L.midagma_data_gram(self.h), self.h, "data_gram")

@@ -316,3 +316,105 @@ def test_sharded_fit_each_rank_ingests_only_its_rows(golden):
         assert np.array_equal(W != 0, W_ref != 0)
         assert abs(h - o.h_final) <= 1e-9 and abs(sc - o.score_final) <= 1e-9
     assert np.array_equal(outs[0][1], outs[1][1]), "replicas diverged"
+
+
+class _CovShardSolver:
+    """CPU double of HipSolver for DagmaLinear.fit in cov mode with a row-sharded X: fit()'s
+    device data preparation (gram / set_cov_gram / get_cov) on this rank's rows only, then the
+    oracle's replicated cov-mode loop (no collective)."""
+
+    def __init__(self, d, loss, mode, device=0):
+        assert loss == "l2" and mode == "cov"
+        self.d = d
+        self.rows_seen = 0
+        self.grams = 0
+
+    def gram(self, X):
+        self.rows_seen += X.shape[0]
+        self.grams += 1
+        return torch.from_numpy(X.T @ X)
+
+    def set_cov_gram(self, G, n):
+        self.cov = G.numpy() / n
+
+    def get_cov(self):
+        return self.cov.copy()
+
+    def set_masks(self, mask_inc, mask_exc):
+        assert mask_inc is None and mask_exc is None
+
+    def minimize(self, W, mu, max_iter, s, lr, tol, b1, b2, lambda1, checkpoint, want_checkpoints=False):
+        from midagma_amd.solver import MinimizeResult
+        from oracle.dagma_oracle import LinearOracle
+        o = LinearOracle("l2")
+        o.cov, o.d, o.n, o.eye = self.cov, self.d, None, np.eye(self.d)
+        o.lambda1, o.checkpoint, o.inc, o.exc, o.X = lambda1, checkpoint, None, None, None
+        Wn, tr = o.minimize(W, mu, max_iter, s, lr, tol, b1, b2)
+        W[...] = Wn
+        return MinimizeResult(iters=tr.iters, success=tr.success, status=_lib.ST_DONE if tr.success else _lib.ST_FAILED,
+                              halvings=tr.halvings, early_stop=tr.early_stop, lr_final=tr.lr_final, slots=tr.iters,
+                              obj_last=0.0, score_last=0.0, h_last=0.0)
+
+    def h_value(self, W, s=1.0, grad=True):
+        from oracle.dagma_oracle import h_logdet
+        return h_logdet(W, s)
+
+    def score_value(self, W):
+        from oracle.dagma_oracle import score
+        return score("l2", W, self.cov)
+
+
+def _cov_fit_worker(rank, world, port, X_shard, n_global, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from midagma_amd import DagmaLinear
+        m = DagmaLinear("l2", solver_factory=_CovShardSolver)
+        Xs = X_shard.copy()
+        W = m.fit(Xs, lambda1=0.03, T=2, warm_iter=300, max_iter=400, n_global=n_global)
+        out_q.put((rank, W, m.cov, Xs, m._solver.rows_seen, m._solver.grams, m.h_final, m.score_final,
+                   [e["iters"] for e in m.minimize_log], m.fit_timing["cov_on"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_cov_mode_fit_one_gram_allreduce(golden):
+    """fit(X_shard, n_global=n) in cov mode over 2 gloo ranks (SURVEY 8e caveat):
+    each rank centres with the all-reduced column sums and forms the Gram of its rows only, one
+    all-reduce of the d x d sum gives every rank cov, and the replicated loop matches the oracle's
+    fit of the full X to 1e-9 with no per-step collective."""
+    from oracle.dagma_oracle import LinearOracle
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    n, world = X.shape[0], 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    spans = [_row_range(n, world, r) for r in range(world)]
+    procs = [ctx.Process(target=_cov_fit_worker, args=(r, world, port, X[lo:hi].copy(), n, q))
+             for r, (lo, hi) in enumerate(spans)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=150) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    o = LinearOracle("l2")
+    W_ref = o.fit(X.copy(), lambda1=0.03, T=2, warm_iter=300, max_iter=400)
+    for r, W, cov, Xs, rows_seen, grams, h, sc, iters, cov_on in outs:
+        lo, hi = spans[r]
+        assert rows_seen == hi - lo and grams == 1 and cov_on == "device"
+        assert np.abs(Xs - o.X[lo:hi]).max() <= 1e-13
+        assert np.abs(cov - o.cov).max() <= 1e-12 * np.abs(o.cov).max()
+        assert iters == [300, 400]
+        assert np.abs(W - W_ref).max() <= 1e-9
+        assert abs(h - o.h_final) <= 1e-9 and abs(sc - o.score_final) <= 1e-9
+    assert np.array_equal(outs[0][1], outs[1][1]), "replicas diverged"
+
+
+def test_fit_gram_argument_validation():
+    from midagma_amd import DagmaLinear
+    X = np.random.default_rng(0).standard_normal((50, 4))
+    with pytest.raises(ValueError):
+        DagmaLinear("l2", solver_factory=_CovShardSolver).fit(X.copy(), gram="gpu")
+    with pytest.raises(ValueError):  # a cov-mode shard needs the Gram all-reduce
+        DagmaLinear("l2", solver_factory=_CovShardSolver).fit(X.copy(), n_global=100, gram="host")
