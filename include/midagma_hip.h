@@ -225,7 +225,8 @@ int midagma_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, co
  * fc1_terms: A[i, j] = sum_m W1[j m1 + m, i]^2 (d x d, the log-det operand) and the |W1| partial
  * sums l1part (midagma_fc1_terms_parts(d) doubles); its backward dW1 = 2 W1 gA^T + gl1 sign(W1).
  * mlp_objective: *obj = mu (half_d log(inv_n *ssq) + lambda1 sum(l1part)) + *h, and its
- * backward from *g: *gssq, gl1part[*], *gh.  All device pointers, on `stream`. */
+ * backward from *g: *gssq, gl1part[*], *gh (ssq and gssq both NULL: only gl1part and gh).
+ * All device pointers, on `stream`. */
 int64_t midagma_fc1_terms_parts(int64_t d);
 int midagma_fc1_terms(const double* W1, int64_t d, int64_t m1, double* A, double* l1part, void* stream);
 int midagma_fc1_terms_bwd(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gscale,
@@ -257,8 +258,9 @@ int midagma_ldfast_create(midagma_ldfast** out, int64_t d);
 void midagma_ldfast_destroy(midagma_ldfast* h);
 int midagma_ldfast_reset(midagma_ldfast* h);
 int64_t midagma_ldfast_parts(const midagma_ldfast* h, int exact);
-int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t lda, double s, double* h_dev, double* Mt_dev,
-                           int64_t ldm, void* stream, int exact, int64_t part);
+/* ABI 7: d (A is d x d) must equal the handle's d, else MIDAGMA_E_ARG. */
+int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t d, int64_t lda, double s, double* h_dev,
+                           double* Mt_dev, int64_t ldm, void* stream, int exact, int64_t part);
 /* gate-open (Gauss-Jordan) steps and fast steps since the last reset (diagnostics; syncs) */
 int midagma_ldfast_stats(midagma_ldfast* h, int64_t* steps, int64_t* exact_steps);
 /* ABI 6: the [d, m1, 1] objective with the scalar objective's backward folded into its consumers

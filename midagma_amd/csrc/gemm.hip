@@ -9,6 +9,7 @@
 // sigmoid and the logistic loss are fused into the epilogue.  Long K (= rows of
 // the shard) is split over blockIdx.z into fixed slices summed in fixed order.
 #include <cstdlib>
+#include <string>
 
 #include "binv_tile.h"
 #include "launch.h"
@@ -944,6 +945,14 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
   HIP_TRY(hipGetLastError());
 }
 
+// The EPI_SUB_MID / EPI_SUB_CROSS_MID tile bodies fold C0 over exactly 16 K-tiles of one K slice
+// (the loop is unrolled with compile-time fold indices), and a workgroup past the tile count would
+// fold nothing: every launcher of them checks that shape on the host.
+static void check_mid_shape(int64_t K, int64_t kslice, int64_t tiles, int64_t grid, const char* who) {
+  if (K != 256 || kslice != K || grid > tiles)
+    throw std::invalid_argument(std::string(who) + ": the C0 fold needs K = kslice = 256 and grid <= tiles");
+}
+
 bool gemm_trail_supported(const GemmSpec& gs) {
   return gs.M % 128 == 0 && gs.N % 128 == 0 && gs.K % 16 == 0 && gs.split >= 1 &&
          !knob_set("MIDAGMA_EXP_GEMM64") && !knob_set("MIDAGMA_EXP_NO_PIPE");
@@ -981,6 +990,7 @@ void launch_gemm_trail(const GemmSpec& gs, const double* Ain, double* Aout, int6
     if (D % 128 || B2 % 128) throw std::invalid_argument("launch_gemm_trail: D, B2 must be multiples of 128");
     Gemm2Args a2{a, (int)((D - B2) / 128), (B2 == 256 && trail_mid()) ? 1 : 0};
     const dim3 grid2((unsigned)(a.n_gemm + a2.tm2 * a2.tm2));
+    if (a2.mid) check_mid_shape(B2, B2, (int64_t)a2.tm2 * a2.tm2, grid2.x - a.n_gemm, "launch_gemm_trail");
 #define MIDAGMA_GT2(AM, BM) \
   hipLaunchKernelGGL((gemm_trail128_kernel<AM, BM>), grid2, dim3(NTHREADS), kGemmPipeLds, stream, a2)
     if (gs.a_trans && gs.bmode == B_PLAIN)
@@ -1022,10 +1032,11 @@ static void launch_trail128_epi(const double* Ain, double* Aout, int64_t D, int6
   static const bool no_pipe = knob_set("MIDAGMA_EXP_NO_PIPE");  // experiment knob
   const dim3 grid((unsigned)(tm * tm));
   const int64_t chk = check ? 1 : 0, b0 = G0 / 128, nb = B2 / 128;
-  if (!no_pipe && mid && B2 == 256)
+  if (!no_pipe && mid && B2 == 256) {
+    check_mid_shape(B2, B2, (int64_t)tm * tm, grid.x, "launch_trail128");
     hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_MID>), grid, dim3(NTHREADS), kGemmPipeLds, stream, B2,
                        B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D, chk, const_cast<double*>(Ain), b0, nb, st);
-  else if (!no_pipe)
+  } else if (!no_pipe)
     hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_BAND>), grid, dim3(NTHREADS), kGemmPipeLds, stream, B2,
                        B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D, chk, const_cast<double*>(Ain), b0, nb, st);
   else
@@ -1073,6 +1084,7 @@ void launch_trail128_split(const double* Ain, double* Aout, int64_t D, int64_t B
   if (part == 0) {
     const int n = nb * (2 * tm - nb);
     // (tiles_n = 2 nb: tiles_m tiles_n >= n, so every tile is in K slice 0)
+    if (mid) check_mid_shape(B2, B2, (int64_t)tm * 2 * nb, n, "launch_trail128_split");
     if (mid)
       hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_CROSS_MID>), dim3((unsigned)n), dim3(NTHREADS),
                          kGemmPipeLds, stream, B2, B2, tm, 2 * nb, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,
@@ -1084,6 +1096,7 @@ void launch_trail128_split(const double* Ain, double* Aout, int64_t D, int64_t B
   } else {
     const int tr = tm - nb;
     if (tr <= 0) return;
+    if (mid) check_mid_shape(B2, B2, (int64_t)tr * tr, (int64_t)tr * tr, "launch_trail128_split");
     if (mid)
       hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_MID>), dim3((unsigned)(tr * tr)), dim3(NTHREADS),
                          kGemmPipeLds, stream, B2, B2, tr, tr, Ain + G0, D, Aout + G0 * D, D, Aout, D, (int64_t)0,

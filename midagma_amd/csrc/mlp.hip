@@ -368,7 +368,7 @@ __global__ __launch_bounds__(NTHREADS) void mlp_objective_bwd_kernel(const doubl
   for (int64_t k = threadIdx.x; k < np; k += NTHREADS) gl1part[k] = gl1;
   if (threadIdx.x == 0) {
     gh[0] = gv;
-    gssq[0] = ((inner * half_d) / (inv_n * ssq[0])) * inv_n;
+    if (ssq != nullptr && gssq != nullptr) gssq[0] = ((inner * half_d) / (inv_n * ssq[0])) * inv_n;
   }
 }
 

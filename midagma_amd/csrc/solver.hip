@@ -1841,9 +1841,11 @@ extern "C" int64_t midagma_ldfast_parts(const midagma_ldfast* h, int exact) {
   return (exact || !h->B) ? h->Dgj / 32 + 2 : kLdfastPasses + 3;
 }
 
-extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t lda, double s, double* h_dev,
-                                      double* Mt_dev, int64_t ldm, void* stream, int exact, int64_t part) {
-  if (!h || !A || !h_dev || !Mt_dev || lda < h->d || ldm < h->d || !(s > 0.0) || part >= midagma_ldfast_parts(h, exact))
+extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t d_in, int64_t lda, double s,
+                                      double* h_dev, double* Mt_dev, int64_t ldm, void* stream, int exact, int64_t part) {
+  if (!h || d_in != h->d)  // the handle's buffers and warm-start ring are sized for its d
+    return fail(nullptr, MIDAGMA_E_ARG, "ldfast_enqueue: A's d differs from the handle's");
+  if (!A || !h_dev || !Mt_dev || lda < h->d || ldm < h->d || !(s > 0.0) || part >= midagma_ldfast_parts(h, exact))
     return fail(nullptr, MIDAGMA_E_ARG, "ldfast_enqueue: bad arguments");
   return guarded(nullptr, [&] {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -2069,7 +2071,7 @@ extern "C" int midagma_mlp_objective(const double* ssq, const double* l1part, in
 extern "C" int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1,
                                          double half_d, double inv_n, double* gssq, double* gl1part, double* gh,
                                          void* stream) {
-  if (!g || !ssq || !gssq || !gl1part || !gh || np < 1)
+  if (!g || (!ssq) != (!gssq) || !gl1part || !gh || np < 1)
     return fail(nullptr, MIDAGMA_E_ARG, "mlp_objective_bwd: bad arguments");
   return guarded(nullptr, [&] {
     launch_mlp_objective_bwd(g, ssq, np, mu, lambda1, half_d, inv_n, gssq, gl1part, gh,

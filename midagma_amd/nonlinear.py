@@ -269,9 +269,10 @@ class _MLPObjective(torch.autograd.Function):
                 _lib.check(L.midagma_fc1_terms_bwd_obj(_vp(W1), d, m1, _vp(Mt), _vp(g), mu, lambda1, _vp(lin), nlin,
                                                        _vp(dW1), st), None, "fc1_terms_bwd_obj")
             else:  # h is also an output whose gradient adds in (not the minimize loop's case)
-                gl1, gh, gdummy = torch.empty(np_, **f64), torch.empty((), **f64), torch.empty((), **f64)
-                _lib.check(L.midagma_mlp_objective_bwd(_vp(g), _vp(part), np_, mu, lambda1, 0.5 * d, 1 / n,
-                                                       _vp(gdummy), _vp(gl1), _vp(gh), st), None, "mlp_objective_bwd")
+                # (d obj / d ssq went into the tail's backward above: only d l1part and d h here)
+                gl1, gh = torch.empty(np_, **f64), torch.empty((), **f64)
+                _lib.check(L.midagma_mlp_objective_bwd(_vp(g), None, np_, mu, lambda1, 0.5 * d, 1 / n,
+                                                       None, _vp(gl1), _vp(gh), st), None, "mlp_objective_bwd")
                 gh = gh + gh_out
                 _lib.check(L.midagma_fc1_terms_bwd(_vp(W1), d, m1, _vp(Mt), _vp(gh), _vp(gl1), _vp(lin), nlin,
                                                    _vp(dW1), st), None, "fc1_terms_bwd")
@@ -352,7 +353,7 @@ class LdFast:
         return int(self.L.midagma_ldfast_parts(self.h, 1 if exact else 0))
 
     def enqueue(self, A, d, s, h, Mt, stream, exact: bool, part: int):
-        _lib.check(self.L.midagma_ldfast_enqueue(self.h, _vp(A), d, float(s), _vp(h), _vp(Mt), d,
+        _lib.check(self.L.midagma_ldfast_enqueue(self.h, _vp(A), d, d, float(s), _vp(h), _vp(Mt), d,
                                                  C.c_void_p(stream) if stream else None, 1 if exact else 0, part),
                    None, "ldfast_enqueue")
 

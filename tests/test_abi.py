@@ -70,7 +70,7 @@ def test_ldfast_entry_points_validate_without_a_device():
     from midagma_amd import _lib
     L = _lib.load()
     assert L.midagma_ldfast_parts(None, 1) == 0
-    assert L.midagma_ldfast_enqueue(None, None, 10, 1.0, None, None, 10, None, 0, -1) == -3
+    assert L.midagma_ldfast_enqueue(None, None, 10, 10, 1.0, None, None, 10, None, 0, -1) == -3
     out = C.c_void_p()
     assert L.midagma_ldfast_create(C.byref(out), 0) == -3
     assert L.midagma_ldfast_reset(None) == -3

@@ -120,3 +120,25 @@ def test_singular_vs_nonfinite_during_minimize():
     with pytest.raises(ValueError):
         sd.minimize(W, 1.0, 5, 1.0, 3e-4, lambda1=0.03)
     sd.close()
+
+
+def test_ldfast_enqueue_refuses_a_different_d():
+    """A warm-started log-det handle is sized for its d (ring, work buffers): an A of another d
+    is refused with ValueError instead of being read out of bounds (ABI 7)."""
+    import ctypes as C
+    import torch
+    from midagma_amd import _lib
+    L = _lib.load()
+    h = C.c_void_p()
+    _lib.check(L.midagma_ldfast_create(C.byref(h), 50), None, "ldfast_create")
+    try:
+        A = torch.zeros(60, 60, dtype=torch.float64, device="cuda:0")
+        hd = torch.zeros((), dtype=torch.float64, device="cuda:0")
+        Mt = torch.zeros(60, 60, dtype=torch.float64, device="cuda:0")
+        rc = L.midagma_ldfast_enqueue(h, C.c_void_p(A.data_ptr()), 60, 60, 1.0, C.c_void_p(hd.data_ptr()),
+                                      C.c_void_p(Mt.data_ptr()), 60, None, 1, -1)
+        assert rc == _lib.E_ARG
+        with pytest.raises(ValueError):
+            _lib.check(rc, None, "ldfast_enqueue")
+    finally:
+        L.midagma_ldfast_destroy(h)

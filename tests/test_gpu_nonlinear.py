@@ -87,6 +87,31 @@ def test_fused_tail_matches_torch(d, m1, n):
         assert torch.max(torch.abs(g1[k] - g0[k])).item() <= 1e-11 * max(1e-300, torch.max(torch.abs(g0[k])).item()), k
 
 
+def test_fused_objective_backward_through_h_and_obj(monkeypatch):
+    """Gradients flowing into both outputs of the fused objective node (h and obj; the minimize
+    loop only backpropagates obj): (obj + 0.37 h).backward() against the PyTorch expressions."""
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    d, m1, n = 24, 10, 400
+    torch.manual_seed(11)
+    model = DagmaMLP(dims=[d, m1, 1]).to("cuda:0")
+    with torch.no_grad():
+        model.fc1.weight.normal_(0, 0.05)
+    dn = DagmaNonlinear(model, device=0)
+    dn.X = torch.randn(n, d, dtype=torch.float64, device="cuda:0")
+    res = {}
+    for fused in (True, False):
+        if not fused:
+            monkeypatch.setenv("MIDAGMA_NO_MLP_TAIL", "1")
+        assert model.fused_tail() == fused
+        model.zero_grad()
+        h, obj = dn._h_and_objective(0.1, 0.02, 1.0)
+        (obj + 0.37 * h).backward()
+        res[fused] = {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+    for k in res[False]:
+        ref = res[False][k]
+        assert torch.max(torch.abs(res[True][k] - ref)).item() <= 1e-10 * max(1e-300, torch.max(torch.abs(ref)).item()), k
+
+
 def test_fused_objective_matches_torch(monkeypatch):
     """mu * (log-MSE score + lambda1 |fc1|_1) + h through the fused kernels (fc1 terms, log-det,
     tail, scalar objective) against the reference's PyTorch expressions: value, h and every
