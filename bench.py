@@ -330,16 +330,6 @@ def bench_mlp(args, device, with_cpu):
     params = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items() if k != "I"}
     K = args.mlp_steps
     Xd = torch.from_numpy(X).to(torch.device("cuda", device))
-    # untimed warm-up: one whole minimize call of K steps on a copy of the model (a process's
-    # first two-stream MLP solver runs 10-20 % slower than the later ones: tools/probe_mlp.py,
-    # DESIGN section 4), so the timed call from the original parameters is a steady-state one
-    model_w = DagmaMLP(dims=[d, 10, 1]).to(torch.device("cuda", device))
-    model_w.load_state_dict(model.state_dict())
-    dn_w = DagmaNonlinear(model_w, device=device)
-    dn_w.X = Xd
-    dn_w.checkpoint = 10 ** 9
-    dn_w.minimize(K, 2e-4, 0.02, 0.005, 0.1, 1.0, tol=-1)
-    del dn_w, model_w
     dn = DagmaNonlinear(model, device=device)
     dn.X = Xd
     dn.checkpoint = 10 ** 9
@@ -354,8 +344,8 @@ def bench_mlp(args, device, with_cpu):
                workload="config5: DagmaNonlinear.minimize, DagmaMLP dims [200, 10, 1], n=1000, 1 GPU "
                         "(the reference's loop; objective as fused HIP kernels: fc1 terms, warm-started log-det, MLP "
                         "tail, scalar objective, multi-tensor Adam; fc1 GEMMs on rocBLAS; the step replayed as a "
-                        "hipGraph; the timed minimize call includes its own graph capture; untimed warm-up: a K-step "
-                        "call on a copy of the model, then the 20-step call the timed one continues)")
+                        "hipGraph; the timed minimize call includes its own graph capture; untimed warm-up: the 20-step "
+                        "call the timed one continues)")
     if getattr(dn, "_ld", None) is not None:
         steps_ld, exact_ld = dn._ld.stats()
         out["logdet"] = {"steps": steps_ld, "gauss_jordan_steps": exact_ld,

@@ -115,6 +115,21 @@ int midagma_center_dev(double* X, int64_t n, int64_t d, int64_t ldx, const doubl
 int midagma_gram(const double* X, int64_t n, int64_t d, int64_t ldx, int on_device, double* G_dev, int64_t ldg,
                  void* stream);
 int midagma_set_cov_dev(midagma_solver* s, const double* G_dev, int64_t ldg, double divisor);
+/* ABI 7: the data-mode score all-reduce inside the library (linear.py:244-246 over row
+ * shards).  comm_unique_id: RCCL's 128-byte ncclUniqueId (rank 0 makes it, the caller broadcasts
+ * it, e.g. over torch.distributed).  comm_init: this solver joins an nranks communicator as `rank`;
+ * from then on every captured slot sums the score partial over the ranks (in place, on the solver
+ * stream, between the GEMMs and the update), so midagma_minimize / midagma_run_slots drive a
+ * multi-rank minimize from replayed graphs, and every host poll all-reduces (status, iters): a
+ * divergent replica makes every rank fail with MIDAGMA_E_STATE instead of hanging.  Needs a ring
+ * all-reduce for bit-identical replicas (NCCL_ALGO=Ring).  RCCL is loaded at run time (the copy in
+ * the process, else ROCm's): MIDAGMA_E_STATE when absent.  comm_ranks: 0 without a communicator. */
+int midagma_comm_unique_id(void* out, int64_t cap); /* returns 128 (the id's size) */
+int midagma_comm_init(midagma_solver* s, const void* id, int64_t id_len, int nranks, int rank);
+int midagma_comm_ranks(const midagma_solver* s);
+/* the score partial of midagma_score_partial (or data_gram) summed over the communicator, on the
+ * solver stream: `_score` in data mode between score_partial and score_finish */
+int midagma_comm_allreduce_zbuf(midagma_solver* s);
 /* The d x d (+ tail) device buffer that carries the per-step score partial Z_k.
  * Bind an external buffer (e.g. a torch tensor that torch.distributed all-reduces). */
 int64_t midagma_zbuf_len(const midagma_solver* s);

@@ -71,6 +71,10 @@ EXPORTED = {
     "midagma_center_dev": (_int, [_vp, _i64, _i64, _i64, _vp, _d, _vp]),
     "midagma_gram": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _vp]),
     "midagma_set_cov_dev": (_int, [_vp, _vp, _i64, _d]),
+    "midagma_comm_unique_id": (_int, [_vp, _i64]),
+    "midagma_comm_init": (_int, [_vp, _vp, _i64, _int, _int]),
+    "midagma_comm_ranks": (_int, [_vp]),
+    "midagma_comm_allreduce_zbuf": (_int, [_vp]),
     "midagma_zbuf_len": (_i64, [_vp]),
     "midagma_bind_zbuf": (_int, [_vp, _vp, _i64]),
     "midagma_minimize": (_int, [_vp, _dp, _d, _i64, _d, _d, _d, _d, _d, _d, _i64, C.POINTER(MidagmaResult)]),

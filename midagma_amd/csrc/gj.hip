@@ -209,6 +209,23 @@ __device__ __forceinline__ bool want_gauss_jordan(const double* Pstore, const St
   return st == nullptr || Pstore == nullptr || st->ckpt_pending || !st->warm_valid;
 }
 
+// Prologue tile t: publish step 0's panels (column tile t, row tile t) and, for t = 0, invert A_00.
+// img: four 32 x ST LDS images, scratch: 4 * NB doubles.
+__device__ __forceinline__ void gj_prologue_tile(int t, const double* __restrict__ A, int64_t lda, int64_t D,
+                                                 double* __restrict__ Cside, double* __restrict__ Rside,
+                                                 double* __restrict__ Pside, double* __restrict__ pivlog,
+                                                 double* __restrict__ Pstore, const State* __restrict__ st,
+                                                 double (*img)[NB * ST], double* scratch) {
+  tile32_copy(Cside + (int64_t)t * NB * NB, NB, A + (int64_t)t * NB * lda, lda);  // column 0
+  tile32_copy(Rside + (int64_t)t * NB, D, A + (int64_t)t * NB, lda);              // row 0
+  if (t != 0) return;
+  const bool want_gj = want_gauss_jordan(Pstore, st);
+  dbl4 acc, x0 = {0.0, 0.0, 0.0, 0.0};
+  acc_foreach(acc, [&](int row, int col, double& v) { v = A[(int64_t)row * lda + col]; });
+  if (!want_gj) acc_foreach(x0, [&](int row, int col, double& v) { v = Pstore[row * NB + col]; });
+  invert_diag_tile(acc, x0, Pside, Pstore, pivlog, want_gj, img[0], img[1], img[2], img[3], scratch);
+}
+
 // Prologue: publish step 0's panels and invert A_00.
 __global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __restrict__ A, int64_t lda, int64_t D,
                                                                double* __restrict__ Cside,
@@ -220,15 +237,7 @@ __global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __r
   if (st && st->status != ST_RUNNING) return;
   __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
   __shared__ double scratch[4 * NB];
-  const int t = blockIdx.x;
-  tile32_copy(Cside + (int64_t)t * NB * NB, NB, A + (int64_t)t * NB * lda, lda);  // column 0
-  tile32_copy(Rside + (int64_t)t * NB, D, A + (int64_t)t * NB, lda);              // row 0
-  if (t != 0) return;
-  const bool want_gj = want_gauss_jordan(Pstore, st);
-  dbl4 acc, x0 = {0.0, 0.0, 0.0, 0.0};
-  acc_foreach(acc, [&](int row, int col, double& v) { v = A[(int64_t)row * lda + col]; });
-  if (!want_gj) acc_foreach(x0, [&](int row, int col, double& v) { v = Pstore[row * NB + col]; });
-  invert_diag_tile(acc, x0, Pside, Pstore, pivlog, want_gj, img[0], img[1], img[2], img[3], scratch);
+  gj_prologue_tile(blockIdx.x, A, lda, D, Cside, Rside, Pside, pivlog, Pstore, st, img, scratch);
 }
 
 // One block step of the elimination (see file header).
@@ -237,24 +246,19 @@ __global__ __launch_bounds__(NTHREADS) void gj_prologue_kernel(const double* __r
 //   global-load latency before its MFMA chain.  The workgroup owning tile (k+1, k+1)
 //   carries the step's serial chain: it takes linear block id 0 (dispatched first),
 //   prefetches its warm start with the operands, inverts before any global store.
-__global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ A, int64_t lda, int64_t D, int k,
-                                                           double* __restrict__ Cside0, double* __restrict__ Cside1,
-                                                           double* __restrict__ Rside0, double* __restrict__ Rside1,
-                                                           double* __restrict__ Pside0, double* __restrict__ Pside1,
-                                                           double* __restrict__ pivlog, double* __restrict__ Pstore,
-                                                           const State* __restrict__ st) {
-  if (st && st->status != ST_RUNNING) return;
-  __shared__ __attribute__((aligned(16))) double L0[NB * ST];  // P            ([m][k])
-  __shared__ __attribute__((aligned(16))) double L1[NB * ST];  // -C_i         ([m][k])
-  __shared__ __attribute__((aligned(16))) double R0[NB * ST];  // R_j or P     ([k][n])
-  __shared__ __attribute__((aligned(16))) double T0[NB * ST];  // P R_j        ([k][n])
-  __shared__ double scratch[4 * NB];
+// Tile (bi, bj) of block step k.  L0, L1, R0, T0: 32 x ST LDS images; scratch 4 * NB doubles.
+// PRIO: raise the diagonal owner's wave priority (the launch-per-step form, where co-resident
+// tiles compete for its SIMD).
+template <bool PRIO>
+__device__ __forceinline__ void gj_step_tile(int bi, int bj, double* __restrict__ A, int64_t lda, int64_t D, int k,
+                                             double* __restrict__ Cside0, double* __restrict__ Cside1,
+                                             double* __restrict__ Rside0, double* __restrict__ Rside1,
+                                             double* __restrict__ Pside0, double* __restrict__ Pside1,
+                                             double* __restrict__ pivlog, double* __restrict__ Pstore,
+                                             const State* __restrict__ st, double* L0, double* L1, double* R0,
+                                             double* T0, double* scratch) {
   const int K = (int)(D / NB);
   const int k1 = k + 1;
-  const int own = k1 < K ? k1 * K + k1 : 0;  // linear id of the diagonal owner
-  int lin = blockIdx.y * K + blockIdx.x;
-  lin = lin == 0 ? own : (lin == own ? 0 : lin);
-  const int bi = lin / K, bj = lin - bi * K;
   const bool odd = k & 1;
   const double* Cs = odd ? Cside1 : Cside0;
   const double* Rs = odd ? Rside1 : Rside0;
@@ -264,7 +268,7 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
   double* Pn = odd ? Pside0 : Pside1;
   double* Aij = A + (int64_t)bi * NB * lda + (int64_t)bj * NB;
   const bool owner = k1 < K && bi == k1 && bj == k1;
-  if (owner) {
+  if (PRIO && owner) {
     __builtin_amdgcn_s_setprio(3);  // its waves win issue arbitration against co-resident tiles
     STAMP(k, 0);
   }
@@ -324,6 +328,73 @@ __global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ 
   if (bi == k1) acc_foreach(acc, [&](int row, int col, double& v) { st_wt(Rn + (int64_t)row * D + (int64_t)bj * NB + col, v); });
 }
 
+__global__ __launch_bounds__(NTHREADS) void gj_step_kernel(double* __restrict__ A, int64_t lda, int64_t D, int k,
+                                                           double* __restrict__ Cside0, double* __restrict__ Cside1,
+                                                           double* __restrict__ Rside0, double* __restrict__ Rside1,
+                                                           double* __restrict__ Pside0, double* __restrict__ Pside1,
+                                                           double* __restrict__ pivlog, double* __restrict__ Pstore,
+                                                           const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  __shared__ __attribute__((aligned(16))) double L0[NB * ST];  // P            ([m][k])
+  __shared__ __attribute__((aligned(16))) double L1[NB * ST];  // -C_i         ([m][k])
+  __shared__ __attribute__((aligned(16))) double R0[NB * ST];  // R_j or P     ([k][n])
+  __shared__ __attribute__((aligned(16))) double T0[NB * ST];  // P R_j        ([k][n])
+  __shared__ double scratch[4 * NB];
+  const int K = (int)(D / NB);
+  const int k1 = k + 1;
+  const int own = k1 < K ? k1 * K + k1 : 0;  // linear id of the diagonal owner
+  int lin = blockIdx.y * K + blockIdx.x;
+  lin = lin == 0 ? own : (lin == own ? 0 : lin);
+  const int bi = lin / K, bj = lin - bi * K;
+  gj_step_tile<true>(bi, bj, A, lda, D, k, Cside0, Cside1, Rside0, Rside1, Pside0, Pside1, pivlog, Pstore, st, L0, L1,
+                     R0, T0, scratch);
+}
+
+// The whole Gauss-Jordan inverse of (sI - A)^T (build, prologue, the D/32 block steps) in ONE
+// workgroup, gated on st: the fallback of a warm-started log-det step whose certificate failed
+// (midagma_ldfast_*), where a closed gate must cost one launch, not the 2 + D/32 of the chain.
+// The tiles run one after the other with the launch-per-step kernels' tile bodies in each phase,
+// so the result is theirs bit for bit (a phase's tiles read only what earlier phases wrote).  Own
+// stores are made visible to the workgroup's later loads by draining them, a barrier, and an
+// agent-scope acquire (which invalidates this CU's L1) between phases.
+__device__ __forceinline__ void gj_1wg_phase_end() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(NTHREADS) void gj_inverse_1wg_kernel(const double* __restrict__ X, int64_t ldx,
+                                                                  double* __restrict__ A, int64_t D, int64_t d,
+                                                                  double s, GJWork w, const State* __restrict__ st) {
+  if (st && st->status != ST_RUNNING) return;
+  __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
+  __shared__ double scratch[4 * NB];
+  double(&tile)[32][33] = *reinterpret_cast<double(*)[32][33]>(&img[0][0]);  // build phase only
+  const int K = (int)(D / NB);
+  for (int bi = 0; bi < K; ++bi)
+    for (int bj = 0; bj < K; ++bj) {
+      build_at_tile<false, 32>(bi, bj, X, ldx, A, D, d, s, nullptr, tile);
+      __syncthreads();
+    }
+  gj_1wg_phase_end();
+  for (int t = 0; t < K; ++t) {
+    gj_prologue_tile(t, A, D, D, w.C, w.R, w.P, w.pivlog, w.Pstore, st, img, scratch);
+    __syncthreads();
+  }
+  gj_1wg_phase_end();
+  for (int k = 0; k < K; ++k) {
+    for (int bi = 0; bi < K; ++bi)
+      for (int bj = 0; bj < K; ++bj) {
+        gj_step_tile<false>(bi, bj, A, D, D, k, w.C, w.C + D * NB, w.R, w.R + NB * D, w.P, w.P + NB * NB, w.pivlog,
+                            w.Pstore, st, img[0], img[1], img[2], img[3], scratch);
+        __syncthreads();
+      }
+    gj_1wg_phase_end();
+  }
+}
+
 void gj_setup_attributes() {}
 
 #ifdef MIDAGMA_STAMPS
@@ -355,6 +426,13 @@ void launch_gj_step(double* A, int64_t lda, int64_t D, const GJWork& w, const St
   const int K = (int)(D / NB);
   hipLaunchKernelGGL(gj_step_kernel, dim3(K, K), dim3(NTHREADS), 0, stream, A, lda, D, k, w.C, w.C + D * NB, w.R,
                      w.R + NB * D, w.P, w.P + NB * NB, w.pivlog, w.Pstore, st);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_gj_inverse_1wg(const double* X, int64_t ldx, double* At, int64_t D, int64_t d, double s, const GJWork& w,
+                           const State* st, hipStream_t stream) {
+  if (D % 32) throw std::invalid_argument("gj_inverse_1wg: D must be a multiple of 32");
+  hipLaunchKernelGGL(gj_inverse_1wg_kernel, dim3(1), dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, w, st);
   HIP_TRY(hipGetLastError());
 }
 

@@ -39,6 +39,10 @@ void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int6
 void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
 // the same as its parts: the prologue, then block steps k = 0 .. D/32 - 1 in order
 void launch_gj_prologue(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
+// build_at (A given, not squared) + the whole Gauss-Jordan inverse in one workgroup, gated on st
+// (bit-identical to launch_build_at + launch_gj_inverse; the rare fallback of a warm-started step)
+void launch_gj_inverse_1wg(const double* X, int64_t ldx, double* At, int64_t D, int64_t d, double s, const GJWork& w,
+                           const State* st, hipStream_t stream);
 void launch_gj_step(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, int k, hipStream_t stream);
 
 // A GEMM launch's arguments (launch_gemm's meaning), for launches that carry one beside other work.
@@ -403,6 +407,16 @@ struct GramPlan {
   int split = 1;
 };
 GramPlan gram_plan(int64_t n, int64_t d, int64_t chunk_rows);
+
+// --- comm.hip (the in-library RCCL communicator of a data-mode solver) -------
+// 128-byte ncclUniqueId into out (returns its size); a communicator of nranks (opaque);
+// in-place all-reduce of n doubles (sum, or max) on stream (graph-capturable)
+int comm_unique_id(void* out);
+void* comm_create(const void* id, int nranks, int rank);
+void comm_destroy(void* comm);
+void comm_allreduce(void* comm, double* buf, size_t n, bool max, hipStream_t stream);
+// out[0..4) = (status, iter, -status, -iter) of *st (one max all-reduce: max and min over ranks)
+void launch_agree_pack(const State* st, double* out, hipStream_t stream);
 
 // --- step.hip ---------------------------------------------------------------
 void launch_reduce_check(const double* Mt, const double* W, const double* Z, const Params* pr, State* st,

@@ -142,8 +142,20 @@ struct midagma_solver {
   int64_t three_pass_left = 0;  // fast slots still to run with 3 passes (after a 2-pass hand-back)
   bool graphs_valid = false;
 
+  // ABI 7: the in-library RCCL communicator (data mode over ranks): the score all-reduce inside
+  // the captured slot graphs, and an agreement all-reduce of (status, iters) at every poll
+  void* comm = nullptr;
+  int comm_ranks = 1;
+  bool inslot_comm = false;  // set while capturing a whole slot
+  DevBuf agree;               // 2 x 4 doubles (double-buffered polls)
+  double* h_agree = nullptr;  // pinned 2 x 4
+
   ~midagma_solver() {
     destroy_graphs();
+    if (stream) (void)hipStreamSynchronize(stream);
+    comm_destroy(comm);
+    agree.release();
+    if (h_agree) (void)hipHostFree(h_agree);
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &npart, &XT, &IW, &scarry,
@@ -257,6 +269,7 @@ struct midagma_solver {
       launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, side, passes, nullptr);
       HIP_TRY(hipEventRecord(ev_join, side));
       enqueue_data_partial(W.p, d_state, IW.p);
+      enqueue_slot_allreduce();
       HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
       gemm_done = true;
     } else if (blocked()) {
@@ -293,6 +306,7 @@ struct midagma_solver {
       if (!gemm_done) enqueue_score_cov(zbuf, d_state, /*sum=*/!(fast && blocked()));
     } else if (!gemm_done) {
       enqueue_data_partial(W.p, d_state, IW.p);
+      enqueue_slot_allreduce();  // beside the forked inverse, before the join
       if (forked_inverse()) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
     }
     // trek regularizer of this slot's W (linear.py:251-258): every slot in 'opt' mode; in 'log'
@@ -303,6 +317,28 @@ struct midagma_solver {
       else
         launch_trek_pst(W.p, d, D, tcfg, tw, d_state, Gtrek.p, stream);
     }
+  }
+
+  // the score partial (and the logistic loss tail) summed over the ranks, in place on the
+  // solver stream, while a whole slot is being captured with a communicator attached
+  void enqueue_slot_allreduce() {
+    if (inslot_comm) comm_allreduce(comm, zbuf, (size_t)(D * D + 64), false, stream);
+  }
+
+  // every rank's (status, iters) at a poll: one max all-reduce into agree[slot], copied to h_agree
+  void enqueue_agree(int slot) {
+    if (!comm) return;
+    launch_agree_pack(d_state, agree.p + 4 * slot, stream);
+    comm_allreduce(comm, agree.p + 4 * slot, 4, true, stream);
+    HIP_TRY(hipMemcpyAsync(h_agree + 4 * slot, agree.p + 4 * slot, 4 * sizeof(double), hipMemcpyDeviceToHost, stream));
+  }
+  void check_agree(int slot) const {
+    if (!comm) return;
+    const double* a = h_agree + 4 * slot;
+    if (a[0] != -a[2] || a[1] != -a[3])
+      throw std::runtime_error("data-parallel replicas diverged: (status, iters) ranges over ranks [" +
+                               std::to_string(-a[2]) + ", " + std::to_string(a[0]) + "], [" + std::to_string(-a[3]) +
+                               ", " + std::to_string(a[1]) + "] (pin NCCL_ALGO=Ring)");
   }
 
   // blocked layout: build_at and the two-level inverse (fast: warm-started diagonal blocks, as
@@ -431,12 +467,15 @@ struct midagma_solver {
   hipGraphExec_t capture(int which, int reps = 1, int passes = NM_PASSES_RUN) {
     hipGraph_t graph = nullptr;
     HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    inslot_comm = comm != nullptr && mode == MIDAGMA_MODE_DATA && (which & 3) == 3;
     try {
       for (int r = 0; r < reps; ++r) {
         if (which & 1) enqueue_part1((which & 4) != 0, passes);
         if (which & 2) enqueue_part2((which & 4) != 0);
       }
+      inslot_comm = false;
     } catch (...) {
+      inslot_comm = false;
       (void)hipStreamEndCapture(stream, &graph);
       if (graph) (void)hipGraphDestroy(graph);
       throw;
@@ -862,7 +901,9 @@ struct midagma_solver {
         for (int64_t b = 0; b < p.singles; ++b) HIP_TRY(hipGraphLaunch(one, stream));
       }
       HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
+      enqueue_agree(0);
       HIP_TRY(hipStreamSynchronize(stream));
+      check_agree(0);
       cur = view(h_state[1]);
       sc.observe(cur);
     }
@@ -923,9 +964,11 @@ struct midagma_solver {
       const int64_t B = graph_next_batch(max_iter, known_iter);
       for (int64_t b = 0; b < B; ++b) HIP_TRY(hipGraphLaunch(g_full, stream));
       launched += B;
+      enqueue_agree(cur);
       snapshot(cur);
       if (pending >= 0) {
         HIP_TRY(hipEventSynchronize(ev[pending]));
+        check_agree(pending);
         known_iter = h_state[pending].iter;
         if (terminal(h_state[pending])) stop = true;
       }
@@ -1303,6 +1346,37 @@ int midagma_set_cov_dev(midagma_solver* s, const double* G_dev, int64_t ldg, dou
     HIP_TRY(hipStreamSynchronize(s->stream));
     if (bad) throw std::invalid_argument(std::string("set_cov_dev: ") + kNonFinite);
     s->has_cov = true;
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_comm_unique_id(void* out, int64_t cap) {
+  if (!out || cap < 128) return fail(nullptr, MIDAGMA_E_ARG, "comm_unique_id: needs a 128-byte buffer");
+  return guarded(nullptr, [&] { return comm_unique_id(out); });
+}
+
+int midagma_comm_init(midagma_solver* s, const void* id, int64_t id_len, int nranks, int rank) {
+  if (!s || !id || id_len != 128 || nranks < 1 || rank < 0 || rank >= nranks || s->mode != MIDAGMA_MODE_DATA)
+    return fail(s, MIDAGMA_E_ARG, "comm_init: bad arguments (data mode, a 128-byte unique id, 0 <= rank < nranks)");
+  return guarded(s, [&] {
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    comm_destroy(s->comm);
+    s->comm = nullptr;
+    s->comm = comm_create(id, nranks, rank);
+    s->comm_ranks = nranks;
+    s->agree.alloc(8);
+    if (!s->h_agree) HIP_TRY(hipHostMalloc(&s->h_agree, 8 * sizeof(double), hipHostMallocDefault));
+    s->graphs_valid = false;  // the slot graphs now carry the all-reduce
+    return MIDAGMA_OK;
+  });
+}
+
+int midagma_comm_ranks(const midagma_solver* s) { return s ? (s->comm ? s->comm_ranks : 0) : 0; }
+
+int midagma_comm_allreduce_zbuf(midagma_solver* s) {
+  if (!s || !s->comm) return fail(s, MIDAGMA_E_STATE, "comm_allreduce_zbuf: comm_init first");
+  return guarded(s, [&] {
+    comm_allreduce(s->comm, s->zbuf, (size_t)(s->D * s->D + 64), false, s->stream);
     return MIDAGMA_OK;
   });
 }
@@ -1877,10 +1951,16 @@ extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_
       if (want(p)) launch_series_pass(h->B, w, h->st, p, st);
     if (want(kLdfastPasses + 1)) {
       launch_ldfast_certify(h->P.p, h->B, d, Mt_dev, ldm, h->st, reinterpret_cast<const int*>(h->done.p), h->gjst, st);
-      // gated: opened by the certificate.  (Off the step's critical path: leaving these 9 gated-off
-      // launches out changed nothing measurable, 7.4-7.6k steps/s either way.)
-      launch_build_at(A, lda, false, h->A.p, D, d, s, nullptr, h->gjst, st);
-      launch_gj_inverse(h->A.p, D, D, h->gjw(), h->gjst, st);
+      // gated: opened by the certificate.  One launch, the whole Gauss-Jordan chain in one
+      // workgroup (bit-identical; slow when open, which the bench window never is): a closed gate
+      // costs one no-op launch instead of the chain's 2 + D/32 (MIDAGMA_EXP_LDFAST_CHAIN=1, the
+      // experiments build: the launch-per-step chain, gated)
+      if (knob_set("MIDAGMA_EXP_LDFAST_CHAIN")) {
+        launch_build_at(A, lda, false, h->A.p, D, d, s, nullptr, h->gjst, st);
+        launch_gj_inverse(h->A.p, D, D, h->gjw(), h->gjst, st);
+      } else {
+        launch_gj_inverse_1wg(A, lda, h->A.p, D, d, s, h->gjw(), h->gjst, st);
+      }
     }
     if (want(kLdfastPasses + 2))
       launch_ldfast_post(h->piv.p, d, dls, h_dev, h->A.p, D, Mt_dev, ldm, h->P.p, h->B, h->ring0.p, h->ring1.p, h->st,

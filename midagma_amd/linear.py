@@ -14,6 +14,10 @@ the C ABI.  Extra keyword-only constructor arguments:
   its row shard of X and the per-step score partial is all-reduced over it.
 * ``force_allreduce``  run the all-reduce path (torch-owned score buffer,
   `dist.all_reduce` on the solver stream) even on one rank (tests, rehearsals).
+* ``comm``  data mode over ranks: 'library' (the solver's own RCCL communicator: the score
+  all-reduce is captured in the slot graphs, the loop runs from the device; the default under an
+  'nccl' process group), 'host' (a `dist.all_reduce` between `step_partial` and `step_finish`
+  every step; the default otherwise, e.g. gloo) or None (the default for the backend).
 * ``solver_factory``  the backend class (default `HipSolver`; tests pass a CPU double).
 
 `fit(X, ..., n_global=N)` (keyword-only extra): X is this rank's row shard of an
@@ -69,7 +73,7 @@ class DagmaLinear:
     def __init__(self, loss_type: str, verbose: bool = False, dtype: type = np.float64, *,
                  trek_reg=None, logger=None, log_cfg=None, score_mode: str | None = None,
                  device: int | None = None, process_group=None, force_allreduce: bool = False,
-                 solver_factory=None) -> None:
+                 comm: str | None = None, solver_factory=None) -> None:
         losses = ["l2", "logistic"]
         assert loss_type in losses, f"loss_type should be one of {losses}"
         if dtype is not np.float64:
@@ -93,6 +97,10 @@ class DagmaLinear:
         self.device = device
         self.process_group = process_group
         self.force_allreduce = bool(force_allreduce)
+        if comm not in (None, "library", "host"):
+            raise ValueError("comm must be 'library', 'host' or None")
+        self.comm = comm
+        self._inlib = False
         self._solver_factory = solver_factory or HipSolver
         self._solver: HipSolver | None = None
         self._allreduce = None
@@ -145,6 +153,17 @@ class DagmaLinear:
             dist.all_reduce(t, group=self.process_group)
         return t
 
+    def _comm_kind(self) -> str:
+        if self.comm is not None:
+            return self.comm
+        try:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_backend(self.process_group) == "nccl":
+                return "library"
+        except Exception:  # pragma: no cover
+            pass
+        return "host"
+
     def _setup_solver(self, s=None, X_local=None, cov_on_device=False, gram_device=False):
         world, rank = self._world()
         if s is None:
@@ -155,7 +174,17 @@ class DagmaLinear:
                 lo, hi = _row_range(self.n, world, rank)
                 X_local = self.X[lo:hi]
             s.set_data(X_local if is_device_tensor(X_local) else np.ascontiguousarray(X_local), n_global=self.n)
-            if world > 1 or self.force_allreduce:
+            self._inlib = (world > 1 or self.force_allreduce) and self._comm_kind() == "library"
+            if self._inlib:
+                # the solver's own communicator: the score all-reduce inside the replayed slots
+                s.attach_comm(self.process_group)
+                if cov_on_device:
+                    G = self._allreduce_tensor(s.gram(X_local))
+                    s.set_cov_gram(G, float(self.n))
+                    self.cov = s.get_cov()
+                else:
+                    s.set_cov(self.cov)
+            elif world > 1 or self.force_allreduce:
                 import torch.distributed as dist
                 zt, on_stream = s.torch_zbuf()
                 pg = self.process_group
@@ -165,7 +194,9 @@ class DagmaLinear:
                         dist.all_reduce(zt, group=pg)
 
                 self._allreduce, self._zt = _allreduce, zt
-            if cov_on_device:
+            if self._inlib:
+                pass
+            elif cov_on_device:
                 # cov = (sum_k X_k^T X_k) / n (linear.py:428) from the ranks' device Gram matrices
                 s.data_gram()
                 if self._allreduce is not None:
@@ -204,6 +235,8 @@ class DagmaLinear:
         self._solver.score_partial(W)
         if self._allreduce is not None:
             self._allreduce()
+        elif self._inlib:
+            self._solver.comm_allreduce_zbuf()
         return self._solver.score_finish()
 
     def _h(self, W: np.ndarray, s: float = 1.0) -> typing.Tuple[float, np.ndarray]:

@@ -243,6 +243,32 @@ class HipSolver:
         ext = torch.cuda.ExternalStream(self.stream, device=dev)
         return zt, (lambda: torch.cuda.stream(ext))
 
+    def attach_comm(self, group=None):
+        """Join an in-library RCCL communicator over `group` (torch.distributed; ABI 7): rank 0's
+        ncclUniqueId is broadcast over the group, then every captured slot all-reduces the score
+        partial itself, and minimize / run_slots drive the multi-rank loop from the device."""
+        import torch
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            check(self.L.midagma_comm_unique_id(C.c_void_p(uid.data_ptr()), 128), None, "comm_unique_id")
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        if dist.get_backend(group) == "nccl":
+            t = uid.to(torch.device("cuda", self.device))
+            dist.broadcast(t, src=src, group=group)
+            uid = t.cpu()
+        else:
+            dist.broadcast(uid, src=src, group=group)
+        check(self.L.midagma_comm_init(self.h, C.c_void_p(uid.data_ptr()), 128, world, rank), self.h, "comm_init")
+
+    def comm_allreduce_zbuf(self):
+        check(self.L.midagma_comm_allreduce_zbuf(self.h), self.h, "comm_allreduce_zbuf")
+
+    @property
+    def comm_ranks(self) -> int:
+        return int(self.L.midagma_comm_ranks(self.h))
+
     @property
     def zbuf_len(self) -> int:
         return int(self.L.midagma_zbuf_len(self.h))

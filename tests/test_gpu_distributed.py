@@ -92,17 +92,45 @@ m0 = DagmaLinear("l2", score_mode="data", device=0)
 W0 = m0.fit(X.copy(), **kw)
 dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=0, world_size=1,
                         device_id=torch.device("cuda", 0))
-m1 = DagmaLinear("l2", score_mode="data", device=0, force_allreduce=True)
+m1 = DagmaLinear("l2", score_mode="data", device=0, force_allreduce=True, comm="host")
 W1 = m1.fit(X.copy(), **kw)
-m2 = DagmaLinear("l2", score_mode="data", device=0, force_allreduce=True)
+m2 = DagmaLinear("l2", score_mode="data", device=0, force_allreduce=True, comm="host")
 W2 = m2.fit(X.copy(), n_global=X.shape[0], **kw)
+# the in-library communicator (ABI 7): the all-reduce captured in the slot graphs, the loop on the device
+m3 = DagmaLinear("l2", score_mode="data", device=0, force_allreduce=True)
+W3 = m3.fit(X.copy(), **kw)
+from midagma_amd.solver import HipSolver
+Xc = X - X.mean(axis=0, keepdims=True)
+res = {}
+for lib_comm in (False, True):
+    for loss in ("l2", "logistic"):
+        Xl = Xc if loss == "l2" else (X > 0).astype(np.float64)
+        s = HipSolver(64, loss, "data", device=0)
+        s.set_data(Xl, n_global=Xl.shape[0])
+        s.set_cov(Xl.T @ Xl / float(Xl.shape[0]))
+        if lib_comm:
+            s.attach_comm(None)
+            assert s.comm_ranks == 1
+        Wk = np.zeros((64, 64))
+        r = s.minimize(Wk, 1.0, 300, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100)
+        s.score_partial(Wk)
+        if lib_comm:
+            s.comm_allreduce_zbuf()
+        res[(lib_comm, loss)] = (Wk, r.iters, s.score_finish()[0])
+        s.close()
 out = dict(it0=[e["iters"] for e in m0.minimize_log], it1=[e["iters"] for e in m1.minimize_log],
            bit_identical=bool(np.array_equal(W1, W0)), h=[m0.h_final, m1.h_final], sc=[m0.score_final, m1.score_final],
            allreduce_path=m1._allreduce is not None and m2._allreduce is not None,
            cov_rel=float(np.abs(m2.cov - m0.cov).max() / np.abs(m0.cov).max()),
-           dW2=float(np.abs(W2 - W0).max()), support2=bool(np.array_equal(W2 != 0, W0 != 0)))
+           dW2=float(np.abs(W2 - W0).max()), support2=bool(np.array_equal(W2 != 0, W0 != 0)),
+           inlib=bool(m3._inlib and m3._allreduce is None and m3._solver.comm_ranks == 1),
+           it3=[e["iters"] for e in m3.minimize_log], lib_fit_identical=bool(np.array_equal(W3, W0)),
+           sc3=m3.score_final,
+           lib_solver_identical={loss: bool(np.array_equal(res[(True, loss)][0], res[(False, loss)][0])
+                                            and res[(True, loss)][1:] == res[(False, loss)][1:])
+                                 for loss in ("l2", "logistic")})
 print(json.dumps(out), flush=True)
-for m in (m0, m1, m2):
+for m in (m0, m1, m2, m3):
     m._solver.close()
 torch.cuda.synchronize()
 dist.destroy_process_group()
@@ -111,11 +139,14 @@ print("DESTROYED", flush=True)
 
 
 def test_nccl_one_rank_allreduce_path_bit_identical():
-    """The RCCL code path at world size 1: DagmaLinear(score_mode='data', force_allreduce=True)
+    """The RCCL code paths at world size 1.  Host-driven (comm='host'): DagmaLinear(score_mode='data', force_allreduce=True)
     under a one-rank 'nccl' process group runs every step as step_partial -> dist.all_reduce of
     the torch-owned score buffer on the solver's stream (ExternalStream) -> step_finish.  A
     one-rank sum is the identity, so W must equal the single-process run bit for bit.  The
     sharded form fit(X, n_global=n) (device Gram + all-reduce for cov) must agree to 1e-9.
+    In-library (the default under 'nccl', ABI 7): the solver's own communicator, the all-reduce
+    captured in the replayed slot graphs and the loop driven from the device: fit() and a
+    HipSolver.minimize (l2 and logistic, 300 steps) equal the single-process runs bit for bit.
     Runs in a child process (its own HIP/RCCL state), which also destroys the process group."""
     import json
     import subprocess
@@ -133,4 +164,8 @@ def test_nccl_one_rank_allreduce_path_bit_identical():
     assert out["h"][0] == out["h"][1] and out["sc"][0] == out["sc"][1]
     assert out["cov_rel"] <= 1e-12
     assert out["dW2"] <= 1e-9 and out["support2"]
+    # the in-library RCCL path (the default under 'nccl'): bit-identical to the single-process run
+    assert out["inlib"] and out["it3"] == out["it0"] and out["lib_fit_identical"]
+    assert out["sc3"] == out["sc"][0]
+    assert out["lib_solver_identical"] == {"l2": True, "logistic": True}, out["lib_solver_identical"]
     assert "DESTROYED" in r.stdout and r.returncode == 0, f"destroy_process_group: rc={r.returncode} {r.stderr[-3000:]}"

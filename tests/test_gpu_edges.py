@@ -142,3 +142,59 @@ def test_ldfast_enqueue_refuses_a_different_d():
             _lib.check(rc, None, "ldfast_enqueue")
     finally:
         L.midagma_ldfast_destroy(h)
+
+
+def test_ldfast_gate_open_fallback_equals_chain():
+    """A warm-started log-det step whose certificate fails (A jumps far from the warm start) opens
+    the device gate and runs the one-workgroup Gauss-Jordan fallback (gj_inverse_1wg_kernel): its
+    h and (sI - A)^-T equal the launch-per-step chain's of an exact step bit for bit; a closed gate
+    leaves the fast inverse, within 1e-12 of the exact one, and the last exact h."""
+    import ctypes as C
+    import torch
+    from midagma_amd import _lib
+    L = _lib.load()
+    d = 200
+    rng = np.random.default_rng(4)
+    A1 = rng.uniform(0.0, 0.5 / d, size=(d, d))
+    A2 = rng.uniform(0.0, 1.2 / d, size=(d, d))  # far from A1 (rho(R) ~ 0.5): the series hands back
+    dev = "cuda:0"
+    f64 = dict(dtype=torch.float64, device=dev)
+
+    def vp(t):
+        return C.c_void_p(t.data_ptr())
+
+    def new():
+        h = C.c_void_p()
+        _lib.check(L.midagma_ldfast_create(C.byref(h), d), None, "ldfast_create")
+        return h
+
+    def step(h, A, exact):
+        At = torch.from_numpy(A).to(dev)
+        hv, Mt = torch.zeros((), **f64), torch.zeros(d, d, **f64)
+        _lib.check(L.midagma_ldfast_enqueue(h, vp(At), d, d, 1.0, vp(hv), vp(Mt), d, None, 1 if exact else 0, -1),
+                   None, "ldfast_enqueue")
+        torch.cuda.synchronize()
+        return float(hv.item()), Mt.cpu().numpy()
+
+    h = new()
+    try:
+        h0, _ = step(h, A1, True)
+        step(h, A1 * (1 + 1e-6), False)          # converges: the gate stays closed
+        h_fast, M_fast = step(h, A1 * (1 + 2e-6), False)
+        a, b = C.c_int64(), C.c_int64()
+        _lib.check(L.midagma_ldfast_stats(h, C.byref(a), C.byref(b)), None, "ldfast_stats")
+        exact_before = b.value
+        h_open, M_open = step(h, A2, False)      # the certificate fails: the fallback runs
+        _lib.check(L.midagma_ldfast_stats(h, C.byref(a), C.byref(b)), None, "ldfast_stats")
+        assert b.value == exact_before + 1, (exact_before, b.value)
+    finally:
+        L.midagma_ldfast_destroy(h)
+    ref = new()
+    try:
+        h_ex, M_ex = step(ref, A2, True)
+        h_ex1, M_ex1 = step(ref, A1 * (1 + 2e-6), True)
+    finally:
+        L.midagma_ldfast_destroy(ref)
+    assert h_open == h_ex and np.array_equal(M_open, M_ex)
+    assert h_fast == h0                          # a certified fast step keeps the last exact h
+    assert np.abs(M_fast - M_ex1).max() <= 1e-12 * np.abs(M_ex1).max()

@@ -83,6 +83,36 @@ if __name__ == "__main__":
             run(K, True, True)
             keep.append(torch.cuda.Stream())
         sys.exit(0)
+    if len(sys.argv) > 2 and sys.argv[2] == "ramp":
+        # the same run repeated, then after a 2 s MFMA burn, with the engine clock read around each
+        # run: is the first solver's slowness the process's first work or the clock it starts at?
+        import subprocess
+
+        def clocks(tag):
+            try:
+                r = subprocess.run(["rocm-smi", "--showclocks"], capture_output=True, text=True, timeout=20)
+                ln = [x.strip() for x in r.stdout.splitlines() if "sclk" in x or "fclk" in x or "mclk" in x]
+                print(f"   clocks {tag}: {' | '.join(ln[:3])}", flush=True)
+            except Exception as e:  # noqa: BLE001
+                print(f"   clocks {tag}: n/a ({e})", flush=True)
+        for rep in range(4):
+            clocks(f"before run {rep}")
+            run(K, True, True)
+        a = torch.randn(8192, 8192, dtype=torch.float64, device="cuda:0")
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 2.0:
+            a = a @ a * 1e-4
+            torch.cuda.synchronize()
+        print("-- after a 2 s DGEMM burn:", flush=True)
+        for rep in range(2):
+            clocks(f"after burn run {rep}")
+            run(K, True, True)
+        time.sleep(5)
+        print("-- after 5 s idle:", flush=True)
+        clocks("after idle")
+        run(K, True, True)
+        run(K, False, True)
+        sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[2] == "fused":  # fc1 + tail on the MFMA (ABI 7) or the ABI-6 sequence
         import midagma_amd.nonlinear as nl
         for rep in range(2):
