@@ -180,8 +180,14 @@ def bench_data(args, world, rank, local):
     torch.cuda.empty_cache()
     allreduce = None
     comm = None
-    if world > 1:
-        ext = torch.cuda.ExternalStream(s.stream, device=dev)
+    # N > 1 over RCCL: the solver's own communicator (ABI 7), the score all-reduce captured in the
+    # replayed slot graphs and the loop driven by run_slots; gloo (the one-GPU rehearsal) and
+    # MIDAGMA_BENCH_COMM=host: the host-driven step_partial -> dist.all_reduce -> step_finish
+    lib_comm = world > 1 and dist.get_backend() == "nccl" and os.environ.get("MIDAGMA_BENCH_COMM", "library") == "library"
+    ext = torch.cuda.ExternalStream(s.stream, device=dev)
+    if lib_comm:
+        s.attach_comm()
+    elif world > 1:
         zt = torch.zeros(s.zbuf_len, dtype=torch.float64, device=dev)
         s.bind_zbuf(zt.data_ptr(), zt.numel())
         # hipEvents around every all-reduce on the solver stream (the stream it runs on):
@@ -201,9 +207,14 @@ def bench_data(args, world, rank, local):
     K, Wm = args.steps, args.warmup
     s.begin(np.zeros((d, d)), 1.0, Wm + K + 64, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
 
+    host_enqueue = []
+
     def steps(m, timed=False):
         if allreduce is None:
+            t_ = time.perf_counter()
             s.run_slots(m)
+            if timed:
+                host_enqueue.append(time.perf_counter() - t_)
         else:
             for _ in range(m):
                 s.step_partial()
@@ -232,12 +243,34 @@ def bench_data(args, world, rank, local):
     s.end(Wf)
     replicas = None
     if world > 1:
-        ar_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        if lib_comm:
+            # the in-graph all-reduce is not separable inside the replayed slot: the same in-place
+            # all-reduce of the score buffer timed alone, eagerly, on the solver stream
+            with torch.cuda.stream(ext):
+                for _ in range(3):
+                    s.comm_allreduce_zbuf()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(20):
+                    s.comm_allreduce_zbuf()
+                b.record()
+            b.synchronize()
+            ev = [(a, b)]
+            ar_scale = 1.0 / 20
+        else:
+            ar_scale = 1.0
+        ar_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) * ar_scale
         t = torch.tensor([ar_ms, -ar_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ar_max, ar_min = float(t[0]), -float(t[1])
         comm = comm_summary(ar_max, ar_min, elapsed / K * 1e3, 8 * s.zbuf_len, dist.get_world_size(),
                             dist.get_backend())
+        comm["path"] = ("in-library RCCL communicator: the all-reduce captured in the replayed slot graph, run_slots "
+                        "drives the loop (allreduce_ms: the same all-reduce timed alone, 20 eager calls)" if lib_comm
+                        else "host-driven: step_partial -> dist.all_reduce on the solver stream -> step_finish, "
+                             "one Python round per step")
+        if lib_comm and host_enqueue:
+            comm["host_enqueue_ms_per_step"] = sum(host_enqueue) / K * 1e3
         # W must be bit-identical on every rank: compare (sum, sum of squares) over ranks
         v = np.array([Wf.sum(), (Wf * Wf).sum()])
         t = torch.tensor(np.concatenate([v, -v]), dtype=torch.float64, device=dev)
@@ -248,7 +281,9 @@ def bench_data(args, world, rank, local):
     # value check: cov = X^T X / n of the same (centered, sharded) X from the device Gram,
     # all-reduced over ranks; rank 0 runs the oracle's reference algorithm on it (linear.py:244)
     s.data_gram()
-    if world > 1:
+    if lib_comm:
+        s.comm_allreduce_zbuf()
+    elif world > 1:
         with torch.cuda.stream(ext):
             dist.all_reduce(zt)
     s.cov_from_zbuf(float(n))
@@ -256,7 +291,11 @@ def bench_data(args, world, rank, local):
     # the per-kernel profile below runs rank 0's kernels alone (no all-reduce): restart from the
     # final W so it times the same matrices
     s.begin(Wf, 1.0, 64, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
-    prof = s.profile_parts(args.profile_reps) if rank == 0 else {}
+    # (with the in-library communicator the profiled slot graph carries the all-reduce: every rank
+    # replays it the same number of times, rank 0 reports)
+    prof = s.profile_parts(args.profile_reps) if (rank == 0 or lib_comm) else {}
+    if rank != 0:
+        prof = {}
     out = dict(ms_per_step=elapsed / K * 1e3, value=K / elapsed, verified_iters=int(r.iters), verified=ok,
                n_local=n_k, prof=prof, D=s.D, sem_gen_s=t_gen, replicas_identical=replicas, comm=comm,
                W=Wf, cov=cov, steps_total=Wm + K)

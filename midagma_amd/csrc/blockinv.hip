@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "binv_tile.h"
+#include "kstamps.h"
 #include "launch.h"
 #include "nm16.h"
 
@@ -164,6 +165,7 @@ __device__ __forceinline__ void nm_resid_body(int wg, const double* __restrict__
   }
   constexpr int B2 = 4 * NW * L;
   const int nt = B2 / 16;
+  KS_DECL(ks);
   int m0, n0;
   nm_tile(wg, nt, xmap, m0, n0);
   if (wg == 0 && threadIdx.x == 0) *done = 0;
@@ -189,13 +191,19 @@ __device__ __forceinline__ void nm_resid_body(int wg, const double* __restrict__
   const int gi = m0 + row, gj = n0 + col;
   const int64_t e = (int64_t)gi * B2 + gj;
   if (elem) st_wt(Y0 + e, extrap ? 2.0 * P1[e] - P2[e] : P1[e]);
+#ifdef MIDAGMA_KSTAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stamps: operands and the warm start arrived)
+  KS_MARK(ks);
+#endif
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   splitk_mfma<L>(a, b, acc);
   const double sum = splitk_sum_w<NW>(acc, red);
+  KS_MARK(ks);
   if (!elem) return;
   const double r = (gi == gj ? 1.0 : 0.0) - sum;
   st_wt(Q0 + e, r);
   store_row_partial(abs_or_inf(r), part0, m0, n0, nt);
+  if (!FROM_W) KS_END(ks, KS_RESID);
 }
 
 template <int L, int NW = 4>
@@ -271,6 +279,7 @@ __global__ __launch_bounds__(64 * NW) void nm_pass_kernel(const double* __restri
   const int dn = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (dn != 0 && dn < pass) return;
   const int wg = blockIdx.x;
+  KS_DECL(ks);
   int m0, n0;
   nm_tile(wg, nt, xmap, m0, n0);
   // operands first: their latency overlaps the rho reduction (Y, Q are complete: the
@@ -285,6 +294,7 @@ __global__ __launch_bounds__(64 * NW) void nm_pass_kernel(const double* __restri
   const int gi = m0 + row, gj = n0 + col;
   const double yold = elem ? Y[(int64_t)gi * B2 + gj] : 0.0;
   const double rho = inf_norm<B2, 64 * NW>(part_prev, red4);
+  KS_MARK(ks);
   if (!(rho <= 0.25)) {  // warm start too far, diverging, or not finite
     if (wg == 0 && tid == 0) st->status = ST_NEED_GJ;
     return;
@@ -303,10 +313,12 @@ __global__ __launch_bounds__(64 * NW) void nm_pass_kernel(const double* __restri
   const double yq = splitk_sum_w<NW>(ay, red);
   __syncthreads();  // red reused
   const double qq = splitk_sum_w<NW>(aq, red);
+  KS_MARK(ks);
   if (!elem) return;
   st_wt(Yn + (int64_t)gi * B2 + gj, yold + yq);
   st_wt(Qn + (int64_t)gi * B2 + gj, qq);
   store_row_partial(abs_or_inf(qq), part_next, m0, n0, nt);
+  KS_END(ks, KS_PASS);
 }
 
 #ifdef MIDAGMA_EXPERIMENTS
@@ -656,10 +668,12 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
   const int job = xcd_spread(blockIdx.x, gridDim.x);
   const int64_t G0 = (int64_t)g0 * NB;
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  KS_DECL(ks);
   if (job < nu) {
     const int a = job / mb, cq = job % mb, c = cq < g0 ? cq : cq + gb;
     tile32_gemm_any(pf, P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, img[0], img[1],
                     img[2], img[3]);
+    KS_MARK(ks);
     double* out = Aout + (G0 + (int64_t)a * NB) * D + (int64_t)c * NB;
     int flag = 0;
     acc_foreach(acc, [&](int row, int col, double& v) {
@@ -667,10 +681,12 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
       flag |= domain_flag(v);
     });
     if (check && flag) atomicOr(&st->flags, flag);
+    KS_END(ks, KS_PANEL);
   } else if (job < 2 * nu) {
     const int j2 = job - nu, iq = j2 / gb, c = j2 % gb, i = iq < g0 ? iq : iq + gb;
     tile32_gemm_any(pf, Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, img[0], img[1],
                     img[2], img[3]);
+    KS_MARK(ks);
     double* out = Aout + (int64_t)i * NB * D + G0 + (int64_t)c * NB;
     int flag = 0;
     acc_foreach(acc, [&](int row, int col, double& v) {
@@ -678,6 +694,7 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
       flag |= domain_flag(-v);
     });
     if (check && flag) atomicOr(&st->flags, flag);
+    KS_END(ks, KS_PANEL);
   } else if (job >= 2 * nu + gb * gb) {  // look-ahead: LPZ = P LZ (next block's residual)
     const int j4 = job - 2 * nu - gb * gb, a = j4 / gb, c = j4 % gb;
     tile32_gemm_any(pf, P + (int64_t)a * NB * ldp, ldp, LZ + (int64_t)c * NB, B2, B2, acc, img[0], img[1], img[2],
@@ -713,7 +730,9 @@ __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __re
   const int job = xcd_spread(blockIdx.x, gridDim.x);
   const int gb = B2 / NB, mb = (int)(D / NB) - gb;
   if (job < mb * mb) {
+    KS_DECL(ks);
     binv_trail_tile(job, Ain, Aout, D, B2, g, check, st, pf, img[0], img[1], img[2], img[3]);
+    KS_END(ks, KS_TRAIL);
     return;
   }
   // R = I - (LW - A(gn, G) LPZ) on the 32 x 32 tile (a, c) of block gn; X0 -> Y0, |R| row partials
@@ -1034,3 +1053,16 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
 }
 
 }  // namespace midagma
+
+#ifdef MIDAGMA_KSTAMPS
+// Diagnostics (kstamps build): the phase sums (KS_KINDS x (KS_POINTS + 2) u64), then zeroed.
+extern "C" int midagma_debug_kstamps(unsigned long long* out) {
+  using namespace midagma;
+  const size_t bytes = sizeof(unsigned long long) * KS_KINDS * (KS_POINTS + 2);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kstamps), bytes) != hipSuccess) return -1;
+  static unsigned long long zero[KS_KINDS * (KS_POINTS + 2)] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_kstamps), zero, bytes) != hipSuccess) return -1;
+  return 0;
+}
+#endif

@@ -240,7 +240,7 @@ if __name__ == "__main__":
         for seq in ("exp", "inv", "log"):
             trek_case(1000, seq, 50)
     if which == "tcc":
-        for d, K in ((20, 2000), (100, 500), (300, 200), (1000, 50)):
+        for d, K in ((8, 2000), (20, 2000), (32, 2000), (100, 500), (300, 200)):
             trek_case(d, "tcc", K)
     if which == "shards":  # config 4's per-rank shard at N = 1, 2, 4, 8 GPUs, timed on one GPU
         for n, K in ((1_000_000, 10), (500_000, 20), (250_000, 40), (125_000, 80)):
