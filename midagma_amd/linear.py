@@ -76,8 +76,15 @@ class DagmaLinear:
                  comm: str | None = None, solver_factory=None) -> None:
         losses = ["l2", "logistic"]
         assert loss_type in losses, f"loss_type should be one of {losses}"
-        if dtype is not np.float64:
-            raise ValueError("the HIP inner solver computes in float64 only (as the reference's cov/X)")
+        # dtype (linear.py:29, 55): the type of Id, the exclusion mask and W_est (408, 220, 429).  The
+        # reference keeps W in that type through its in-place Adam updates while cov, the
+        # gradients and the inverse's products come out float64; here the loop computes in
+        # float64 and W is handed back in dtype after every minimize call, so a float32 fit
+        # agrees with the reference's float32 fit to within the reference's own float32 /
+        # float64 spread (tests/test_gpu_parity.py::test_full_fit_float32_dtype)
+        dtype = np.dtype(dtype).type
+        if dtype not in (np.float32, np.float64):
+            raise ValueError("dtype must be np.float64 or np.float32 (the solver computes in float64)")
         if trek_reg is not None and trek_reg.enabled() and str(trek_reg.name).lower().strip() not in ("pst", "tcc"):
             raise ValueError(f"Unknown trek regularizer: {trek_reg.name}. Has to be in ['pst', 'tcc']")
         self.loss_type = loss_type
@@ -280,6 +287,9 @@ class DagmaLinear:
         t0 = time.time()
         self.vprint(f'\n\nMinimize with -- mu:{mu} -- lr: {lr} -- s: {s} -- l1: {self.lambda1} '
                     f'for {max_iter} max iterations')
+        w_type = np.asarray(W).dtype.type
+        if w_type not in (np.float32, np.float64):
+            w_type = np.float64
         W = np.ascontiguousarray(W, dtype=np.float64)
         mask_inc, mask_exc = self._masks(mu)
         self._solver.set_masks(mask_inc, mask_exc)
@@ -307,7 +317,8 @@ class DagmaLinear:
                                       halvings=res.halvings, seconds=time.time() - t0))
         if pbar is not None:  # the reference ticks once per iteration (linear.py:329, 332)
             pbar.update(int(max_iter) if res.early_stop else res.iters)
-        return W, res.success
+        # the reference updates W in place (linear.py:275): the result keeps W's floating type
+        return (W.astype(w_type) if w_type is not np.float64 else W), res.success
 
     def fit(self, X: np.ndarray, lambda1: float = 0.03, w_threshold: float = 0.3, T: int = 5,
             mu_init: float = 1.0, mu_factor: float = 0.1,

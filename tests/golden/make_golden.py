@@ -264,6 +264,20 @@ def gen_fit_envelope(X, seeds=(7, 11, 13, 17, 19, 23, 29, 31)):
                         **{k: np.array(v, dtype=np.float64) for k, v in rows.items()})
 
 
+def gen_fit_f32(X):
+    """A shortened fit (T = 3) with dtype=np.float32 and the same fit with float64: the reference
+    keeps W in float32 through its in-place Adam updates (linear.py:275, 429), so the two runs
+    differ by float32 rounding; the pair bounds the dtype=float32 drop-in."""
+    out = {}
+    for tag, dt in (("f32", np.float32), ("f64", np.float64)):
+        m = DagmaLinear(loss_type="l2", verbose=False, dtype=dt)
+        W = m.fit(X.copy(), lambda1=0.03, T=3, s=[1.0, .9, .8], warm_iter=4000, max_iter=5000)
+        out[f"W_{tag}"] = W
+        out[f"h_final_{tag}"] = np.array(m.h_final)
+        out[f"score_final_{tag}"] = np.array(m.score_final)
+    np.savez_compressed(os.path.join(HERE, "fit_f32_d20.npz"), **out)
+
+
 def gen_trek():
     """PST trek regularizer value and gradient from the reference (notreks.trek_value_grad)
     for every seq and agg it offers, on a small in-domain W."""
@@ -399,6 +413,7 @@ def main():
         gen_branches(X20)
         gen_fit(X20)
         gen_fit_envelope(X20)
+        gen_fit_f32(X20)
         gen_trek()
         gen_tcc(X20)
         gen_mlp()
@@ -412,6 +427,6 @@ if __name__ == "__main__":
             X20 = np.load(os.path.join(HERE, "data_d20_n1000_seed0.npz"))["X"]
             for name in sys.argv[1:]:
                 fn = globals()[name]
-                fn(X20) if name in ("gen_tcc", "gen_mlp_traj") else fn()  # e.g. gen_traj_logistic_d100
+                fn(X20) if name in ("gen_tcc", "gen_mlp_traj", "gen_fit_f32") else fn()  # e.g. gen_traj_logistic_d100
     else:
         main()

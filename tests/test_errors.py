@@ -45,3 +45,14 @@ def test_abi_codes_map_to_reference_exceptions(monkeypatch):
     with pytest.raises(_lib.HipSolverError):
         _lib.check(_lib.E_HIP, None, "x")
     assert _lib.check(0) == 0
+
+
+def test_dtype_choices():
+    """dtype (linear.py:29): float64 and float32 are accepted (the loop computes in float64, W is
+    handed back in dtype); anything else is refused at construction, before any device call."""
+    from midagma_amd import DagmaLinear
+    assert DagmaLinear("l2", dtype=np.float32).dtype is np.float32
+    assert DagmaLinear("l2", dtype=np.dtype("float64")).dtype is np.float64
+    for bad in (np.float16, np.int64):
+        with pytest.raises(ValueError):
+            DagmaLinear("l2", dtype=bad)

@@ -180,6 +180,24 @@ def test_full_fit_d20(hip, golden, parity):
     assert abs(m.score_final - f["score_final"]) <= max(2 * env_s, 1e-9 * abs(float(f["score_final"])))
 
 
+def test_full_fit_float32_dtype(hip, golden):
+    """dtype=np.float32 (linear.py:29): the reference keeps W in float32 through its in-place Adam
+    updates, so its float32 and float64 fits differ by float32 rounding (fit_f32_d20.npz: T = 3,
+    max |dW| 1.6e-4, identical support).  The GPU loop computes in float64 and returns W in
+    float32: the support must be the reference's and W within twice the reference's own
+    float32 / float64 spread of its float32 fit, and within 1e-6 of its float64 fit."""
+    from midagma_amd import DagmaLinear
+    f = golden("fit_f32_d20.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    m = DagmaLinear("l2", dtype=np.float32)
+    W = m.fit(X, lambda1=0.03, T=3, s=[1.0, .9, .8], warm_iter=4000, max_iter=5000)
+    assert W.dtype == np.float32
+    spread = float(np.abs(f["W_f32"] - f["W_f64"]).max())
+    assert np.array_equal(W != 0, f["W_f32"] != 0)
+    assert np.abs(W - f["W_f32"]).max() <= 2 * spread
+    assert np.abs(W.astype(np.float64) - f["W_f64"]).max() <= 1e-6
+
+
 def test_full_fit_d1000_matches_reference_algorithm(hip, golden, parity):
     """BASELINE config 2 end to end: the default fit at d=1000, n=1e4 (ER(s0=d) Gaussian SEM,
     seed 0) against the oracle's run of the reference algorithm (fit_d1000_ref.npz, 2.5 h of
