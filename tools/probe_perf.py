@@ -242,6 +242,16 @@ if __name__ == "__main__":
     if which == "tcc":
         for d, K in ((8, 2000), (20, 2000), (32, 2000), (100, 500), (300, 200)):
             trek_case(d, "tcc", K)
+    if which == "tcc20":  # one size, for a kernel trace
+        trek_case(20, "tcc", 2000)
+    if which == "tccnb":  # the one-workgroup TCC at each block count it fits
+        for d, nbs in ((8, ("8", "16", "32")), (16, ("8", "16", "32")), (20, ("16", "32")), (32, ("16", "32")),
+                       (64, ("32",))):
+            for nb in nbs:
+                os.environ["MIDAGMA_EXP_TCC_NB"] = nb
+                print(f"MIDAGMA_EXP_TCC_NB={nb}", end=" ")
+                trek_case(d, "tcc", 2000)
+        os.environ.pop("MIDAGMA_EXP_TCC_NB")
     if which == "shards":  # config 4's per-rank shard at N = 1, 2, 4, 8 GPUs, timed on one GPU
         for n, K in ((1_000_000, 10), (500_000, 20), (250_000, 40), (125_000, 80)):
             data_case(1000, n, 2, K)
