@@ -61,6 +61,7 @@ def parse():
     p.add_argument("--no-large", action="store_true", help="skip the config 3 leg (d=5000, n=5e4, cov mode)")
     p.add_argument("--no-mlp", action="store_true", help="skip the config 5 leg (DagmaNonlinear, dims [200,10,1])")
     p.add_argument("--no-small", action="store_true", help="skip the config 1 leg (d=20, one persistent workgroup)")
+    p.add_argument("--no-tcc", action="store_true", help="skip the TCC trek-regularizer leg (SURVEY 8f-3, d=20)")
     p.add_argument("--mlp-steps", type=int, default=2000)
     p.add_argument("--large-d", type=int, default=5000)
     p.add_argument("--large-n", type=int, default=50_000)
@@ -542,6 +543,59 @@ def bench_small(args, device, with_cpu):
     return out
 
 
+def bench_tcc(args, device, with_cpu):
+    """the TCC trek regularizer inside the loop (notreks.trek_value_grad with its defaults:
+    spectral penalty, 'approx_trek_graph', Perron pairs of A = [[W o W, S], [I, (W o W)^T]]) at d=20,
+    config 1's data, 'opt' mode on 30 % of the upper pairs, weight 0.1: steps/s over 2000 Adam steps
+    (csrc/tcc.hip: the one-workgroup Noda / Gauss-Jordan kernel), the CPU oracle's step with the same
+    regularizer (numpy eig, as the reference) timed beside it, and a separate 200-step run from
+    W = 0 checked against the oracle."""
+    from midagma_amd.simulate import make_dataset
+    from midagma_amd.solver import HipSolver
+    d, n, K, Kc, weight = 20, 1000, 2000, 200, 0.1
+    X, _, _ = make_dataset(d, n, seed=args.seed)
+    Xc = X - X.mean(0, keepdims=True)
+    cov = Xc.T @ Xc / float(n)
+    rng = np.random.default_rng(args.seed)
+    iu = np.array(np.triu_indices(d, 1)).T
+    pairs = iu[rng.uniform(size=len(iu)) < 0.3]
+    s = HipSolver(d, "l2", "cov", device=device)
+    s.set_cov(cov)
+    s.set_trek_tcc(pairs, mode="opt", weight=weight)
+    s.begin(np.zeros((d, d)), 1.0, K + 100, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
+    s.run_slots(20)
+    s.sync()
+    t0 = time.perf_counter()
+    s.run_slots(K)
+    s.sync()
+    t1 = time.perf_counter()
+    r = s.poll()
+    Wc = np.zeros((d, d))
+    rc = s.minimize(Wc, 1.0, Kc, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=10 ** 9)
+    s.close()
+    ms = (t1 - t0) / K * 1e3
+    out = dict(value=K / (t1 - t0), unit="steps/s", ms_per_step=ms, steps=K,
+               verified=(r.status == 0 and r.iters == K + 20 and rc.iters == Kc),
+               workload=f"f3: cov-mode loop at d={d}, n={n} (config 1's data) with the TCC regularizer in 'opt' mode, "
+                        f"{len(pairs)} pairs (30 % of the upper triangle), weight {weight}, 1 GPU",
+               reference_ms_per_step={"value": 1.33, "source": "the reference's minimize with the same regularizer, "
+                                      "one thread, measured in the build container (DESIGN.md section 4)"})
+    out["_check"] = dict(W=Wc, cov=cov, pairs=pairs, K=Kc, weight=weight)
+    if with_cpu:
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "tcc.npz")
+            np.savez(path, cov=cov, pairs=pairs, weight=weight)
+            t = _cpu_runs("tcc", d, path, [1], steps=300)
+        if t:
+            th, v = _best(t)
+            out["cpu_baseline"] = dict(value=v, unit="steps/s", cores=th, kind="port", note=PORT_NOTE,
+                                       sample=f"oracle cov-mode Adam steps at d={d} with the TCC regularizer "
+                                              f"(numpy eig of A and A^T each step, as the reference): 300 steps, 1 thread")
+            out["vs_cpu"] = out["value"] / v
+    return out
+
+
 def bench_cov_large(args, device):
     """Config 3: d=5000, n=5e4, l2, cov mode on one GPU -- the inverse-dominated
     size.  X is generated and reduced to cov = X^T X / n on the GPU (torch plumbing: a CPU
@@ -622,6 +676,11 @@ if mode == "fit":                       # config 1: the whole default fit() (lin
 if mode == "cov":                       # the reference algorithm: cov precomputed once
     o = LinearOracle("l2")
     o.cov, o.X, o.n = np.load(extra), None, 10000
+elif mode == "tcc":                     # the reference algorithm with the TCC trek regularizer ('opt')
+    T = np.load(extra)
+    o = LinearOracle("l2")
+    o.cov, o.X, o.n = T["cov"], None, 10000
+    o.trek = dict(kind="tcc", pairs=T["pairs"], mode="opt", weight=float(T["weight"]))
 elif mode == "data":                    # the workload's math: -(mu/n) X^T (X (I - W)) per step
     n = int(extra)
     o = LinearOracle("l2", score_mode="data")
@@ -689,6 +748,17 @@ with threadpool_limits(limits=th):
         o._objective = lambda W, mu, s: (0.0, 0.0, 0.0)   # tol=-1: the objective decides nothing
         W, tr = o.minimize(np.zeros((d, d)), 1.0, int(P["K"]), 1.0, 3e-4, tol=-1.0)
         out = dict(W=W, iters=tr.iters, halvings=tr.halvings)
+    elif kind == "tcc":
+        from oracle.dagma_oracle import LinearOracle
+        o = LinearOracle("l2")
+        o.cov = P["cov"]
+        o.X, o.n = None, 1
+        d = o.cov.shape[0]
+        o.d, o.eye, o.lambda1, o.checkpoint, o.inc, o.exc = d, np.eye(d), float(P["lambda1"]), 10 ** 9, None, None
+        o.trek = dict(kind="tcc", pairs=P["pairs"], mode="opt", weight=float(P["weight"]))
+        o._objective = lambda W, mu, s: (0.0, 0.0, 0.0)   # tol=-1: the objective decides nothing
+        W, tr = o.minimize(np.zeros((d, d)), 1.0, int(P["K"]), 1.0, 3e-4, tol=-1.0)
+        out = dict(W=W, iters=tr.iters)
     elif kind == "fit":
         from oracle.dagma_oracle import LinearOracle
         o = LinearOracle("l2")
@@ -775,8 +845,16 @@ def logistic_check(c, threads=8):
             "oracle": "LinearOracle('logistic') and its 64-row blocked-sum variant (the reference's order envelope)"}
 
 
-def value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world, fit4=None):
+def value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world, fit4=None, tcc_res=None):
     """Every leg's value check (attached as `value_check`; `verified` requires it)."""
+    if tcc_res is not None and "_check" in tcc_res:
+        c = tcc_res.pop("_check")
+        out = oracle_run("tcc", {"cov": c["cov"], "pairs": c["pairs"], "K": c["K"], "weight": c["weight"],
+                                 "lambda1": 0.03}, threads=1)
+        tcc_res["value_check"] = w_check(c["W"], None if out is None else out["W"], 1e-9, c["K"],
+                                         "oracle minimize with the TCC regularizer (numpy eig Perron pairs, "
+                                         "oracle/trek_oracle.py), same steps from W = 0")
+
     if fit4 is not None and "_check" in fit4:
         c = fit4.pop("_check")
         vc = check_l2(c["W"], c["cov"], c["K"], "oracle reference algorithm on the fit's device-Gram cov, "
@@ -848,7 +926,7 @@ def value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world,
                                  "takes ~10 s); the n=1e4 leg checks the same kernels"}
         else:
             lg["value_check"] = logistic_check(c)
-    for leg in (cov_res, large_res, small_res, mlp_res):
+    for leg in (cov_res, large_res, small_res, mlp_res, tcc_res):
         if leg is not None and "value_check" in leg:
             leg["verified"] = bool(leg["verified"] and leg["value_check"]["ok"])
     if small_res is not None and "value_check" in small_res.get("fit", {}):
@@ -1089,6 +1167,9 @@ def main():
     small_res = None
     if rank == 0 and world == 1 and not args.no_small and args.workload == "data":
         small_res = bench_small(args, local, with_cpu=not args.no_cpu)
+    tcc_res = None
+    if rank == 0 and world == 1 and not args.no_tcc and args.workload == "data":
+        tcc_res = bench_tcc(args, local, with_cpu=not args.no_cpu)
     logi = None
     if rank == 0 and world == 1 and not args.no_logistic and args.workload == "data":
         logi = [bench_logistic(args, local, nn, args.logistic_steps if nn > 100_000 else 200)
@@ -1097,8 +1178,8 @@ def main():
     if args.workload == "data" and not args.no_fit4:
         fit4 = bench_fit_config4(args, world, rank, local, res["ms_per_step"] if res else None)
     if not args.no_check:
-        value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world, fit4)
-    for leg in (small_res, mlp_res, *(logi or [])):
+        value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world, fit4, tcc_res)
+    for leg in (small_res, mlp_res, tcc_res, *(logi or [])):
         if leg is not None:
             leg.pop("_check", None)
     cpu = None
@@ -1120,7 +1201,8 @@ def main():
         cov_out = None if cov_res is None else {k: v for k, v in cov_res.items()
                                                 if not isinstance(v, np.ndarray) and k not in ("cov", "_check")}
         print(json.dumps({"cov_mode": cov_out, "config3": out, "full_fit": fit_res, "config5": mlp_res,
-                          "config1": small_res, "logistic": logi, "full_fit_config4": fit4}), flush=True)
+                          "config1": small_res, "logistic": logi, "full_fit_config4": fit4,
+                          "tcc": tcc_res}), flush=True)
         return
     if rank == 0:
         d = args.d
@@ -1224,6 +1306,8 @@ def main():
             line["logistic"] = logi
         if small_res is not None:
             line["config1"] = small_res
+        if tcc_res is not None:
+            line["tcc"] = tcc_res
         if fit4 is not None:
             f4 = dict(fit4)
             f4.pop("_check", None)

@@ -720,6 +720,171 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
   }
 }
 
+// ---- panels on 64 x 64 tiles (B2 = 256, large D) ------------------------------------------------
+// The 32 x 32 panel tile reads a 32 x 256 and a 256 x 32 operand slab for 0.5 MFLOP (4 flop per
+// byte, one 16 x 16 accumulator per wave): at D = 5120 its 2496 workgroups take 34 us for 1.27
+// GFLOP (37 TF) against a 16 us MFMA floor.  The 64 x 64 tile gives each wave a 32 x 32 quadrant
+// (2 x 2 accumulators: twice the flops per byte) in 624 workgroups, one round at three per CU.
+constexpr int P64_AS = 34;  // A chunk image [64][32] (m-major; = 2 mod 32: conflict-free MFMA A reads)
+constexpr int P64_BS = 80;  // B chunk image [32][64] (= 16 mod 32: the two kq halves on disjoint banks)
+constexpr int P64_PF = 2;   // chunks in flight in registers ahead of the MFMAs
+
+// acc[i][j] += A(64 x 32) B(32 x 64) on this wave's 32 x 32 quadrant.  CHAINS: mma32's order per
+// accumulator (four k-chains per 32-deep chunk summed (c0 + c1) + (c2 + c3): bit-identical to
+// the 32 x 32 panel), else one chain per accumulator, the four accumulators interleaved (fewer
+// live registers)
+template <bool CHAINS>
+__device__ __forceinline__ void mma64x32(const double* __restrict__ As, const double* __restrict__ Bs,
+                                         dbl4 (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4, w = threadIdx.x >> 6;
+  const int m0 = (w >> 1) * 32, n0 = (w & 1) * 32;
+  if constexpr (CHAINS) {
+    const dbl4 z = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const double* La = As + (m0 + 16 * i + r) * P64_AS + kq;
+        const double* Rb = Bs + kq * P64_BS + n0 + 16 * j + r;
+        dbl4 c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[0], Rb[0], acc[i][j], 0, 0, 0);
+        dbl4 c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[4], Rb[4 * P64_BS], z, 0, 0, 0);
+        dbl4 c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[8], Rb[8 * P64_BS], z, 0, 0, 0);
+        dbl4 c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[12], Rb[12 * P64_BS], z, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[16], Rb[16 * P64_BS], c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[20], Rb[20 * P64_BS], c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[24], Rb[24 * P64_BS], c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(La[28], Rb[28 * P64_BS], c3, 0, 0, 0);
+        acc[i][j] = (c0 + c1) + (c2 + c3);
+      }
+  } else {
+    const double* La = As + (m0 + r) * P64_AS + kq;
+    const double* Rb = Bs + kq * P64_BS + n0 + r;
+#pragma unroll
+    for (int k = 0; k < 32; k += 4) {
+      const double a0 = La[k], a1 = La[16 * P64_AS + k];
+      const double b0 = Rb[k * P64_BS], b1 = Rb[k * P64_BS + 16];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+}
+
+// acc = A(64 x 256) B(256 x 64) (global, row-major): 32-deep chunks through one LDS image pair,
+// the next P64_PF chunks in registers (the operands come from the previous launch: MALL trips)
+template <bool CHAINS>
+__device__ __forceinline__ void tile64_gemm_k256(const double* __restrict__ A, int64_t lda,
+                                                 const double* __restrict__ B, int64_t ldb, dbl4 (&acc)[2][2],
+                                                 double* As, double* Bs) {
+  constexpr int NK = 8;
+  const int tid = threadIdx.x;
+  double2 ra[P64_PF][4], rb[P64_PF][4];
+  auto load = [&](double2 (&a)[4], double2 (&b)[4], int kc) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int item = it * NTHREADS + tid;
+      const int ar = item >> 4, ac = (item & 15) * 2;  // A chunk: 64 rows x 32
+      const int br = item >> 5, bc = (item & 31) * 2;  // B chunk: 32 rows x 64
+      a[it] = *reinterpret_cast<const double2*>(A + (int64_t)ar * lda + kc * 32 + ac);
+      b[it] = *reinterpret_cast<const double2*>(B + (int64_t)(kc * 32 + br) * ldb + bc);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int p = 0; p < P64_PF; ++p) load(ra[p], rb[p], p);
+  for (int kc = 0; kc < NK; ++kc) {
+    __syncthreads();  // the previous chunk's MFMAs are done with the images
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int item = it * NTHREADS + tid;
+      *reinterpret_cast<double2*>(As + (item >> 4) * P64_AS + (item & 15) * 2) = ra[0][it];
+      *reinterpret_cast<double2*>(Bs + (item >> 5) * P64_BS + (item & 31) * 2) = rb[0][it];
+    }
+#pragma unroll
+    for (int p = 0; p + 1 < P64_PF; ++p)
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        ra[p][it] = ra[p + 1][it];
+        rb[p][it] = rb[p + 1][it];
+      }
+    if (kc + P64_PF < NK) load(ra[P64_PF - 1], rb[P64_PF - 1], kc + P64_PF);
+    __syncthreads();
+    mma64x32<CHAINS>(As, Bs, acc);
+  }
+}
+
+template <class F>
+__device__ __forceinline__ void acc64_foreach(dbl4 (&acc)[2][2], F&& f) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m0 = (w >> 1) * 32, n0 = (w & 1) * 32;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) f(m0 + 16 * i + acc_row(lane, t), n0 + 16 * j + acc_col(lane), acc[i][j][t]);
+}
+
+// binv_panel_kernel's U, V and P outputs at B2 = 256 on 64 x 64 tiles (jobs: U (cq, a) with the
+// four row tiles of one column tile consecutive, V (iq, c), then the 16 P tiles); no look-ahead
+// CHAINS (experiments: MIDAGMA_EXP_P64_CHAINS=1): mma32's summation order, bit-identical to
+// binv_panel_kernel, at 2 workgroups per CU (its chains hold 186 VGPRs); the product runs one
+// chain per accumulator at 3 per CU (160 VGPRs), which rounds differently in the last bits
+template <bool CHAINS>
+__global__ __launch_bounds__(NTHREADS, CHAINS ? 2 : 3) void binv_panel64_kernel(const double* __restrict__ Ain,
+                                                                double* __restrict__ Aout, int64_t D, int g,
+                                                                const double* __restrict__ P, int64_t ldp,
+                                                                double* __restrict__ Pe, double* __restrict__ Po,
+                                                                const int* __restrict__ done, int check,
+                                                                State* __restrict__ st) {
+  constexpr int B2 = 256, GB = B2 / 64;
+  if (st && st->status != ST_RUNNING) return;
+  if (done && *done == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) double As[64 * P64_AS];
+  __shared__ __attribute__((aligned(16))) double Bs[32 * P64_BS];
+  const int nb = (int)(D / 64), g0 = g * GB, mb = nb - GB, nu = GB * mb;
+  const int job = xcd_spread(blockIdx.x, gridDim.x);
+  const int64_t G0 = (int64_t)g * B2;
+  int flag = 0;
+  if (job < 2 * nu) {
+    const bool u = job < nu;
+    const int j = u ? job : job - nu, q = j / GB, k = j % GB, t = q < g0 ? q : q + GB;
+    // U: rows 64 k of G times column tile t; V: row tile t times columns 64 k of G
+    const double* A = u ? P + (int64_t)k * 64 * ldp : Ain + (int64_t)t * 64 * D + G0;
+    const double* B = u ? Ain + G0 * D + (int64_t)t * 64 : P + (int64_t)k * 64;
+    double* out = u ? Aout + (G0 + (int64_t)k * 64) * D + (int64_t)t * 64 : Aout + (int64_t)t * 64 * D + G0 + k * 64;
+    dbl4 acc[2][2];
+    tile64_gemm_k256<CHAINS>(A, u ? ldp : D, B, u ? D : ldp, acc, As, Bs);
+    acc64_foreach(acc, [&](int row, int col, double v) {
+      const double o = u ? v : -v;
+      st_wt(out + (int64_t)row * D + col, o);
+      flag |= domain_flag(o);
+    });
+  } else if (job < 2 * nu + GB * GB) {
+    const int j3 = job - 2 * nu, a = j3 / GB, c = j3 % GB;
+    const double* src = P + (int64_t)a * 64 * ldp + c * 64;
+    double* out = Aout + (G0 + (int64_t)a * 64) * D + G0 + c * 64;
+    double* Pst = (st && (st->slots & 1)) ? Po : Pe;  // this slot's store (parity of k)
+    double* ps = Pst + (int64_t)a * 64 * B2 + c * 64;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int e = it * NTHREADS + threadIdx.x, row = e >> 6, col = e & 63;
+      const double v = src[(int64_t)row * ldp + col];
+      st_wt(out + (int64_t)row * D + col, v);
+      st_wt(ps + (int64_t)row * B2 + col, v);
+      flag |= domain_flag(v);
+    }
+  }
+  if (check && flag) atomicOr(&st->flags, flag);
+}
+
 // Trailing update of outer step g, one 32 x 32 tile per workgroup (binv_trail_tile).
 // With la.LW: the next block's residual tiles follow the mb x mb trailing tiles (TrailLA).
 __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __restrict__ Ain,
@@ -763,6 +928,13 @@ __global__ __launch_bounds__(NTHREADS) void binv_trail_kernel(const double* __re
 // (D - B2) from which the trailing update runs on the 128-tile GEMM: (D - B2)/128 >= 14
 // gives >= 196 workgroups
 static const int64_t TRAIL128_MIN = knob("MIDAGMA_EXP_TRAIL128", 1792);
+
+// D from which the panels of B2 = 256 run on 64 x 64 tiles (binv_panel64_kernel; experiment knob
+// MIDAGMA_EXP_PANEL64_MIN, e.g. 1000000 for the 32 x 32 panel everywhere)
+static int64_t panel64_min() {
+  static const int64_t m = knob("MIDAGMA_EXP_PANEL64_MIN", 2048);
+  return m;
+}
 
 int binv_block(int64_t D) {
   // D = 128 (64 < d <= 128): one outer block, so the fast slot's whole inverse is the warm-started
@@ -1027,6 +1199,12 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
                          Ain, Aout, D, g, P, Pe, Po, done, check, st);
     } else
 #endif
+    if (B2 == 256 && !ahead && D >= panel64_min()) {
+      const int m64 = (int)(D / 64) - 4;
+      static const bool chains = knob("MIDAGMA_EXP_P64_CHAINS", 0) != 0;
+      hipLaunchKernelGGL(chains ? binv_panel64_kernel<true> : binv_panel64_kernel<false>, dim3(2 * 4 * m64 + 16),
+                         dim3(NTHREADS), 0, stream, Ain, Aout, D, g, P, ldp, Pe, Po, done, check, st);
+    } else
     hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb * (ahead ? 2 : 1)), dim3(NTHREADS), 0, stream,
                        Ain, Aout, D, B2, g, P, ldp, Pe, Po, done, check, st, t32_pf(), ahead ? bw.LZ : nullptr,
                        ahead ? bw.LPZ : nullptr);

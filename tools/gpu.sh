@@ -12,7 +12,7 @@
 #   rehearse2             bench.py --gpus 2 with both ranks on cuda:0 over gloo (the N > 1 path end to end on
 #                         a one-GPU box; not a scaling number) -> gpurun_out/rehearse2.json
 #   prof LEG              rocprofv3 --kernel-trace --stats of one bench leg -> gpurun_out/prof_LEG/
-#                         LEG: data | cov | large | small | logistic | mlp | fit4 (one bench leg each)
+#                         LEG: data | cov | large | small | logistic | mlp | fit4 | tcc (one bench leg each)
 #   pmc LEG               FETCH_SIZE and WRITE_SIZE passes (each its own run) of one leg,
 #                         summarised per kernel -> gpurun_out/pmc_LEG.json (tools/pmc_summary.py)
 #   probe NAME [ARGS]     python tools/NAME.py ARGS (probe_perf, peak_probe, blocked_debug, ...); probe_perf
@@ -24,7 +24,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 
 leg_args() {
-  local skip="--no-cpu --no-check --no-fit --no-fit4 --no-cov --no-large --no-mlp --no-logistic --no-small"
+  local skip="--no-cpu --no-check --no-fit --no-fit4 --no-cov --no-large --no-mlp --no-logistic --no-small --no-tcc"
   case "$1" in
     data)     echo "--steps 5 --warmup 1 ${skip}" ;;
     cov)      echo "--workload cov --cov-steps 2000 --no-cpu --no-check --no-fit --no-fit4 --no-large" ;;
@@ -33,6 +33,7 @@ leg_args() {
     mlp)      echo "--no-data ${skip/--no-mlp/}" ;;
     logistic) echo "--no-data ${skip/--no-logistic/}" ;;
     small)    echo "--no-data ${skip/--no-small/}" ;;
+    tcc)      echo "--no-data ${skip/--no-tcc/}" ;;
     *) return 1 ;;
   esac
 }

@@ -242,6 +242,9 @@ if __name__ == "__main__":
     if which == "tcc":
         for d, K in ((8, 2000), (20, 2000), (32, 2000), (100, 500), (300, 200)):
             trek_case(d, "tcc", K)
+    if which == "large3":  # the large-D cov slots (run once per knob setting: the knobs are read once)
+        for d, K in ((2000, 300), (3000, 100), (5000, 40)):
+            cov_case(d, d + 1000, 3, K)
     if which == "tcc20":  # one size, for a kernel trace
         trek_case(20, "tcc", 2000)
     if which == "tccnb":  # the one-workgroup TCC at each block count it fits
