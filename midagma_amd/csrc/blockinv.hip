@@ -31,73 +31,13 @@
 #include "kstamps.h"
 #include "launch.h"
 #include "nm16.h"
+#include "nm_series.h"
 
 namespace midagma {
 
 namespace {
 
 
-
-template <int L>
-__device__ __forceinline__ void splitk_load_a(const double* __restrict__ A, int64_t lda, int m0, double (&a)[L]) {
-  const double* ap = A + (int64_t)(m0 + (threadIdx.x & 15)) * lda + splitk_k0<L>();
-#pragma unroll
-  for (int q = 0; q < L; ++q) a[q] = ap[q];
-}
-template <int L>
-__device__ __forceinline__ void splitk_load_b(const double* __restrict__ B, int64_t ldb, int n0, double (&b)[L]) {
-  const double* bp = B + (int64_t)splitk_k0<L>() * ldb + n0 + (threadIdx.x & 15);
-#pragma unroll
-  for (int q = 0; q < L; ++q) b[q] = bp[(int64_t)q * ldb];
-}
-
-// splitk_load_a of S = (sI - W∘W)^T[0:B2, 0:B2] (outer block 0) computed from W itself:
-// S[i][k] = (k == i ? s : 0) - W[k][i]^2, identity in the padding -- build_at's values, bit for bit
-// (build_at_tile), so block 0's residual can run in build_at's launch (build_resid0_kernel)
-template <int L>
-__device__ __forceinline__ void splitk_load_a_w(const double* __restrict__ W, int64_t ldw, int64_t d, double s,
-                                                int m0, double (&a)[L]) {
-  const int64_t i = m0 + (threadIdx.x & 15), k0 = splitk_k0<L>();
-#pragma unroll
-  for (int q = 0; q < L; ++q) {
-    const int64_t k = k0 + q;
-    if (i < d && k < d) {
-      const double x = W[k * ldw + i];
-      const double f = x * x;
-      a[q] = (k == i ? s : 0.0) - f;
-    } else {
-      a[q] = (k == i) ? 1.0 : 0.0;
-    }
-  }
-}
-
-// Row partial of |Q| over this tile's 16 columns -> rowpart[(m0 + row) * NT + tile column]
-__device__ __forceinline__ void store_row_partial(double a, double* __restrict__ rowpart, int m0, int n0, int NT) {
-  a = row_sum16(a);
-  int row, col;
-  tile_elem(threadIdx.x, row, col);
-  if (col == 0) rowpart[(int64_t)(m0 + row) * NT + n0 / 16] = a;
-}
-
-template <int B2, int NTH = NTHREADS>
-__device__ __forceinline__ double inf_norm(const double* __restrict__ rowpart, float* red4) {
-  return inf_norm_rows<B2, NTH>([&](int i) { return rowpart[i]; }, red4);
-}
-
-// The warm start X0 of a block (see nm_resid_kernel) as the B operand of a split-K tile
-template <int L>
-__device__ __forceinline__ void load_x0_b(const double* __restrict__ Pe, const double* __restrict__ Po,
-                                          const State* __restrict__ st, int n0, double (&b)[L]) {
-  constexpr int B2 = 16 * L;
-  const bool odd = (st->slots & 1) != 0;
-  splitk_load_b<L>(odd ? Pe : Po, B2, n0, b);
-  if (st->warm_run >= 2) {
-    double b2[L];
-    splitk_load_b<L>(odd ? Po : Pe, B2, n0, b2);
-#pragma unroll
-    for (int q = 0; q < L; ++q) b[q] = 2.0 * b[q] - b2[q];
-  }
-}
 
 // Look-ahead residual of the next outer block gn = g + 1 (fast path).  With X0 its warm start
 // and S = A(gn,gn) - A(gn,G) P_g A(G,gn) the Schur complement the trailing update of step g
@@ -122,89 +62,6 @@ struct TrailLA {  // trailing-launch extra tiles
   int* done;
   int gn;
 };
-
-// Tile of workgroup wg in a series launch over an nt x nt grid of 16 x 16 tiles.  xmap (256-wide
-// blocks, nt = 16): the 32 workgroups the dispatcher puts on one XCD (wg, wg + 8, ...) take a
-// 4 x 8 block of tiles, so that XCD's L2 serves 4 row bands and 8 column bands of the operands
-// instead of all 16 row bands (row-major order: every XCD read the whole of Y and Q)
-__device__ __forceinline__ void nm_tile(int wg, int nt, int xmap, int& m0, int& n0) {
-  int t = wg;
-  if (xmap && nt == 16) {
-    const int x = wg & 7, l = wg >> 3;
-    t = (4 * (x >> 1) + (l >> 3)) * 16 + 8 * (x & 1) + (l & 7);
-  }
-  m0 = (t / nt) * 16;
-  n0 = (t % nt) * 16;
-}
-
-// X0 = the warm start of this block: with two consecutive stored slots (st->warm_run >= 2)
-// the linear extrapolation 2 P1 - P2 of the last two inverses (P1 = slot k-1's, P2 = slot
-// k-2's, by the parity of k = st->slots), else P1.  Adam moves W smoothly (beta1 = 0.99), so
-// the extrapolation leaves a residual ~100x smaller than P1 alone (2 product-form passes
-// instead of 3 at d = 1000, measured on the default fit).
-// R = I - S X0 (tile (m0, n0) of the B2 x B2 block), row partials of |R| -> part0; the
-// workgroup also writes its tile of X0 -> Y0 (the first pass's iterate).
-// NW waves split K (B2 = 4 NW L): NW = 4 for B2 <= 256; B2 = 512 runs NW = 8 with L = 16, so
-// the per-lane operand runs and registers stay those of the 256-wide kernel
-// Body of the residual launch for workgroup wg; FROM_W: S from W (outer block 0, SW = {W, ldw,
-// d, s}) instead of the At block S (lds)
-struct SFromW {
-  const double* W;
-  int64_t ldw, d;
-  const Params* pr;
-};
-template <int L, int NW, bool FROM_W>
-__device__ __forceinline__ void nm_resid_body(int wg, const double* __restrict__ S, int64_t lds, const SFromW& sw,
-                                              const double* __restrict__ Pe, const double* __restrict__ Po,
-                                              double* __restrict__ Y0, double* __restrict__ Q0,
-                                              double* __restrict__ part0, int* __restrict__ done,
-                                              State* __restrict__ st, int xmap, double* red) {
-  if (st->ckpt_pending) {  // a log-det is due: pivots come from the slow path only
-    if (wg == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
-    return;
-  }
-  constexpr int B2 = 4 * NW * L;
-  const int nt = B2 / 16;
-  KS_DECL(ks);
-  int m0, n0;
-  nm_tile(wg, nt, xmap, m0, n0);
-  if (wg == 0 && threadIdx.x == 0) *done = 0;
-  const bool odd = (st->slots & 1) != 0;
-  const double* P1 = odd ? Pe : Po;  // slot k-1
-  const double* P2 = odd ? Po : Pe;  // slot k-2
-  const bool extrap = st->warm_run >= 2;
-  double a[L], b[L];
-  if (FROM_W)
-    splitk_load_a_w<L>(sw.W, sw.ldw, sw.d, sw.pr->s, m0, a);
-  else
-    splitk_load_a<L>(S, lds, m0, a);
-  splitk_load_b<L>(P1, B2, n0, b);
-  if (extrap) {
-    double b2[L];
-    splitk_load_b<L>(P2, B2, n0, b2);
-#pragma unroll
-    for (int q = 0; q < L; ++q) b[q] = 2.0 * b[q] - b2[q];
-  }
-  int row, col;
-  const bool elem = threadIdx.x < 256;  // the tile's 256 elements (NW > 4: the other waves only sum)
-  tile_elem(elem ? threadIdx.x : 0, row, col);
-  const int gi = m0 + row, gj = n0 + col;
-  const int64_t e = (int64_t)gi * B2 + gj;
-  if (elem) st_wt(Y0 + e, extrap ? 2.0 * P1[e] - P2[e] : P1[e]);
-#ifdef MIDAGMA_KSTAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (stamps: operands and the warm start arrived)
-  KS_MARK(ks);
-#endif
-  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  splitk_mfma<L>(a, b, acc);
-  const double sum = splitk_sum_w<NW>(acc, red);
-  KS_MARK(ks);
-  if (!elem) return;
-  const double r = (gi == gj ? 1.0 : 0.0) - sum;
-  st_wt(Q0 + e, r);
-  store_row_partial(abs_or_inf(r), part0, m0, n0, nt);
-  if (!FROM_W) KS_END(ks, KS_RESID);
-}
 
 template <int L, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restrict__ S, int64_t lds,
@@ -246,7 +103,7 @@ __global__ __launch_bounds__(NTHREADS) void build_resid0_kernel(const double* __
 
 // Pass p: rho = ||Q||_inf from the previous launch's row partials; converged -> P = Y + Y Q
 // (done = p), else Y' = Y + Y Q, Q' = Q Q and the row partials of |Q'|.  Far or diverging
-// -> ST_NEED_GJ.
+// -> ST_NEED_GJ.  (Tile body: nm_pass_body, nm_series.h.)
 template <int L, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void nm_pass_kernel(const double* __restrict__ Y,
                                                           const double* __restrict__ Q, double* __restrict__ Yn,
@@ -274,51 +131,7 @@ __global__ __launch_bounds__(64 * NW) void nm_pass_kernel(const double* __restri
     st_wt(la.out + (int64_t)(m0 + row) * B2 + n0 + col, sum);
     return;
   }
-  // an EARLIER pass converged (done holds its number; this pass's own workgroups may store
-  // theirs meanwhile, which must not make a sibling skip its tile of P)
-  const int dn = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (dn != 0 && dn < pass) return;
-  const int wg = blockIdx.x;
-  KS_DECL(ks);
-  int m0, n0;
-  nm_tile(wg, nt, xmap, m0, n0);
-  // operands first: their latency overlaps the rho reduction (Y, Q are complete: the
-  // previous launch wrote them)
-  double aY[L], aQ[L], bQ[L];
-  splitk_load_a<L>(Y, B2, m0, aY);
-  splitk_load_b<L>(Q, B2, n0, bQ);
-  splitk_load_a<L>(Q, B2, m0, aQ);
-  int row, col;
-  const bool elem = tid < 256;  // the tile's 256 elements (NW > 4: the other waves only sum)
-  tile_elem(elem ? tid : 0, row, col);
-  const int gi = m0 + row, gj = n0 + col;
-  const double yold = elem ? Y[(int64_t)gi * B2 + gj] : 0.0;
-  const double rho = inf_norm<B2, 64 * NW>(part_prev, red4);
-  KS_MARK(ks);
-  if (!(rho <= 0.25)) {  // warm start too far, diverging, or not finite
-    if (wg == 0 && tid == 0) st->status = ST_NEED_GJ;
-    return;
-  }
-  dbl4 ay = {0.0, 0.0, 0.0, 0.0};
-  if (rho <= 1e-8) {  // last factor: P = Y (I + Q)
-    splitk_mfma<L>(aY, bQ, ay);
-    const double yq = splitk_sum_w<NW>(ay, red);
-    if (elem) st_wt(P + (int64_t)gi * B2 + gj, yold + yq);
-    if (wg == 0 && tid == 0) __hip_atomic_store(done, pass, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  dbl4 aq = {0.0, 0.0, 0.0, 0.0};
-  splitk_mfma<L>(aY, bQ, ay);
-  splitk_mfma<L>(aQ, bQ, aq);
-  const double yq = splitk_sum_w<NW>(ay, red);
-  __syncthreads();  // red reused
-  const double qq = splitk_sum_w<NW>(aq, red);
-  KS_MARK(ks);
-  if (!elem) return;
-  st_wt(Yn + (int64_t)gi * B2 + gj, yold + yq);
-  st_wt(Qn + (int64_t)gi * B2 + gj, qq);
-  store_row_partial(abs_or_inf(qq), part_next, m0, n0, nt);
-  KS_END(ks, KS_PASS);
+  nm_pass_body<L, NW>(blockIdx.x, Y, Q, Yn, Qn, P, part_prev, part_next, done, pass, st, xmap, red, red4);
 }
 
 #ifdef MIDAGMA_EXPERIMENTS
@@ -637,6 +450,13 @@ __global__ __launch_bounds__(NTHREADS, 1) void panel5_kernel(const double* __res
 
 #endif  // MIDAGMA_EXPERIMENTS
 
+// the next block's series counters (launch_trail128_series), zeroed by the panel launch before
+// the trailing update that runs that series: [0] diagonal tiles, [32 p] phase p (p <= NM_PASSES)
+__device__ __forceinline__ void zero_sync(int* zsync) {
+  if (zsync && blockIdx.x == 0 && threadIdx.x <= NM_PASSES)
+    __hip_atomic_store(zsync + 32 * threadIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // prefetch depth of the panel / trailing tiles (experiment knob MIDAGMA_EXP_T32_PF: 1, 2, 3;
 // d=1000 fast slot: 4160 steps/s at 1, 4340 at 3, two runs each)
 static int t32_pf() {
@@ -656,8 +476,9 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
                                                               const int* __restrict__ done, int check,
                                                               State* __restrict__ st, int pf,
                                                               const double* __restrict__ LZ,
-                                                              double* __restrict__ LPZ) {
+                                                              double* __restrict__ LPZ, int* __restrict__ zsync) {
   if (st && st->status != ST_RUNNING) return;
+  zero_sync(zsync);
   if (done && *done == 0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
     return;
@@ -840,9 +661,10 @@ __global__ __launch_bounds__(NTHREADS, CHAINS ? 2 : 3) void binv_panel64_kernel(
                                                                 const double* __restrict__ P, int64_t ldp,
                                                                 double* __restrict__ Pe, double* __restrict__ Po,
                                                                 const int* __restrict__ done, int check,
-                                                                State* __restrict__ st) {
+                                                                State* __restrict__ st, int* __restrict__ zsync) {
   constexpr int B2 = 256, GB = B2 / 64;
   if (st && st->status != ST_RUNNING) return;
+  zero_sync(zsync);
   if (done && *done == 0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
     return;
@@ -934,6 +756,13 @@ static const int64_t TRAIL128_MIN = knob("MIDAGMA_EXP_TRAIL128", 1792);
 static int64_t panel64_min() {
   static const int64_t m = knob("MIDAGMA_EXP_PANEL64_MIN", 2048);
   return m;
+}
+
+// workgroups that run the next block's series inside a trailing update (launch_trail128_series;
+// experiment knob MIDAGMA_EXP_TRAIL_SERIES: 0 keeps the series launches)
+static int trail_series_workers() {
+  const int w = (int)knob("MIDAGMA_EXP_TRAIL_SERIES", 0);  // read at each enqueue (graph capture)
+  return w > 0 ? (w + 7) / 8 * 8 : 0;
 }
 
 int binv_block(int64_t D) {
@@ -1099,7 +928,7 @@ static bool blocked_inverse_lookahead(double* Mt, int64_t D, int B2, const BInvW
       launch_neumann<8>(Ain, D, G0, bw, g, st, passes, true, nullptr, side);
     const int check = g == K2 - 1;
     hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, side, Ain, Aout, D, B2, g,
-                       bw.P, (int64_t)B2, Pe, Po, bw.done + g, check, st, t32_pf(), nullptr, nullptr);
+                       bw.P, (int64_t)B2, Pe, Po, bw.done + g, check, st, t32_pf(), nullptr, nullptr, nullptr);
     if (g < K2 - 1) {
       HIP_TRY(hipEventRecord(ev[1 + 2 * g], side));
       HIP_TRY(hipStreamWaitEvent(stream, ev[1 + 2 * g], 0));
@@ -1147,6 +976,8 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
   bufs[1] = bufs[0] == Mt ? bw.Aalt : Mt;
   // look-ahead residual (NmLA / TrailLA): fast path with 32 x 32 trailing updates
   const bool look = fast && bw.LW && K2 > 1 && D - B2 < TRAIL128_MIN && resid_lookahead();
+  // blocks 1 .. K2 - 1's series inside the previous step's trailing update (128-tile updates)
+  const bool tser = fast && bw.sync && B2 == 256 && K2 > 1 && D - B2 >= TRAIL128_MIN && trail_series_workers() > 0;
   for (int g = 0; g < K2; ++g) {
     double* Ain = bufs[g & 1];
     double* Aout = bufs[(g + 1) & 1];
@@ -1168,6 +999,7 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     }
     if (fast) {
       const bool resid = (!look || g == 0) && !(g == 0 && resid0_done);  // (block 0: launch_build_resid0)
+      const bool own = !(tser && g > 0);  // else the series ran in trailing update g - 1
 #ifdef MIDAGMA_EXPERIMENTS
       if (B2 == 512 && !ahead && resid && nm5_on())
         launch_neumann5(Ain, D, G0, bw, g, st, passes, stream);
@@ -1175,8 +1007,10 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
 #endif
       if (B2 == 512)
         launch_neumann<16, 8>(Ain, D, G0, bw, g, st, passes, resid, ahead ? la : nullptr, stream);
-      else if (B2 == 256)
+      else if (B2 == 256 && own)
         launch_neumann<16>(Ain, D, G0, bw, g, st, passes, resid, ahead ? la : nullptr, stream);
+      else if (B2 == 256) {
+      }
       else
         launch_neumann<8>(Ain, D, G0, bw, g, st, passes, resid, ahead ? la : nullptr, stream);
       P = bw.P;
@@ -1192,6 +1026,8 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
     }
     // the fast slot takes the domain flags from the last outer step's outputs (no reduce_check)
     const int check = fast && g == K2 - 1;
+    const bool ser_next = tser && g + 1 < K2;  // trailing update g runs block g + 1's series
+    int* zsync = ser_next ? bw.sync + (int64_t)(g + 1) * 256 : nullptr;
 #ifdef MIDAGMA_EXPERIMENTS
     if (B2 == 512 && fast && !ahead && nm5_on()) {
       const int jobs = 2 * NT5 * (int)(D / 32 - NT5);
@@ -1203,17 +1039,23 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
       const int m64 = (int)(D / 64) - 4;
       static const bool chains = knob("MIDAGMA_EXP_P64_CHAINS", 0) != 0;
       hipLaunchKernelGGL(chains ? binv_panel64_kernel<true> : binv_panel64_kernel<false>, dim3(2 * 4 * m64 + 16),
-                         dim3(NTHREADS), 0, stream, Ain, Aout, D, g, P, ldp, Pe, Po, done, check, st);
+                         dim3(NTHREADS), 0, stream, Ain, Aout, D, g, P, ldp, Pe, Po, done, check, st, zsync);
     } else
     hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb * (ahead ? 2 : 1)), dim3(NTHREADS), 0, stream,
                        Ain, Aout, D, B2, g, P, ldp, Pe, Po, done, check, st, t32_pf(), ahead ? bw.LZ : nullptr,
-                       ahead ? bw.LPZ : nullptr);
+                       ahead ? bw.LPZ : nullptr, zsync);
     if (mb > 0) {
       // large D: 128 x 128 tiles (operand reuse; enough tiles to fill the chip), else 32 x 32
       if (D - B2 >= TRAIL128_MIN) {
         if (fuse && fast && g == K2 - 1 && gemm_trail_supported(*fuse)) {
           launch_gemm_trail(*fuse, Ain, Aout, D, B2, g, check, st, t32_pf(), -1, stream);
           fused = true;
+        } else if (ser_next) {
+          const int64_t gn = g + 1;
+          TrailSeries ts{bw.Pst + gn * B2 * B2, bw.Pst1 + gn * B2 * B2, {bw.Y[0], bw.Y[1]}, {bw.Q[0], bw.Q[1]}, bw.P,
+                         bw.part + gn * (NM_PASSES + 1) * PART_STRIDE, bw.done + gn, zsync,
+                         std::min(passes, NM_PASSES), nm_xmap(), trail_series_workers()};
+          launch_trail128_series(Ain, Aout, D, g, check != 0, st, ts, stream);
         } else {
           launch_trail128(Ain, Aout, D, B2, g, check, st, stream);
         }

@@ -8,12 +8,15 @@
 // LDS in conflict-free images (mfma64.h); I - W is formed while staging B, the
 // sigmoid and the logistic loss are fused into the epilogue.  Long K (= rows of
 // the shard) is split over blockIdx.z into fixed slices summed in fixed order.
+#include <algorithm>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "binv_tile.h"
 #include "launch.h"
 #include "mfma64.h"
+#include "nm_series.h"
 
 namespace midagma {
 
@@ -1048,6 +1051,172 @@ static void launch_trail128_epi(const double* Ain, double* Aout, int64_t D, int6
 void launch_trail128(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check, const State* st,
                      hipStream_t stream) {
   launch_trail128_epi(Ain, Aout, D, B2, g, check, st, stream, trail_mid());
+}
+
+// ---- the trailing update with the next block's series in the same launch (large D) ---------
+// At d = 5000 the 19 trailing updates of a slot (1444 tiles, 2.8 rounds, ~194 us each) are
+// followed by block g + 1's series: a residual and two pass launches of 256 workgroups, each
+// 6-7 us of mostly operand latency (0.4 ms a slot).  The series needs only block g + 1's
+// diagonal, which the trailing update writes in four of its tiles; those run first, and the
+// series runs on `workers` workgroups placed after the first round of tiles (they start as the
+// first tiles finish, when the diagonal is ready), beside the rest of the update.
+struct TrailSeriesArgs {
+  const double* Ain;
+  double* Aout;
+  int64_t D;
+  int g, check, tm, woff;
+  int diag[4];                    // slots 0..3: block g + 1's diagonal tiles
+  int exc_slot[4], exc_tile[4];   // the other slots whose tile is not xcd_remap's (-1: none)
+  TrailSeries ts;
+  State* st;
+};
+
+constexpr uint64_t TS_TIMEOUT = 5000000;  // device real-time ticks (100 MHz): 50 ms
+
+// lane 0 polls the counter (relaxed agent loads) until it reaches `target` or the time runs out;
+// then one agent acquire, its wait, and the barrier (MI355X_MICROARCH.md: Consumer, always)
+__device__ __forceinline__ bool ts_wait(const int* ctr, int target, int* go) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int ok = 0;
+    for (;;) {
+      if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+        ok = 1;
+        break;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > TS_TIMEOUT) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *go = ok;
+  }
+  __syncthreads();
+  return *go != 0;
+}
+// every wave's stores drained, the barrier, then lane 0: agent release and one counter add
+__device__ __forceinline__ void ts_signal(int* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// a bounded wait ran out: the slot goes back to the host's pivoted path (every later launch of
+// the slot is a no-op; P and *done of this series are not used), and sync[224] counts it
+__device__ __forceinline__ void ts_abort(const TrailSeriesArgs& a) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&a.st->status, (int32_t)ST_NEED_GJ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(a.ts.sync + 224, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// worker w of the series of block g + 1: tiles w, w + workers, ... of each phase (nm_tile's
+// XCD placement holds: workers is a multiple of 8 and woff too)
+__device__ void ts_worker(const TrailSeriesArgs& a, int w, double* smem) {
+  const TrailSeries& s = a.ts;
+  double* red = smem;
+  float* red4 = reinterpret_cast<float*>(smem + 4 * 256);
+  int* go = reinterpret_cast<int*>(smem + 4 * 256 + 4);
+  const int64_t GN0 = (int64_t)(a.g + 1) * 256;
+  if (!ts_wait(s.sync, 4, go)) return ts_abort(a);
+  const double* S = a.Aout + GN0 * a.D + GN0;
+  for (int wg = w; wg < 256; wg += s.workers) {
+    __syncthreads();  // red is reused by consecutive tiles
+    nm_resid_body<16, 4, false>(wg, S, a.D, SFromW{}, s.Pe, s.Po, s.Y[0], s.Q[0], s.part, s.done, a.st, s.xmap, red);
+  }
+  for (int p = 1; p <= s.passes; ++p) {
+    ts_signal(s.sync + 32 * p);
+    if (!ts_wait(s.sync + 32 * p, s.workers, go)) return ts_abort(a);
+    for (int wg = w; wg < 256; wg += s.workers) {
+      __syncthreads();
+      nm_pass_body<16, 4>(wg, s.Y[(p - 1) & 1], s.Q[(p - 1) & 1], s.Y[p & 1], s.Q[p & 1], s.P,
+                          s.part + (int64_t)(p - 1) * PART_STRIDE, s.part + (int64_t)p * PART_STRIDE, s.done, p,
+                          a.st, s.xmap, red, red4);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS, 2) void trail_series_kernel(TrailSeriesArgs a) {
+  if (a.st->status != ST_RUNNING) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x, nw = a.ts.workers;
+  if (b >= a.woff && b < a.woff + nw) {
+    ts_worker(a, b - a.woff, smem);
+    return;
+  }
+  const int s = b < a.woff ? b : b - nw, ntiles = a.tm * a.tm;
+  int t = s < 4 ? a.diag[s] : xcd_remap(s, ntiles);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (s == a.exc_slot[k]) t = a.exc_tile[k];
+  const int64_t G0 = (int64_t)a.g * 256;
+  gemm_pipe_tile<0, B_PLAIN, EPI_SUB_MID>(t, 256, 256, a.tm, a.tm, a.Ain + G0, a.D, a.Aout + G0 * a.D, a.D, a.Aout,
+                                          a.D, (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, 2, a.st, smem);
+  if (s < 4) ts_signal(a.ts.sync);  // block g + 1's diagonal tile is in Aout
+}
+
+// linear index of tile (bm, bn) (pivot band skipped) in gemm_pipe_tile's order for tm x tm tiles
+static int pipe_tile_index(int bm, int bn, int tm) {
+  if (tm > 8) {
+    const int fm = (bm / 8) * 8, rows = tm - fm < 8 ? tm - fm : 8;
+    return fm * tm + bn * rows + (bm - fm);
+  }
+  return bm * tm + bn;
+}
+static int host_xcd_remap(int w, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = w % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
+}
+
+void launch_trail128_series(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, State* st,
+                            const TrailSeries& ts, hipStream_t stream) {
+  if (D % 128) throw std::invalid_argument("launch_trail128_series: D must be a multiple of 128");
+  const int tm = (int)((D - 256) / 128), K2 = (int)(D / 256);
+  if (g + 1 >= K2 || tm < 4 || ts.workers <= 0 || ts.workers % 8 || ts.passes < 1 || ts.passes > NM_PASSES)
+    throw std::invalid_argument("launch_trail128_series: needs a next block, workers a multiple of 8, 1..4 passes");
+  check_mid_shape(256, 256, (int64_t)tm * tm, (int64_t)tm * tm, "launch_trail128_series");
+  const int ntiles = tm * tm;
+  TrailSeriesArgs a{};
+  a.Ain = Ain;
+  a.Aout = Aout;
+  a.D = D;
+  a.g = (int)g;
+  a.check = check ? 1 : 0;
+  a.tm = tm;
+  // block g + 1 sits right after the skipped pivot band: tiles 2g, 2g + 1 in both dimensions
+  const int b0 = 2 * (int)g;
+  std::vector<int> perm(ntiles);
+  for (int s = 0; s < ntiles; ++s) perm[s] = host_xcd_remap(s, ntiles);
+  for (int k = 0; k < 4; ++k) {
+    a.diag[k] = pipe_tile_index(b0 + k / 2, b0 + k % 2, tm);
+    const int j = (int)(std::find(perm.begin() + k, perm.end(), a.diag[k]) - perm.begin());
+    std::swap(perm[k], perm[j]);
+  }
+  int ne = 0;
+  for (int k = 0; k < 4; ++k) a.exc_slot[k] = a.exc_tile[k] = -1;
+  for (int s = 4; s < ntiles; ++s)
+    if (perm[s] != host_xcd_remap(s, ntiles)) {
+      if (ne == 4) throw std::logic_error("launch_trail128_series: tile permutation");
+      a.exc_slot[ne] = s;
+      a.exc_tile[ne++] = perm[s];
+    }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int woff = std::min(ntiles, 2 * cus) & ~7;  // after the first round (2 workgroups per CU)
+  a.woff = woff;
+  a.ts = ts;
+  a.st = st;
+  hipLaunchKernelGGL(trail_series_kernel, dim3((unsigned)(ntiles + ts.workers)), dim3(NTHREADS), kGemmPipeLds, stream,
+                     a);
+  HIP_TRY(hipGetLastError());
 }
 
 #ifdef MIDAGMA_EXPERIMENTS

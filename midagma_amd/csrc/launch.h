@@ -82,6 +82,9 @@ struct BInvWork {
   double* LW;      // A(g+1, g+1) X0(g+1)      (extra tiles of block g's first pass)
   double* LZ;      // A(G, g+1) X0(g+1)        (same launch)
   double* LPZ;     // P_g LZ                   (extra tiles of block g's panel launch)
+  // (D / B2) x 256 ints: block g's counters for its series run inside trailing update g - 1
+  // (launch_trail128_series; null: off)
+  int* sync = nullptr;
 };
 // Outer block width of the two-level inverse (0: not available, use launch_gj_inverse).
 int binv_block(int64_t D);
@@ -132,6 +135,29 @@ void launch_series(const double* S, int64_t lds, int B2, const SeriesWork& w, St
                    hipStream_t stream);
 // pass p (1 .. NM_PASSES) of that series alone
 void launch_series_pass(int B2, const SeriesWork& w, State* st, int p, hipStream_t stream);
+
+// --- gemm.hip: the trailing update with the next block's series in the same launch ---------
+// Outer step g's 128-tile trailing update (launch_trail128, B2 = 256, C0 folded in the K loop)
+// whose launch also runs block g + 1's product-form series (residual and `passes` passes, the
+// series launches' tile bodies: nm_series.h) on `workers` workgroups placed after the first
+// round of tiles: block g + 1's diagonal S = Aout[G', G'] comes from the launch's first four
+// tiles, which signal a counter; the workers hand each phase on through counters of their own
+// (agent-scope release / acquire).  The counters must be 0 at launch (the panel launch of step g
+// zeroes them); every wait is bounded, and a timeout hands the slot back to the pivoted path
+// (ST_NEED_GJ).  sync: 8 counters of 32 ints ([0] diagonal tiles, [32 p] phase p, [224] timeouts).
+struct TrailSeries {
+  const double* Pe;  // block g + 1's warm-start ring (blockinv.hip's Pst / Pst1 rows)
+  const double* Po;
+  double* Y[2];
+  double* Q[2];
+  double* P;
+  double* part;      // block g + 1's (NM_PASSES + 1) x PART_STRIDE row partials
+  int* done;
+  int* sync;
+  int passes, xmap, workers;
+};
+void launch_trail128_series(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, State* st,
+                            const TrailSeries& ts, hipStream_t stream);
 
 // --- dfinv.hip --------------------------------------------------------------
 // The fast slot's blocked inverse as one dataflow launch (tile tasks, host-planned order).

@@ -92,7 +92,7 @@ struct midagma_solver {
   State* cgates = nullptr;
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
-  DevBuf Malt, Pst2, Pst2b, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone, nmLW, nmLZ, nmLPZ;
+  DevBuf Malt, Pst2, Pst2b, nmY0, nmY1, nmQ0, nmQ1, nmP, nmPart, nmDone, nmLW, nmLZ, nmLPZ, nmSync;
   // the fast slot's inverse as one dataflow launch (dfinv.hip; experiments build only,
   // MIDAGMA_EXP_DF=1: measured slower than the launch-per-phase inverse)
   bool df_on = false;
@@ -158,7 +158,7 @@ struct midagma_solver {
     if (h_agree) (void)hipHostFree(h_agree);
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
-                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &npart, &XT, &IW, &scarry,
+                      &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &nmSync, &npart, &XT, &IW, &scarry,
                       &sprev})
       b->release();
 #ifdef MIDAGMA_EXPERIMENTS
@@ -204,7 +204,8 @@ struct midagma_solver {
                     reinterpret_cast<int*>(nmDone.p),
                     nmLW.p,
                     nmLZ.p,
-                    nmLPZ.p};
+                    nmLPZ.p,
+                    reinterpret_cast<int*>(nmSync.p)};
   }
   bool blocked() const { return B2 > 0; }
   // k extent of the GEMMs whose K is the padded node dimension: the rows of A past d are zero
@@ -686,6 +687,8 @@ struct midagma_solver {
       for (DevBuf* b : {&nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmLW, &nmLZ, &nmLPZ}) b->alloc((size_t)b2 * b2);
       nmPart.alloc((size_t)(D / b2) * (NM_PASSES + 1) * PART_STRIDE);
       nmDone.alloc(D / b2);
+      nmSync.alloc((size_t)(D / b2) * 128);  // 256 ints per block (launch_trail128_series' counters)
+      HIP_TRY(hipMemsetAsync(nmSync.p, 0, (size_t)(D / b2) * 128 * sizeof(double), stream));
     }
 #ifdef MIDAGMA_EXPERIMENTS
     if (blocked() && mode == MIDAGMA_MODE_COV && df_available(D) && knob("MIDAGMA_EXP_DF", 0) != 0) setup_df();

@@ -120,3 +120,27 @@ def test_small_shard_fork_bit_identical(monkeypatch, loss):
         out[ff] = (W, r)
     (W0, r0), (W1, r1) = out["0"], out["1"]
     assert r0.iters == r1.iters == K and np.array_equal(W0, W1)
+
+
+@pytest.mark.parametrize("d", [2000, 3000])
+def test_trail_series_bit_identical(monkeypatch, d):
+    """Blocks 1 .. K2 - 1's product-form series inside the previous step's trailing update
+    (MIDAGMA_EXP_TRAIL_SERIES = workers, gemm.hip trail_series_kernel: the same tile bodies in the
+    same order) leave W, the iterations and the checkpoint objectives bit-identical to the series
+    launches.  d = 2000 -> D = 2048 (8 outer blocks), 3000 -> 3072 (12); checkpoints every 10 mix
+    pivoted and fast slots; 40 steps."""
+    X, _, _ = make_dataset(d, d + 500, seed=3)
+    Xc = X - X.mean(0)
+    cov = Xc.T @ Xc / X.shape[0]
+    out = {}
+    for w in ("0", "64", "32"):
+        monkeypatch.setenv("MIDAGMA_EXP_TRAIL_SERIES", w)
+        s = _solver(d, cov)
+        W = np.zeros((d, d))
+        r = s.minimize(W, 1.0, 40, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=10, want_checkpoints=True)
+        out[w] = (W, r.iters, [c.obj for c in r.checkpoints])
+        s.close()
+    for w in ("64", "32"):
+        assert out[w][1] == out["0"][1] == 40
+        assert np.array_equal(out[w][0], out["0"][0])
+        assert out[w][2] == out["0"][2]
