@@ -754,7 +754,7 @@ static const int64_t TRAIL128_MIN = knob("MIDAGMA_EXP_TRAIL128", 1792);
 // D from which the panels of B2 = 256 run on 64 x 64 tiles (binv_panel64_kernel; experiment knob
 // MIDAGMA_EXP_PANEL64_MIN, e.g. 1000000 for the 32 x 32 panel everywhere)
 static int64_t panel64_min() {
-  static const int64_t m = knob("MIDAGMA_EXP_PANEL64_MIN", 2048);
+  static const int64_t m = knob("MIDAGMA_EXP_PANEL64_MIN", int64_t(1) << 40);  // off until measured
   return m;
 }
 
