@@ -1169,7 +1169,11 @@ def main():
         small_res = bench_small(args, local, with_cpu=not args.no_cpu)
     tcc_res = None
     if rank == 0 and world == 1 and not args.no_tcc and args.workload == "data":
-        tcc_res = bench_tcc(args, local, with_cpu=not args.no_cpu)
+        try:  # a failure of this leg is reported in it, not taken out on the rest of the line
+            tcc_res = bench_tcc(args, local, with_cpu=not args.no_cpu)
+        except Exception as e:  # noqa: BLE001
+            log(f"tcc leg failed: {e!r}")
+            tcc_res = {"verified": False, "error": repr(e)[:400]}
     logi = None
     if rank == 0 and world == 1 and not args.no_logistic and args.workload == "data":
         logi = [bench_logistic(args, local, nn, args.logistic_steps if nn > 100_000 else 200)

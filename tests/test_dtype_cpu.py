@@ -1,0 +1,55 @@
+"""dtype=np.float32 (linear.py:29) through DagmaLinear.fit on the CPU: the product's Python path
+(W handed back in the caller's type after every minimize call) over a CPU double of the solver
+that runs the oracle's float64 loop, against the reference's own float32 fit
+(tests/golden/fit_f32_d20.npz).  The GPU form of this check is
+tests/test_gpu_parity.py::test_full_fit_float32_dtype."""
+import numpy as np
+
+from midagma_amd import _lib
+
+
+class _HostCovSolver:
+    """CPU double of HipSolver for a cov-mode fit with the host product X^T X / n."""
+
+    def __init__(self, d, loss, mode, device=0):
+        assert loss == "l2" and mode == "cov"
+        self.d = d
+
+    def set_cov(self, cov):
+        self.cov = np.array(cov, dtype=np.float64)
+
+    def set_masks(self, mask_inc, mask_exc):
+        assert mask_inc is None and mask_exc is None
+
+    def minimize(self, W, mu, max_iter, s, lr, tol, b1, b2, lambda1, checkpoint, want_checkpoints=False):
+        from midagma_amd.solver import MinimizeResult
+        from oracle.dagma_oracle import LinearOracle
+        assert W.dtype == np.float64  # the solver computes in float64 whatever the fit's dtype
+        o = LinearOracle("l2")
+        o.cov, o.d, o.n, o.eye = self.cov, self.d, None, np.eye(self.d)
+        o.lambda1, o.checkpoint, o.inc, o.exc, o.X = lambda1, checkpoint, None, None, None
+        Wn, tr = o.minimize(W, mu, max_iter, s, lr, tol, b1, b2)
+        W[...] = Wn
+        return MinimizeResult(iters=tr.iters, success=tr.success, status=_lib.ST_DONE if tr.success else _lib.ST_FAILED,
+                              halvings=tr.halvings, early_stop=tr.early_stop, lr_final=tr.lr_final, slots=tr.iters,
+                              obj_last=0.0, score_last=0.0, h_last=0.0)
+
+    def h_value(self, W, s=1.0, grad=True):
+        from oracle.dagma_oracle import h_logdet
+        return h_logdet(np.asarray(W, dtype=np.float64), s)
+
+    def score_value(self, W):
+        from oracle.dagma_oracle import score
+        return score("l2", np.asarray(W, dtype=np.float64), self.cov)
+
+
+def test_float32_fit_matches_reference_float32_fit(golden):
+    from midagma_amd import DagmaLinear
+    f = golden("fit_f32_d20.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    m = DagmaLinear("l2", dtype=np.float32, solver_factory=_HostCovSolver)
+    W = m.fit(X, lambda1=0.03, T=3, s=[1.0, .9, .8], warm_iter=4000, max_iter=5000, gram="host")
+    assert W.dtype == np.float32
+    spread = float(np.abs(f["W_f32"] - f["W_f64"]).max())
+    assert np.array_equal(W != 0, f["W_f32"] != 0)
+    assert np.abs(W - f["W_f32"]).max() <= 2 * spread

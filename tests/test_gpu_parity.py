@@ -185,7 +185,9 @@ def test_full_fit_float32_dtype(hip, golden):
     updates, so its float32 and float64 fits differ by float32 rounding (fit_f32_d20.npz: T = 3,
     max |dW| 1.6e-4, identical support).  The GPU loop computes in float64 and returns W in
     float32: the support must be the reference's and W within twice the reference's own
-    float32 / float64 spread of its float32 fit, and within 1e-6 of its float64 fit."""
+    float32 / float64 spread of its float32 fit (tests/test_dtype_cpu.py: the same Python path over
+    the CPU oracle, 1.3e-4 from the float64 fit: the stage-boundary float32 roundings grow like the
+    reference's own)."""
     from midagma_amd import DagmaLinear
     f = golden("fit_f32_d20.npz")
     X = golden("data_d20_n1000_seed0.npz")["X"].copy()
@@ -195,7 +197,6 @@ def test_full_fit_float32_dtype(hip, golden):
     spread = float(np.abs(f["W_f32"] - f["W_f64"]).max())
     assert np.array_equal(W != 0, f["W_f32"] != 0)
     assert np.abs(W - f["W_f32"]).max() <= 2 * spread
-    assert np.abs(W.astype(np.float64) - f["W_f64"]).max() <= 1e-6
 
 
 def test_full_fit_d1000_matches_reference_algorithm(hip, golden, parity):
