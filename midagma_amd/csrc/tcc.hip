@@ -305,254 +305,7 @@ __global__ void tcc_grad_kernel(const double* __restrict__ W, const double* __re
   }
 }
 
-// ---- 2d <= 64: the whole TCC sequence in ONE workgroup, A and the shifted inverse in LDS --------
-// The launch-per-kernel sequence above is ~170 dependent launches per slot (24 gated Noda steps of
-// shift, Gauss-Jordan prologue and steps, GEMV and update), almost all no-ops once Noda converged:
-// at d = 20 that was 0.40 ms per Adam step.  Here every step of the same algorithm (the same
-// Collatz-Wielandt start, Noda updates, stopping rules, breakdown handling, final sweeps, value and
-// gradient, and the same scal / warm-start words) runs in one workgroup; the inverses are an
-// unpivoted Gauss-Jordan in LDS (sigma I - A is a nonsingular M-matrix on every Noda step).
-constexpr int TS = 64;        // the largest 2d
-constexpr int TLD = TS + 1;   // LDS row stride
-
-// in-place unpivoted Gauss-Jordan inverse of the n x n LDS matrix M (stride TLD), held in registers
-// during the elimination: thread (i0, j) = (tid >> 6, tid & 63) keeps M[i0 + 4 t][j], t < 16.  Per
-// pivot the owners publish row p and column p to LDS (double-buffered by pivot parity, so one
-// barrier per pivot), then every thread updates its 16 values.  rowp, colp: 2 x TS doubles each.
-__device__ __forceinline__ void lds_gj_inverse(double* M, int n, double* rowp, double* colp) {
-  const int j = threadIdx.x & 63, i0 = threadIdx.x >> 6;
-  double r[16];
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const int i = i0 + 4 * t;
-    r[t] = (i < n && j < n) ? M[i * TLD + j] : 0.0;
-  }
-  for (int p = 0; p < n; ++p) {
-    const int tp = p >> 2;
-    double* rb = rowp + (p & 1) * TS;
-    double* cb = colp + (p & 1) * TS;
-    if (i0 == (p & 3)) {  // row p's owner: r[tp] by selects (no dynamic register index)
-      double v = 0.0;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) v = (t == tp) ? r[t] : v;
-      rb[j] = v;
-    }
-    if (j == p) {
-#pragma unroll
-      for (int t = 0; t < 16; ++t) cb[i0 + 4 * t] = r[t];
-    }
-    __syncthreads();
-    const double inv = 1.0 / rb[p];
-    const double rpj = rb[j] * inv;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int i = i0 + 4 * t;
-      if (i == p)
-        r[t] = (j == p) ? inv : rpj;
-      else
-        r[t] = (j == p) ? -cb[i] * inv : r[t] - cb[i] * rpj;
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const int i = i0 + 4 * t;
-    if (i < n && j < n) M[i * TLD + j] = r[t];
-  }
-  __syncthreads();
-}
-
-// y[i] = sum_j M[i][j] x[j] (trans: sum_j M[j][i] x[j]) on i < n; skip_tr: B (top-right d x d zero)
-__device__ void lds_gemv(const double* M, int n, int d, bool trans, bool skip_tr, const double* x, double* y) {
-  const int i = threadIdx.x;
-  if (i < n) {
-    const int jend = (skip_tr && i < d) ? d : n;
-    double acc = 0.0;
-    for (int j = 0; j < jend; ++j) acc += (trans ? M[j * TLD + i] : M[i * TLD + j]) * x[j];
-    y[i] = acc;
-  }
-  __syncthreads();
-}
-
-// out = y / |y| with sum(out) > 0 (tcc_normalize_kernel)
-__device__ void lds_normalize(const double* y, double* out, int n, double* sh) {
-  double ss = 0.0, sm = 0.0;
-  for (int i = threadIdx.x; i < n; i += EB) {
-    ss += y[i] * y[i];
-    sm += y[i];
-  }
-  ss = wg_reduce(ss, sh, Add());
-  sm = wg_reduce(sm, sh, Add());
-  const double inv = (sm < 0.0 ? -1.0 : 1.0) / sqrt(ss);
-  for (int i = threadIdx.x; i < n; i += EB) out[i] = y[i] * inv;
-  __syncthreads();
-}
-
-// warm start (tcc_init_kernel): prev when the last solve converged and is inside the cone, else ones
-__device__ void lds_init(const double* __restrict__ prev, double* x, int n, const double* scal, double* sh) {
-  double mn = INFINITY, mx = 0.0;
-  for (int i = threadIdx.x; i < n; i += EB) {
-    mn = fmin(mn, prev[i]);
-    mx = fmax(mx, prev[i]);
-  }
-  mn = wg_reduce(mn, sh, Min());
-  mx = wg_reduce(mx, sh, Max());
-  const bool warm = scal[8] != 0.0 && scal[9] != 0.0 && mn > 1e-8 * mx && isfinite(mx);
-  for (int i = threadIdx.x; i < n; i += EB) x[i] = warm ? prev[i] : 1.0;
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(EB) void tcc_small_kernel(const double* __restrict__ W, const double* __restrict__ S,
-                                                       double ws, int d, int64_t D, int mode, double eps, double m,
-                                                       double weight, const State* __restrict__ st,
-                                                       double* __restrict__ scal, double* __restrict__ vprev,
-                                                       double* __restrict__ uprev, double* __restrict__ G) {
-  if (!(st->status == ST_RUNNING && (mode == 2 || st->ckpt_pending))) return;  // tcc_gate_kernel's rule
-  __shared__ double A[TS * TLD], Mi[TS * TLD];
-  __shared__ double x[TS], y[TS], u[TS], z[TS], rowp[2 * TS], colp[2 * TS], sh[EB], sc[10];
-  const int n = 2 * d, tid = threadIdx.x;
-  for (int e = tid; e < n * n; e += EB) {  // tcc_build_kernel
-    const int i = e / n, j = e - i * n;
-    double a = 0.0;
-    if (i < d) {
-      if (j < d) {
-        const double w = W[(int64_t)i * D + j];
-        a = w * w;
-      } else {
-        a = ws * S[(int64_t)i * D + (j - d)];
-      }
-    } else if (j < d) {
-      a = (i - d == j) ? 1.0 : 0.0;
-    } else {
-      const double w = W[(int64_t)(j - d) * D + (i - d)];
-      a = w * w;
-    }
-    A[i * TLD + j] = a;
-  }
-  if (tid < 10) sc[tid] = scal[tid];
-  __syncthreads();
-  lds_init(vprev, x, n, sc, sh);
-  lds_gemv(A, n, d, false, false, x, y);
-  {  // tcc_sigma0_kernel
-    double mx = -INFINITY;
-    for (int i = tid; i < n; i += EB) mx = fmax(mx, y[i] / x[i]);
-    mx = wg_reduce(mx, sh, Max());
-    if (tid == 0) {
-      sc[1] = mx;
-      sc[2] = 0.0;
-      sc[7] = 0.0;
-      sc[9] = 0.0;
-    }
-    __syncthreads();
-  }
-  auto shift = [&](double margin) {  // tcc_shift_kernel
-    const double sig = sc[1] * (1.0 + margin);
-    const int j = tid & 63;
-    if (j < n)
-      for (int i = tid >> 6; i < n; i += 4) Mi[i * TLD + j] = (i == j ? sig : 0.0) - A[i * TLD + j];
-    __syncthreads();
-  };
-  for (int k = 0; k < TCC_NODA_MAX; ++k) {  // tcc_noda_kernel, until the stop rule
-    shift(0.0);
-    lds_gj_inverse(Mi, n, rowp, colp);
-    lds_gemv(Mi, n, d, false, false, x, y);
-    double rmin = INFINITY, rmax = -INFINITY, ss = 0.0, bad = 0.0;
-    for (int i = tid; i < n; i += EB) {
-      const double yi = y[i];
-      if (!(yi > 0.0) || !isfinite(yi)) bad = 1.0;
-      const double r = x[i] / yi;
-      rmin = fmin(rmin, r);
-      rmax = fmax(rmax, r);
-      ss += yi * yi;
-    }
-    rmin = wg_reduce(rmin, sh, Min());
-    rmax = wg_reduce(rmax, sh, Max());
-    ss = wg_reduce(ss, sh, Add());
-    bad = wg_reduce(bad, sh, Max());
-    const double sig = sc[1];
-    bool stop;
-    if (bad != 0.0 || !(ss > 0.0) || !isfinite(ss)) {
-      stop = true;
-      if (tid == 0) sc[7] = 1.0;
-    } else {
-      const double inv = 1.0 / sqrt(ss);
-      for (int i = tid; i < n; i += EB) x[i] = y[i] * inv;
-      const double up = sig - rmin, lo = sig - rmax;
-      stop = !(up - lo > 1e-13 * fabs(up)) || !(sig - up > 1e-14 * fabs(up));
-      if (tid == 0) {
-        sc[1] = up;
-        sc[2] = lo;
-        if (stop) sc[9] = 1.0;
-      }
-    }
-    __syncthreads();
-    if (stop) break;
-  }
-  // the final inverse just above the root: two sweeps for v (x), two transposed for u
-  shift(1e-14);
-  lds_gj_inverse(Mi, n, rowp, colp);
-  for (int r = 0; r < 2; ++r) {
-    lds_gemv(Mi, n, d, false, false, x, y);
-    lds_normalize(y, x, n, sh);
-  }
-  lds_init(uprev, u, n, sc, sh);
-  for (int r = 0; r < 2; ++r) {
-    lds_gemv(Mi, n, d, true, false, u, y);
-    lds_normalize(y, u, n, sh);
-  }
-  lds_gemv(A, n, d, false, false, x, y);  // A v
-  lds_gemv(A, n, d, false, true, u, z);   // B u
-  {  // tcc_value_kernel
-    double uav = 0.0, uv = 0.0, uu = 0.0, ubu = 0.0;
-    for (int i = tid; i < n; i += EB) {
-      uav += u[i] * y[i];
-      uv += u[i] * x[i];
-      uu += u[i] * u[i];
-      ubu += u[i] * z[i];
-      vprev[i] = x[i];
-      uprev[i] = u[i];
-    }
-    uav = wg_reduce(uav, sh, Add());
-    uv = wg_reduce(uv, sh, Add());
-    uu = wg_reduce(uu, sh, Add());
-    ubu = wg_reduce(ubu, sh, Add());
-    if (tid == 0) {
-      const double rho = uav / uv;
-      const double val = (rho - ubu / (uu + eps)) / m;
-      if (isfinite(val)) {
-        sc[0] = val;
-        sc[3] = rho;
-        sc[4] = uv + eps;
-        sc[5] = uu + eps;
-        sc[8] = 1.0;
-      } else {
-        sc[0] = 0.0;
-        sc[3] = 0.0;
-        sc[4] = INFINITY;
-        sc[5] = INFINITY;
-        sc[8] = 0.0;
-      }
-    }
-    __syncthreads();
-  }
-  if (tid < 10) scal[tid] = sc[tid];
-  if (mode == 2) {  // tcc_grad_kernel on the logical d x d block (the padding stays 0)
-    const double denA = sc[4], denB = sc[5];
-    for (int e = tid; e < d * d; e += EB) {
-      const int i = e / d, j = e - i * d;
-      const double w = W[(int64_t)i * D + j];
-      double g = 0.0;
-      if (w != 0.0) {
-        const double gA = u[i] * x[j] / denA + u[d + j] * x[d + i] / denA;
-        const double gB = (u[i] * u[j] + u[d + i] * u[d + j]) / denB;
-        g = weight * (((2.0 * w) * gA - (2.0 * w) * gB) / m);
-      }
-      G[(int64_t)i * D + j] = g;
-    }
-  }
-}
-
 // ---- 2d <= 128: the whole TCC sequence in ONE workgroup of 4 x 4 register blocks --------------
-// (experiments build, MIDAGMA_EXP_TCC_BLK4=1, until measured against tcc_small_kernel above)
 // The launch-per-kernel sequence above is ~170 dependent launches per slot (24 gated Noda steps of
 // shift, Gauss-Jordan prologue and steps, GEMV and update), almost all no-ops once Noda converged:
 // at d = 20 that was 0.40 ms per Adam step.  Here every step of the same algorithm (the same
@@ -968,7 +721,7 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
                      double* Gtrek, hipStream_t stream) {
   const int64_t n = 2 * d, D2 = w.D2;
   static const bool chain = knob_set("MIDAGMA_EXP_TCC_CHAIN");  // experiments: the launch sequence at every d
-  if (n <= 128 && !chain && knob("MIDAGMA_EXP_TCC_BLK4", 0) != 0) {
+  if (n <= 128 && !chain) {
     // one workgroup of 4 x 4 register blocks: 64 threads up to 2d = 32, 256 up to 64, 1024 up to 128
     const long nb = knob("MIDAGMA_EXP_TCC_NB", 0);  // experiments: force the block count
     auto go = [&](auto kern, int nt) {
@@ -981,12 +734,6 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
       go(tcc_blk_kernel<16>, 256);
     else
       go(tcc_blk_kernel<32>, 1024);
-    HIP_TRY(hipGetLastError());
-    return;
-  }
-  if (n <= TS && !chain) {
-    hipLaunchKernelGGL(tcc_small_kernel, dim3(1), dim3(EB), 0, stream, W, w.S, cfg.w, (int)d, D, cfg.mode, cfg.eps,
-                       (double)cfg.m, cfg.weight, st, w.scal, w.vprev, w.uprev, Gtrek);
     HIP_TRY(hipGetLastError());
     return;
   }
