@@ -758,10 +758,16 @@ static int64_t panel64_min() {
   return m;
 }
 
-// workgroups that run the next block's series inside a trailing update (launch_trail128_series;
-// experiment knob MIDAGMA_EXP_TRAIL_SERIES: 0 keeps the series launches)
-static int trail_series_workers() {
-  const int w = (int)knob("MIDAGMA_EXP_TRAIL_SERIES", 0);  // read at each enqueue (graph capture)
+// workgroups that run the next block's series inside a trailing update (launch_trail128_series):
+// 64 where the update has >= 1024 tiles (D >= 4352: at least two rounds to hide the series
+// behind; d = 5000 108.2 -> 110.7 steps/s, while at d = 2000 / 3000 the series outlasts the
+// update's one round: 1100 -> 731, 393 -> 298; profiles/r04_probe_large3_ts*.log).  Experiment
+// knob MIDAGMA_EXP_TRAIL_SERIES = workers (0: the series launches everywhere), read at each
+// enqueue (graph capture).
+static int trail_series_workers(int64_t D) {
+  const int w = (int)knob("MIDAGMA_EXP_TRAIL_SERIES", -1);
+  const int64_t tm = (D - 256) / 128;
+  if (w < 0) return tm * tm >= 1024 ? 64 : 0;
   return w > 0 ? (w + 7) / 8 * 8 : 0;
 }
 
@@ -977,7 +983,7 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
   // look-ahead residual (NmLA / TrailLA): fast path with 32 x 32 trailing updates
   const bool look = fast && bw.LW && K2 > 1 && D - B2 < TRAIL128_MIN && resid_lookahead();
   // blocks 1 .. K2 - 1's series inside the previous step's trailing update (128-tile updates)
-  const bool tser = fast && bw.sync && B2 == 256 && K2 > 1 && D - B2 >= TRAIL128_MIN && trail_series_workers() > 0;
+  const bool tser = fast && bw.sync && B2 == 256 && K2 > 1 && D - B2 >= TRAIL128_MIN && trail_series_workers(D) > 0;
   for (int g = 0; g < K2; ++g) {
     double* Ain = bufs[g & 1];
     double* Aout = bufs[(g + 1) & 1];
@@ -1054,7 +1060,7 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
           const int64_t gn = g + 1;
           TrailSeries ts{bw.Pst + gn * B2 * B2, bw.Pst1 + gn * B2 * B2, {bw.Y[0], bw.Y[1]}, {bw.Q[0], bw.Q[1]}, bw.P,
                          bw.part + gn * (NM_PASSES + 1) * PART_STRIDE, bw.done + gn, zsync,
-                         std::min(passes, NM_PASSES), nm_xmap(), trail_series_workers()};
+                         std::min(passes, NM_PASSES), nm_xmap(), trail_series_workers(D)};
           launch_trail128_series(Ain, Aout, D, g, check != 0, st, ts, stream);
         } else {
           launch_trail128(Ain, Aout, D, B2, g, check, st, stream);

@@ -1094,13 +1094,19 @@ __device__ __forceinline__ bool ts_wait(const int* ctr, int target, int* go) {
   __syncthreads();
   return *go != 0;
 }
-// every wave's stores drained, the barrier, then lane 0: agent release and one counter add
-__device__ __forceinline__ void ts_signal(int* ctr) {
+// every wave's stores drained, the barrier, then lane 0: one counter add, behind an agent release
+// when the handed-off bytes were plain stores (the diagonal tiles: the release writes back the XCD
+// L2's dirty lines, the trailing tiles' too), without one when every handed-off byte was stored
+// write-through (sc1: the series' Y, Q, P, row partials; MI355X_MICROARCH.md, "(2) without an
+// agent release") -- a release per worker and phase flushed the L2s under the running update
+__device__ __forceinline__ void ts_signal(int* ctr, bool release) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (release) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -1129,7 +1135,7 @@ __device__ void ts_worker(const TrailSeriesArgs& a, int w, double* smem) {
     nm_resid_body<16, 4, false>(wg, S, a.D, SFromW{}, s.Pe, s.Po, s.Y[0], s.Q[0], s.part, s.done, a.st, s.xmap, red);
   }
   for (int p = 1; p <= s.passes; ++p) {
-    ts_signal(s.sync + 32 * p);
+    ts_signal(s.sync + 32 * p, false);
     if (!ts_wait(s.sync + 32 * p, s.workers, go)) return ts_abort(a);
     for (int wg = w; wg < 256; wg += s.workers) {
       __syncthreads();
@@ -1156,7 +1162,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void trail_series_kernel(TrailSeriesAr
   const int64_t G0 = (int64_t)a.g * 256;
   gemm_pipe_tile<0, B_PLAIN, EPI_SUB_MID>(t, 256, 256, a.tm, a.tm, a.Ain + G0, a.D, a.Aout + G0 * a.D, a.D, a.Aout,
                                           a.D, (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, 2, a.st, smem);
-  if (s < 4) ts_signal(a.ts.sync);  // block g + 1's diagonal tile is in Aout
+  if (s < 4) ts_signal(a.ts.sync, true);  // block g + 1's diagonal tile is in Aout (plain stores)
 }
 
 // linear index of tile (bm, bn) (pivot band skipped) in gemm_pipe_tile's order for tm x tm tiles
@@ -1210,7 +1216,10 @@ void launch_trail128_series(const double* Ain, double* Aout, int64_t D, int64_t 
     HIP_TRY(hipGetDevice(&dev));
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  const int woff = std::min(ntiles, 2 * cus) & ~7;  // after the first round (2 workgroups per CU)
+  // the workers' place in the grid: after the first round of tiles (2 workgroups per CU; they start
+  // as the first tiles finish), or (experiment knob MIDAGMA_EXP_TS_WOFF=0) after all tiles, in
+  // the slots the last round leaves idle
+  const int woff = (knob("MIDAGMA_EXP_TS_WOFF", 1) != 0 ? std::min(ntiles, 2 * cus) : ntiles) & ~7;
   a.woff = woff;
   a.ts = ts;
   a.st = st;

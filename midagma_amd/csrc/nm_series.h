@@ -49,7 +49,7 @@ __device__ __forceinline__ void store_row_partial(double a, double* __restrict__
   a = row_sum16(a);
   int row, col;
   tile_elem(threadIdx.x, row, col);
-  if (col == 0) rowpart[(int64_t)(m0 + row) * NT + n0 / 16] = a;
+  if (col == 0) st_wt(rowpart + (int64_t)(m0 + row) * NT + n0 / 16, a);  // write-through: handed to other CUs
 }
 
 template <int B2, int NTH = NTHREADS>
