@@ -197,10 +197,21 @@ int small_block(int64_t d);
 // checkpoint step's norms and the warm-start count, pstore (2 x 32 x 32) the last two
 // inverses; zero carry before a call's first launch.  Slots after a terminal status are
 // not run.
+// tcc (nullable; d <= 32): the TCC trek regularizer inside every slot ('opt') or every
+// checkpoint slot ('log'), tcc_blk.h's body on the workgroup, its state words read at entry and
+// written back at exit (the graph-replayed slots' TccWork words, so the two paths interleave).
+struct SmallTcc {
+  const double* S;        // D x D pair indicator
+  double ws, eps, m, weight;
+  int mode;               // 1 'log', 2 'opt'
+  double* scal;           // TccWork::scal, vprev, uprev
+  double* vprev;
+  double* uprev;
+};
 void launch_small_minimize(const Params* pr, State* st, double* W, double* m, double* v, const double* covs,
                            const double* minc, const double* mexc, const double* bc_table, CkptRec* ckpt,
                            int64_t ckpt_cap, double* carry, double* pstore, int64_t d, int64_t n_slots,
-                           hipStream_t stream);
+                           hipStream_t stream, const SmallTcc* tcc = nullptr);
 
 // --- trek.hip ---------------------------------------------------------------
 enum TrekSeq : int { TREK_EXP = 0, TREK_INV = 1, TREK_LOG = 2, TREK_BINOM = 3 };

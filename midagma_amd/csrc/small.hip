@@ -1,4 +1,5 @@
-// Small-d cov-mode inner loop in ONE persistent workgroup (d <= 64, l2, no trek regularizer).
+// Small-d cov-mode inner loop in ONE persistent workgroup (d <= 64, l2; the TCC trek regularizer
+// at d <= 32, tcc_blk.h; no PST).
 //
 // At d = 20 a graph-replayed slot is 8 dependent launches of a 64 x 64 padded problem, each
 // 4-6 us (profiles/r01_rocprof_cov_small_kernel_stats.csv): the GPU ran the reference's loop
@@ -24,8 +25,11 @@
 // (w / (DS/16), w % (DS/16)); lane l owns column 16 tc + (l & 15), rows 16 tr + (l >> 4) + 4 t
 // for t = 0..3.  DS = 16, 32, 64 -> 1, 4, 16 waves.
 // Arithmetic per element is step.hip's, in the same order (built with -ffp-contract=off).
+#include <type_traits>
+
 #include "launch.h"
 #include "mfma64.h"
+#include "tcc_blk.h"
 
 namespace midagma {
 namespace {
@@ -81,7 +85,7 @@ template <int NW>
 __device__ __noinline__ void small_control(const Params* __restrict__ pr, State& S, SmallCtl& ctl,
                                            const double (*red)[NW], const double (*nred)[NW], const int* flw,
                                            CkptRec* __restrict__ ckpt, int64_t ckpt_cap, double bc1n,
-                                           double bc2n) {
+                                           double bc2n, const double* trek_val) {
     int flags = 0;
 #pragma unroll 1
     for (int x = 0; x < NW; ++x) flags |= flw[x];
@@ -111,7 +115,9 @@ __device__ __noinline__ void small_control(const Params* __restrict__ pr, State&
       S.ckpt_pending = 0;
       const double h = -ld + pr->d_log_s;
       const double score = pr->score_scale * sd;
-      const double obj = pr->mu * (score + pr->lambda1 * l1) + h;
+      double obj = pr->mu * (score + pr->lambda1 * l1) + h;
+      const double tv = trek_val ? trek_val[0] : 0.0;
+      if (trek_val && pr->trek_mode == 2) obj = obj + pr->trek_weight * tv;  // linear.py:131-133
       if (S.n_ckpt < ckpt_cap) {
         CkptRec& r = ckpt[S.n_ckpt];
         r.iter = S.iter;
@@ -130,8 +136,8 @@ __device__ __noinline__ void small_control(const Params* __restrict__ pr, State&
         r.grad_l1_norm = sqrt(nf[NF_GL1]);
         r.grad_inc_norm = sqrt(nf[NF_GINC]);
         r.elapsed = (double)(__builtin_amdgcn_s_memrealtime() - S.t0) * 1e-8;
-        r.reg_trek_value = 0.0;
-        r.grad_trek_norm = 0.0;
+        r.reg_trek_value = tv;
+        r.grad_trek_norm = trek_val ? sqrt(nf[NF_GTREK]) : 0.0;
       }
       S.n_ckpt += 1;
       S.obj_last = obj;
@@ -190,13 +196,16 @@ __device__ __noinline__ void small_control(const Params* __restrict__ pr, State&
     ctl.bc2 = S.bc2;
 }
 
-template <int DS, int NW>
+template <int DS, int NW, bool TCC>
 __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     const Params* __restrict__ pr, State* __restrict__ stg, double* __restrict__ Wg, double* __restrict__ mg,
     double* __restrict__ vg, const double* __restrict__ covs, const double* __restrict__ minc,
     const double* __restrict__ mexc, const double* __restrict__ bc_table, CkptRec* __restrict__ ckpt,
-    int64_t ckpt_cap, double* __restrict__ carry, double* __restrict__ pstore, int64_t n_slots) {
+    int64_t ckpt_cap, double* __restrict__ carry, double* __restrict__ pstore, int64_t n_slots, SmallTcc tc) {
   constexpr int NT = 64 * NW, TPR = DS / 16, TPW = TPR * TPR / NW, E = 4 * TPW;
+  // TCC: tcc_blk.h's body on this workgroup, NB x NB = NT threads (DS = 16: NB = 8, DS = 32: 16)
+  constexpr int TNB = DS / 2;
+  static_assert(!TCC || (TNB * TNB == NT && DS <= 32), "TCC in the small loop: d <= 32");
   static_assert(TPW * NW == TPR * TPR, "whole tiles per wave");
   constexpr int SW = DS + 2;                         // W, cov images: 16 rows x 4 cols per read
   constexpr int SI = ((DS + 15) / 32) * 32 + 16;     // I - W image: B operand rows, = 16 mod 32
@@ -227,6 +236,9 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   __shared__ int flw[NW];
   __shared__ State S;                         // the controller's (thread 0's) state
   __shared__ SmallCtl ctl;                    // its decision for the slot, read by every thread
+  // TCC: the body's LDS and the regularizer's state words (scal, v, u), loaded at entry
+  __shared__ std::conditional_t<TCC, tccb::TccLds<TNB>, char> TL;
+  __shared__ double tsc[TCC ? 10 : 1], tvp[TCC ? 4 * TNB : 1], tup[TCC ? 4 * TNB : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane >> 4, c = lane & 15;
@@ -273,6 +285,13 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     for (int e = tid; e < DS * SW; e += NT) Wimg[e] = 0.0;
   for (int e = tid; e < DS; e += NT) wdiag[e] = 0.0;
   for (int e = tid; e < DS * SI; e += NT) IWimg[e] = 0.0;
+  if constexpr (TCC) {
+    if (tid < 10) tsc[tid] = tc.scal[tid];
+    for (int e = tid; e < 2 * (int)pr->d; e += NT) {
+      tvp[e] = tc.vprev[e];
+      tup[e] = tc.uprev[e];
+    }
+  }
   __syncthreads();
   if (!ctl.run) return;
 #pragma unroll
@@ -297,6 +316,17 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   __syncthreads();
 
   for (int64_t slot = 0; slot < n_slots; ++slot) {
+    // the TCC regularizer of this slot's W (linear.py:251-258; tcc_gate_kernel's rule: every slot
+    // in 'opt' mode, checkpoint slots in 'log' mode)
+    bool tcc_ran = false;
+    if constexpr (TCC) {
+      if (tc.mode == 2 || S.ckpt_pending) {
+        tccb::tcc_blk_body<TNB>([&](int i, int j) { return Wimg[i * SW + j]; },
+                                [&](int i, int j) { return tc.S[(int64_t)i * D + j]; }, tc.ws, di, tc.mode, tc.eps,
+                                tc.m, tc.weight, tsc, tvp, tup, nullptr, D, TL);
+        tcc_ran = true;
+      }
+    }
     // 1 - beta^it for it = iter + 1 from the host table (read early: latency under the inverse)
     double bc1n = 1.0, bc2n = 1.0;
     if (tid == 0 && S.iter < pr->ld_table) {
@@ -519,7 +549,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     __syncthreads();
 
     // ---- control, thread 0 (step.hip control_kernel; linear.py:230-241, 279-331)
-    if (tid == 0) small_control<NW>(pr, S, ctl, red, nred, flw, ckpt, ckpt_cap, bc1n, bc2n);
+    if (tid == 0) small_control<NW>(pr, S, ctl, red, nred, flw, ckpt, ckpt_cap, bc1n, bc2n, TCC ? tsc : nullptr);
     __syncthreads();
     const int act = ctl.act;
     if (act == ACT_NOOP) break;  // terminal: nothing of this slot is applied
@@ -550,6 +580,13 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
           gi = minc[idx] * sg;
           gobj = gobj + gi;
         }
+        double gtr = 0.0;
+        if constexpr (TCC) {  // Gobj + weight * trek_grad (linear.py:257-258), step.hip's order
+          if (tc.mode == 2 && tcc_ran) {
+            gtr = tccb::tcc_grad_elem<TNB>(TL, di, rows[e], cols[e], wo, tc.m, tc.weight);
+            gobj = gobj + gtr;
+          }
+        }
         const double mm = mv[e] * pr->beta1 + pr->c1 * gobj;
         const double vx = vv[e] * pr->beta2 + pr->c2 * (gobj * gobj);
         const double mh = mm / bc1;
@@ -566,6 +603,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
           qf[NF_GDAG] += gh * gh;
           qf[NF_GL1] += gl1 * gl1;
           qf[NF_GINC] += gi * gi;
+          qf[NF_GTREK] += gtr * gtr;
           qf[NF_GSTEP] += gd * gd;
           qf[NF_W2] += wn * wn;
           qf[NF_WMAX] = fmax(qf[NF_WMAX], fabs(wn));
@@ -610,6 +648,13 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     pstore[rows[e] * DS + cols[e]] = p1[e];
     pstore[DS * DS + rows[e] * DS + cols[e]] = p2[e];
   }
+  if constexpr (TCC) {
+    if (tid < 10) tc.scal[tid] = tsc[tid];
+    for (int e = tid; e < 2 * (int)pr->d; e += NT) {
+      tc.vprev[e] = tvp[e];
+      tc.uprev[e] = tup[e];
+    }
+  }
   if (tid == 0) {
     carry[NORM_FIELDS] = (double)warm;
     if (S.ckpt_pending)
@@ -636,19 +681,28 @@ int small_block(int64_t d) {
 void launch_small_minimize(const Params* pr, State* st, double* W, double* m, double* v, const double* covs,
                            const double* minc, const double* mexc, const double* bc_table, CkptRec* ckpt,
                            int64_t ckpt_cap, double* carry, double* pstore, int64_t d, int64_t n_slots,
-                           hipStream_t stream) {
+                           hipStream_t stream, const SmallTcc* tcc) {
   const int ds = small_block(d);
   if (ds == 0) throw std::invalid_argument("small_minimize: d > 64");
-#define MIDAGMA_SMALL(DS_, NW_)                                                                                  \
-  hipLaunchKernelGGL((small_minimize_kernel<DS_, NW_>), dim3(1), dim3(64 * NW_), 0, stream, pr, st, W, m, v, covs, \
-                     minc, mexc, bc_table, ckpt, ckpt_cap, carry, pstore, n_slots)
+  if (tcc && ds > 32) throw std::invalid_argument("small_minimize: the TCC regularizer needs d <= 32");
+  const SmallTcc tc = tcc ? *tcc : SmallTcc{};
+#define MIDAGMA_SMALL(DS_, NW_, TCC_)                                                                           \
+  hipLaunchKernelGGL((small_minimize_kernel<DS_, NW_, TCC_>), dim3(1), dim3(64 * NW_), 0, stream, pr, st, W, m, v, \
+                     covs, minc, mexc, bc_table, ckpt, ckpt_cap, carry, pstore, n_slots, tc)
   // one wave per 16 x 16 tile
-  if (ds == 16)
-    MIDAGMA_SMALL(16, 1);
-  else if (ds == 32)
-    MIDAGMA_SMALL(32, 4);
-  else
-    MIDAGMA_SMALL(64, 16);
+  if (ds == 16) {
+    if (tcc)
+      MIDAGMA_SMALL(16, 1, true);
+    else
+      MIDAGMA_SMALL(16, 1, false);
+  } else if (ds == 32) {
+    if (tcc)
+      MIDAGMA_SMALL(32, 4, true);
+    else
+      MIDAGMA_SMALL(32, 4, false);
+  } else {
+    MIDAGMA_SMALL(64, 16, false);
+  }
 #undef MIDAGMA_SMALL
   HIP_TRY(hipGetLastError());
 }

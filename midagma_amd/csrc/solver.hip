@@ -73,8 +73,11 @@ struct midagma_solver {
   // cov mode, l2, d <= 64, no trek regularizer: the one-workgroup persistent loop (small.hip)
   DevBuf scarry, sprev;  // between two small-loop launches: pending norms + warm count, last inverses
   bool use_small = !knob_set("MIDAGMA_EXP_NO_SMALL");
+  bool small_tcc = knob("MIDAGMA_EXP_SMALL_TCC", 1) != 0;  // experiments: 0 keeps TCC on the graph slots
+  // (the TCC regularizer runs inside it up to d = 32, tcc_blk.h; PST keeps the graph-replayed slots)
   bool small_on() const {
-    return use_small && mode == MIDAGMA_MODE_COV && loss == MIDAGMA_LOSS_L2 && !trek_on && small_block(d) > 0;
+    return use_small && mode == MIDAGMA_MODE_COV && loss == MIDAGMA_LOSS_L2 && small_block(d) > 0 &&
+           (!trek_on || (trek_tcc && small_block(d) <= 32 && small_tcc));
   }
   // PST trek regularizer (trek.hip)
   TrekCfg tcfg{};
@@ -939,9 +942,12 @@ struct midagma_solver {
     for (int64_t launched = 0;;) {
       const int64_t B = small_next_batch(n_slots, launched, cap, kSmallBatch);
       if (B <= 0) break;
+      SmallTcc tc{};
+      if (trek_on && trek_tcc)
+        tc = SmallTcc{cw.S, ccfg.w, ccfg.eps, (double)ccfg.m, ccfg.weight, ccfg.mode, cw.scal, cw.vprev, cw.uprev};
       launch_small_minimize(d_params, d_state, W.p, m.p, v.p, covs.p, has_inc ? minc.p : nullptr,
                             has_exc ? mexc.p : nullptr, bc_table.p, d_ckpt, ckpt_cap, scarry.p, sprev.p, d, B,
-                            stream);
+                            stream, trek_on && trek_tcc ? &tc : nullptr);
       launched += B;
       HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));

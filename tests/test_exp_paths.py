@@ -144,3 +144,35 @@ def test_trail_series_bit_identical(monkeypatch, d):
         assert out[w][1] == out["0"][1] == 40
         assert np.array_equal(out[w][0], out["0"][0])
         assert out[w][2] == out["0"][2]
+
+
+@pytest.mark.parametrize("d", [8, 20, 32])
+@pytest.mark.parametrize("mode", ["opt", "log"])
+def test_small_path_tcc_vs_graph_path(d, mode, monkeypatch):
+    """The TCC regularizer inside the persistent small loop (small.hip + tcc_blk.h, d <= 32)
+    against the graph-replayed slots with the one-workgroup TCC launch (MIDAGMA_EXP_SMALL_TCC=0):
+    same iterations and checkpoints; W within 1e-11 and the checkpoints' objective,
+    reg_trek_value and grad_trek_norm within 1e-10 rel after 500 steps (checkpoint every 100)."""
+    X, _, _ = make_dataset(d, max(200, 10 * d), seed=7)
+    o = _oracle(X, 100)
+    rng = np.random.default_rng(d)
+    iu = np.array(np.triu_indices(d, 1)).T
+    pairs = iu[rng.uniform(size=len(iu)) < 0.3]
+    K = 500
+    runs = []
+    for small in ("1", "0"):
+        monkeypatch.setenv("MIDAGMA_EXP_SMALL_TCC", small)
+        s = _solver(d, o.cov)
+        s.set_trek_tcc(pairs, mode=mode, weight=0.2)
+        W = np.zeros((d, d))
+        r = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100, want_checkpoints=True)
+        runs.append((W, r))
+        s.close()
+    (Wa, ra), (Wb, rb) = runs
+    assert ra.iters == rb.iters == K
+    assert np.abs(Wa - Wb).max() <= 1e-11
+    assert [c.iter for c in ra.checkpoints] == [c.iter for c in rb.checkpoints]
+    for a, b in zip(ra.checkpoints, rb.checkpoints):
+        assert abs(a.obj - b.obj) <= 1e-10 * abs(b.obj)
+        assert abs(a.reg_trek_value - b.reg_trek_value) <= 1e-10 * abs(b.reg_trek_value) + 1e-300
+        assert abs(a.grad_trek_norm - b.grad_trek_norm) <= 1e-10 * b.grad_trek_norm + 1e-300
