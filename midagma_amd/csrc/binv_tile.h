@@ -15,8 +15,9 @@ __device__ __forceinline__ int xcd_spread(int w, int nwg) {
 // acc += A[0:32, 0:K] B[0:K, 0:32] (global operands, K = 32 NK), 32-deep chunks through double-
 // buffered LDS images; the register loads run PF chunks ahead of the MFMAs (the operands were
 // written by the previous launch on other XCDs: each chunk is a MALL round trip).  One barrier
-// per chunk.
-template <int PF, int NK>
+// per chunk; SB (As0 == As1, Bs0 == Bs1: one image each) adds the barrier after the MFMAs that
+// double buffering saves, for half the LDS.
+template <int PF, int NK, bool SB = false>
 __device__ __forceinline__ void tile32_gemm_pf(const double* __restrict__ A, int64_t lda,
                                                const double* __restrict__ B, int64_t ldb, dbl4& acc,
                                                double* As0, double* As1, double* Bs0, double* Bs1) {
@@ -55,14 +56,20 @@ __device__ __forceinline__ void tile32_gemm_pf(const double* __restrict__ A, int
     }
     if (kc + PF < nk) T32_LOAD(PF - 1, kc + PF);
     mma32(As, Bs, acc);
+    if (SB) __syncthreads();
   }
 #undef T32_LOAD
 }
 
+// SBPF > 0: single-buffered at a fixed prefetch depth SBPF, K = 256 (the panel variant; one
+// instantiation, so the kernel holds only that depth's registers)
+template <int SBPF = 0>
 __device__ __forceinline__ void tile32_gemm_any(int pf, const double* __restrict__ A, int64_t lda,
                                                 const double* __restrict__ B, int64_t ldb, int K, dbl4& acc,
                                                 double* As0, double* As1, double* Bs0, double* Bs1) {
-  if (K == 128) {
+  if constexpr (SBPF > 0) {
+    tile32_gemm_pf<SBPF, 8, true>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
+  } else if (K == 128) {
     if (pf >= 2)
       tile32_gemm_pf<2, 4>(A, lda, B, ldb, acc, As0, As1, Bs0, Bs1);
     else

@@ -469,6 +469,10 @@ static int t32_pf() {
 //   V  Aout[i, G] = -Ain[i, G] P        (i outside G)
 //   P  Aout[G, G] = P, Pst = P          (next slot's warm start)
 // With `done` (fast path) an unconverged block hands the slot to the host (ST_NEED_GJ).
+// SBPF > 0: one LDS image per operand (17 KB instead of 34 KB; two barriers per chunk) at the
+// fixed prefetch depth SBPF (fewer VGPRs than the runtime-depth kernel's 132), B2 = 256; the
+// same arithmetic
+template <int SBPF>
 __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __restrict__ Ain,
                                                               double* __restrict__ Aout, int64_t D, int B2, int g,
                                                               const double* __restrict__ P, int64_t ldp,
@@ -483,7 +487,12 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
     if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
     return;
   }
-  __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
+  constexpr bool SB = SBPF > 0;
+  __shared__ __attribute__((aligned(16))) double img[SB ? 2 : 4][NB * ST];
+  double* const i0 = img[0];
+  double* const i1 = img[SB ? 0 : 1];
+  double* const i2 = img[SB ? 1 : 2];
+  double* const i3 = img[SB ? 1 : 3];
   const int nb = (int)(D / NB), gb = B2 / NB, g0 = g * gb, mb = nb - gb;
   const int nu = gb * mb;
   const int job = xcd_spread(blockIdx.x, gridDim.x);
@@ -492,8 +501,8 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
   KS_DECL(ks);
   if (job < nu) {
     const int a = job / mb, cq = job % mb, c = cq < g0 ? cq : cq + gb;
-    tile32_gemm_any(pf, P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, img[0], img[1],
-                    img[2], img[3]);
+    tile32_gemm_any<SBPF>(pf, P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, i0, i1, i2,
+                        i3);
     KS_MARK(ks);
     double* out = Aout + (G0 + (int64_t)a * NB) * D + (int64_t)c * NB;
     int flag = 0;
@@ -505,8 +514,7 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
     KS_END(ks, KS_PANEL);
   } else if (job < 2 * nu) {
     const int j2 = job - nu, iq = j2 / gb, c = j2 % gb, i = iq < g0 ? iq : iq + gb;
-    tile32_gemm_any(pf, Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, img[0], img[1],
-                    img[2], img[3]);
+    tile32_gemm_any<SBPF>(pf, Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, i0, i1, i2, i3);
     KS_MARK(ks);
     double* out = Aout + (int64_t)i * NB * D + G0 + (int64_t)c * NB;
     int flag = 0;
@@ -518,8 +526,7 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
     KS_END(ks, KS_PANEL);
   } else if (job >= 2 * nu + gb * gb) {  // look-ahead: LPZ = P LZ (next block's residual)
     const int j4 = job - 2 * nu - gb * gb, a = j4 / gb, c = j4 % gb;
-    tile32_gemm_any(pf, P + (int64_t)a * NB * ldp, ldp, LZ + (int64_t)c * NB, B2, B2, acc, img[0], img[1], img[2],
-                    img[3]);
+    tile32_gemm_any<SBPF>(pf, P + (int64_t)a * NB * ldp, ldp, LZ + (int64_t)c * NB, B2, B2, acc, i0, i1, i2, i3);
     double* out = LPZ + (int64_t)a * NB * B2 + (int64_t)c * NB;
     acc_foreach(acc, [&](int row, int col, double& v) { st_wt(out + (int64_t)row * B2 + col, v); });
   } else {
@@ -539,6 +546,17 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
     }
     if (check && flag) atomicOr(&st->flags, flag);
   }
+}
+
+using PanelKernel = void (*)(const double*, double*, int64_t, int, int, const double*, int64_t, double*, double*,
+                             const int*, int, State*, int, const double*, double*, int*);
+// the panel kernel at B2 = 256: single-buffered at prefetch depth MIDAGMA_EXP_PANEL_SB (1..3) from
+// D >= MIDAGMA_EXP_PANEL_SB_MIN on (experiment knobs), else the double-buffered runtime-depth one
+static PanelKernel panel_kernel_sb(int64_t D) {
+  const long pf = knob("MIDAGMA_EXP_PANEL_SB", 0);  // (read per launch: tests switch it in one process)
+  const long from = knob("MIDAGMA_EXP_PANEL_SB_MIN", 0);
+  if (D < from || pf <= 0) return binv_panel_kernel<0>;
+  return pf == 1 ? binv_panel_kernel<1> : pf == 2 ? binv_panel_kernel<2> : binv_panel_kernel<3>;
 }
 
 // ---- panels on 64 x 64 tiles (B2 = 256, large D) ------------------------------------------------
@@ -933,7 +951,7 @@ static bool blocked_inverse_lookahead(double* Mt, int64_t D, int B2, const BInvW
     else
       launch_neumann<8>(Ain, D, G0, bw, g, st, passes, true, nullptr, side);
     const int check = g == K2 - 1;
-    hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, side, Ain, Aout, D, B2, g,
+    hipLaunchKernelGGL(binv_panel_kernel<0>, dim3(2 * gb * mb + gb * gb), dim3(NTHREADS), 0, side, Ain, Aout, D, B2, g,
                        bw.P, (int64_t)B2, Pe, Po, bw.done + g, check, st, t32_pf(), nullptr, nullptr, nullptr);
     if (g < K2 - 1) {
       HIP_TRY(hipEventRecord(ev[1 + 2 * g], side));
@@ -1047,7 +1065,8 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
       hipLaunchKernelGGL(chains ? binv_panel64_kernel<true> : binv_panel64_kernel<false>, dim3(2 * 4 * m64 + 16),
                          dim3(NTHREADS), 0, stream, Ain, Aout, D, g, P, ldp, Pe, Po, done, check, st, zsync);
     } else
-    hipLaunchKernelGGL(binv_panel_kernel, dim3(2 * gb * mb + gb * gb * (ahead ? 2 : 1)), dim3(NTHREADS), 0, stream,
+    hipLaunchKernelGGL(B2 != 256 ? binv_panel_kernel<0> : panel_kernel_sb(D),
+                       dim3(2 * gb * mb + gb * gb * (ahead ? 2 : 1)), dim3(NTHREADS), 0, stream,
                        Ain, Aout, D, B2, g, P, ldp, Pe, Po, done, check, st, t32_pf(), ahead ? bw.LZ : nullptr,
                        ahead ? bw.LPZ : nullptr, zsync);
     if (mb > 0) {

@@ -146,6 +146,30 @@ def test_trail_series_bit_identical(monkeypatch, d):
         assert out[w][2] == out["0"][2]
 
 
+@pytest.mark.parametrize("d", [1000, 3000])
+def test_panel_single_buffered_bit_identical(monkeypatch, d):
+    """The panel launch single-buffered at a fixed prefetch depth (MIDAGMA_EXP_PANEL_SB = 1, 2, 3:
+    blockinv.hip binv_panel_kernel<SBPF>, the same tile arithmetic with one LDS image per operand)
+    leaves W, the iterations and the checkpoint objectives bit-identical to the product's panel.
+    d = 1000 (32 x 32 trailing tiles) and 3000 (the 128-tile update with the series inside);
+    checkpoints every 10; 30 steps."""
+    X, _, _ = make_dataset(d, d + 500, seed=5)
+    Xc = X - X.mean(0)
+    cov = Xc.T @ Xc / X.shape[0]
+    out = {}
+    for pf in ("0", "1", "2", "3"):
+        monkeypatch.setenv("MIDAGMA_EXP_PANEL_SB", pf)
+        s = _solver(d, cov)
+        W = np.zeros((d, d))
+        r = s.minimize(W, 1.0, 30, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=10, want_checkpoints=True)
+        out[pf] = (W, r.iters, [c.obj for c in r.checkpoints])
+        s.close()
+    for pf in ("1", "2", "3"):
+        assert out[pf][1] == out["0"][1] == 30
+        assert np.array_equal(out[pf][0], out["0"][0])
+        assert out[pf][2] == out["0"][2]
+
+
 @pytest.mark.parametrize("d", [8, 20, 32])
 @pytest.mark.parametrize("mode", ["opt", "log"])
 def test_small_path_tcc_vs_graph_path(d, mode, monkeypatch):
