@@ -2,6 +2,7 @@
 // that runs the cov score GEMM beside the last trailing update (gemm.hip, gemm_trail_kernel).
 #pragma once
 
+#include "kstamps.h"
 #include "nm16.h"
 
 namespace midagma {
@@ -113,5 +114,73 @@ __device__ __forceinline__ void binv_trail_tile(int job, const double* __restric
   if (check && flag) atomicOr(&st->flags, flag);
 }
 
+
+// One job of the panels of outer step g (one 32 x 32 tile; binv_panel_kernel's grid, or a job
+// claimed by the trailing update that runs the next block's panel, gemm.hip trail_panel_kernel):
+//   U  Aout[G, j] = P Ain[G, j]         (j outside G)           jobs [0, nu)
+//   V  Aout[i, G] = -Ain[i, G] P        (i outside G)           jobs [nu, 2 nu)
+//   P  Aout[G, G] = P, Pst = P          (next slot's warm start) jobs [2 nu, 2 nu + gb^2)
+//   look-ahead LPZ = P LZ                                        jobs past those
+// i0..i3: the LDS images (SBPF > 0: i0 == i1, i2 == i3)
+template <int SBPF>
+__device__ __forceinline__ void binv_panel_job(int job, const double* __restrict__ Ain, double* __restrict__ Aout,
+                                               int64_t D, int B2, int g, const double* __restrict__ P, int64_t ldp,
+                                               double* __restrict__ Pe, double* __restrict__ Po, int check,
+                                               State* __restrict__ st, int pf, const double* __restrict__ LZ,
+                                               double* __restrict__ LPZ, double* i0, double* i1, double* i2,
+                                               double* i3) {
+  const int nb = (int)(D / NB), gb = B2 / NB, g0 = g * gb, mb = nb - gb;
+  const int nu = gb * mb;
+  const int64_t G0 = (int64_t)g0 * NB;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  KS_DECL(ks);
+  if (job < nu) {
+    const int a = job / mb, cq = job % mb, c = cq < g0 ? cq : cq + gb;
+    tile32_gemm_any<SBPF>(pf, P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, i0, i1, i2,
+                        i3);
+    KS_MARK(ks);
+    double* out = Aout + (G0 + (int64_t)a * NB) * D + (int64_t)c * NB;
+    int flag = 0;
+    acc_foreach(acc, [&](int row, int col, double& v) {
+      st_wt(out + (int64_t)row * D + col, v);
+      flag |= domain_flag(v);
+    });
+    if (check && flag) atomicOr(&st->flags, flag);
+    KS_END(ks, KS_PANEL);
+  } else if (job < 2 * nu) {
+    const int j2 = job - nu, iq = j2 / gb, c = j2 % gb, i = iq < g0 ? iq : iq + gb;
+    tile32_gemm_any<SBPF>(pf, Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, i0, i1, i2, i3);
+    KS_MARK(ks);
+    double* out = Aout + (int64_t)i * NB * D + G0 + (int64_t)c * NB;
+    int flag = 0;
+    acc_foreach(acc, [&](int row, int col, double& v) {
+      st_wt(out + (int64_t)row * D + col, -v);
+      flag |= domain_flag(-v);
+    });
+    if (check && flag) atomicOr(&st->flags, flag);
+    KS_END(ks, KS_PANEL);
+  } else if (job >= 2 * nu + gb * gb) {  // look-ahead: LPZ = P LZ (next block's residual)
+    const int j4 = job - 2 * nu - gb * gb, a = j4 / gb, c = j4 % gb;
+    tile32_gemm_any<SBPF>(pf, P + (int64_t)a * NB * ldp, ldp, LZ + (int64_t)c * NB, B2, B2, acc, i0, i1, i2, i3);
+    double* out = LPZ + (int64_t)a * NB * B2 + (int64_t)c * NB;
+    acc_foreach(acc, [&](int row, int col, double& v) { st_wt(out + (int64_t)row * B2 + col, v); });
+  } else {
+    const int j3 = job - 2 * nu, a = j3 / gb, c = j3 % gb;
+    const double* src = P + (int64_t)a * NB * ldp + (int64_t)c * NB;
+    double* out = Aout + (G0 + (int64_t)a * NB) * D + G0 + (int64_t)c * NB;
+    double* Pst = (st && (st->slots & 1)) ? Po : Pe;  // this slot's store (parity of k)
+    double* ps = Pst + (int64_t)a * NB * B2 + (int64_t)c * NB;
+    int flag = 0;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int e = it * NTHREADS + threadIdx.x, row = e >> 5, col = e & 31;
+      const double v = src[(int64_t)row * ldp + col];
+      st_wt(out + (int64_t)row * D + col, v);
+      st_wt(ps + (int64_t)row * B2 + col, v);
+      flag |= domain_flag(v);
+    }
+    if (check && flag) atomicOr(&st->flags, flag);
+  }
+}
 
 }  // namespace midagma

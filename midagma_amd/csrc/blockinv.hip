@@ -453,8 +453,11 @@ __global__ __launch_bounds__(NTHREADS, 1) void panel5_kernel(const double* __res
 // the next block's series counters (launch_trail128_series), zeroed by the panel launch before
 // the trailing update that runs that series: [0] diagonal tiles, [32 p] phase p (p <= NM_PASSES)
 __device__ __forceinline__ void zero_sync(int* zsync) {
-  if (zsync && blockIdx.x == 0 && threadIdx.x <= NM_PASSES)
-    __hip_atomic_store(zsync + 32 * threadIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (zsync && blockIdx.x == 0 && threadIdx.x < 8) {  // the pass words, and the fused panel's (launch.h)
+    const int w = threadIdx.x <= NM_PASSES ? 32 * threadIdx.x
+                                           : (threadIdx.x == 5 ? TS_FIN : threadIdx.x == 6 ? TS_BAND : TS_JOB);
+    __hip_atomic_store(zsync + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // prefetch depth of the panel / trailing tiles (experiment knob MIDAGMA_EXP_T32_PF: 1, 2, 3;
@@ -489,63 +492,8 @@ __global__ __launch_bounds__(NTHREADS) void binv_panel_kernel(const double* __re
   }
   constexpr bool SB = SBPF > 0;
   __shared__ __attribute__((aligned(16))) double img[SB ? 2 : 4][NB * ST];
-  double* const i0 = img[0];
-  double* const i1 = img[SB ? 0 : 1];
-  double* const i2 = img[SB ? 1 : 2];
-  double* const i3 = img[SB ? 1 : 3];
-  const int nb = (int)(D / NB), gb = B2 / NB, g0 = g * gb, mb = nb - gb;
-  const int nu = gb * mb;
-  const int job = xcd_spread(blockIdx.x, gridDim.x);
-  const int64_t G0 = (int64_t)g0 * NB;
-  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  KS_DECL(ks);
-  if (job < nu) {
-    const int a = job / mb, cq = job % mb, c = cq < g0 ? cq : cq + gb;
-    tile32_gemm_any<SBPF>(pf, P + (int64_t)a * NB * ldp, ldp, Ain + G0 * D + (int64_t)c * NB, D, B2, acc, i0, i1, i2,
-                        i3);
-    KS_MARK(ks);
-    double* out = Aout + (G0 + (int64_t)a * NB) * D + (int64_t)c * NB;
-    int flag = 0;
-    acc_foreach(acc, [&](int row, int col, double& v) {
-      st_wt(out + (int64_t)row * D + col, v);
-      flag |= domain_flag(v);
-    });
-    if (check && flag) atomicOr(&st->flags, flag);
-    KS_END(ks, KS_PANEL);
-  } else if (job < 2 * nu) {
-    const int j2 = job - nu, iq = j2 / gb, c = j2 % gb, i = iq < g0 ? iq : iq + gb;
-    tile32_gemm_any<SBPF>(pf, Ain + (int64_t)i * NB * D + G0, D, P + (int64_t)c * NB, ldp, B2, acc, i0, i1, i2, i3);
-    KS_MARK(ks);
-    double* out = Aout + (int64_t)i * NB * D + G0 + (int64_t)c * NB;
-    int flag = 0;
-    acc_foreach(acc, [&](int row, int col, double& v) {
-      st_wt(out + (int64_t)row * D + col, -v);
-      flag |= domain_flag(-v);
-    });
-    if (check && flag) atomicOr(&st->flags, flag);
-    KS_END(ks, KS_PANEL);
-  } else if (job >= 2 * nu + gb * gb) {  // look-ahead: LPZ = P LZ (next block's residual)
-    const int j4 = job - 2 * nu - gb * gb, a = j4 / gb, c = j4 % gb;
-    tile32_gemm_any<SBPF>(pf, P + (int64_t)a * NB * ldp, ldp, LZ + (int64_t)c * NB, B2, B2, acc, i0, i1, i2, i3);
-    double* out = LPZ + (int64_t)a * NB * B2 + (int64_t)c * NB;
-    acc_foreach(acc, [&](int row, int col, double& v) { st_wt(out + (int64_t)row * B2 + col, v); });
-  } else {
-    const int j3 = job - 2 * nu, a = j3 / gb, c = j3 % gb;
-    const double* src = P + (int64_t)a * NB * ldp + (int64_t)c * NB;
-    double* out = Aout + (G0 + (int64_t)a * NB) * D + G0 + (int64_t)c * NB;
-    double* Pst = (st && (st->slots & 1)) ? Po : Pe;  // this slot's store (parity of k)
-    double* ps = Pst + (int64_t)a * NB * B2 + (int64_t)c * NB;
-    int flag = 0;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int e = it * NTHREADS + threadIdx.x, row = e >> 5, col = e & 31;
-      const double v = src[(int64_t)row * ldp + col];
-      st_wt(out + (int64_t)row * D + col, v);
-      st_wt(ps + (int64_t)row * B2 + col, v);
-      flag |= domain_flag(v);
-    }
-    if (check && flag) atomicOr(&st->flags, flag);
-  }
+  binv_panel_job<SBPF>(xcd_spread(blockIdx.x, gridDim.x), Ain, Aout, D, B2, g, P, ldp, Pe, Po, check, st, pf, LZ, LPZ,
+                       img[0], img[SB ? 0 : 1], img[SB ? 1 : 2], img[SB ? 1 : 3]);
 }
 
 using PanelKernel = void (*)(const double*, double*, int64_t, int, int, const double*, int64_t, double*, double*,
@@ -789,6 +737,15 @@ static int trail_series_workers(int64_t D) {
   return w > 0 ? (w + 7) / 8 * 8 : 0;
 }
 
+// workgroups that claim the next block's panel jobs inside the trailing update
+// (launch_trail128_panel; experiment knob MIDAGMA_EXP_TRAIL_PANEL, 0: the panel launches)
+// (-1: the fused launch's tile order and band hand-offs without its panel workgroups; the
+// panels stay launches: a diagnostic)
+static int trail_panel_workers(int64_t) {
+  const int w = (int)knob("MIDAGMA_EXP_TRAIL_PANEL", 0);
+  return w > 0 || w == -1 ? w : 0;
+}
+
 int binv_block(int64_t D) {
   // D = 128 (64 < d <= 128): one outer block, so the fast slot's whole inverse is the warm-started
   // product form (3 launches instead of the Gauss-Jordan's prologue and 4 block steps)
@@ -1002,6 +959,8 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
   const bool look = fast && bw.LW && K2 > 1 && D - B2 < TRAIL128_MIN && resid_lookahead();
   // blocks 1 .. K2 - 1's series inside the previous step's trailing update (128-tile updates)
   const bool tser = fast && bw.sync && B2 == 256 && K2 > 1 && D - B2 >= TRAIL128_MIN && trail_series_workers(D) > 0;
+  // ... and their panels too (the default 32 x 32 panel only)
+  const int tpan = tser && D < panel64_min() ? trail_panel_workers(D) : 0;  // (< 0: band order only)
   for (int g = 0; g < K2; ++g) {
     double* Ain = bufs[g & 1];
     double* Aout = bufs[(g + 1) & 1];
@@ -1059,7 +1018,9 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
                          Ain, Aout, D, g, P, Pe, Po, done, check, st);
     } else
 #endif
-    if (B2 == 256 && !ahead && D >= panel64_min()) {
+    if (tpan > 0 && g > 0) {
+      // block g's panel ran inside trailing update g - 1
+    } else if (B2 == 256 && !ahead && D >= panel64_min()) {
       const int m64 = (int)(D / 64) - 4;
       static const bool chains = knob("MIDAGMA_EXP_P64_CHAINS", 0) != 0;
       hipLaunchKernelGGL(chains ? binv_panel64_kernel<true> : binv_panel64_kernel<false>, dim3(2 * 4 * m64 + 16),
@@ -1080,7 +1041,14 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
           TrailSeries ts{bw.Pst + gn * B2 * B2, bw.Pst1 + gn * B2 * B2, {bw.Y[0], bw.Y[1]}, {bw.Q[0], bw.Q[1]}, bw.P,
                          bw.part + gn * (NM_PASSES + 1) * PART_STRIDE, bw.done + gn, zsync,
                          std::min(passes, NM_PASSES), nm_xmap(), trail_series_workers(D)};
-          launch_trail128_series(Ain, Aout, D, g, check != 0, st, ts, stream);
+          if (tpan != 0) {
+            TrailPanel tp{bw.Pst + gn * B2 * B2, bw.Pst1 + gn * B2 * B2,
+                          tpan > 0 && gn + 1 < K2 ? bw.sync + (gn + 1) * 256 : nullptr, gn == K2 - 1 ? 1 : 0,
+                          t32_pf(), tpan > 0 ? tpan : 0};
+            launch_trail128_panel(Ain, Aout, D, g, check != 0, st, ts, tp, stream);
+          } else {
+            launch_trail128_series(Ain, Aout, D, g, check != 0, st, ts, stream);
+          }
         } else {
           launch_trail128(Ain, Aout, D, B2, g, check, st, stream);
         }

@@ -1069,6 +1069,9 @@ struct TrailSeriesArgs {
   int exc_slot[4], exc_tile[4];   // the other slots whose tile is not xcd_remap's (-1: none)
   TrailSeries ts;
   State* st;
+  // trail_panel_kernel only (np = 0 elsewhere)
+  TrailPanel tp;
+  int np, nband, nband_pad, nrest, njobs;
 };
 
 constexpr uint64_t TS_TIMEOUT = 5000000;  // device real-time ticks (100 MHz): 50 ms
@@ -1144,6 +1147,7 @@ __device__ void ts_worker(const TrailSeriesArgs& a, int w, double* smem) {
                           a.st, s.xmap, red, red4);
     }
   }
+  if (a.np > 0) ts_signal(s.sync + TS_FIN, false);  // P and done are in (write-through stores)
 }
 
 __global__ __launch_bounds__(NTHREADS, 2) void trail_series_kernel(TrailSeriesArgs a) {
@@ -1163,6 +1167,132 @@ __global__ __launch_bounds__(NTHREADS, 2) void trail_series_kernel(TrailSeriesAr
   gemm_pipe_tile<0, B_PLAIN, EPI_SUB_MID>(t, 256, 256, a.tm, a.tm, a.Ain + G0, a.D, a.Aout + G0 * a.D, a.D, a.Aout,
                                           a.D, (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, 2, a.st, smem);
   if (s < 4) ts_signal(a.ts.sync, true);  // block g + 1's diagonal tile is in Aout (plain stores)
+}
+
+// ---- ... and block g + 1's panel in the same launch (large D) -----------------------------------
+// The panel launch of block g + 1 (≈35 us at D = 5120, its 2496 32 x 32 jobs latency-bound) needs
+// block g + 1's P (the series above) and block g + 1's row and column bands of Aout (148 of the
+// update's tiles); it writes those bands of Ain, which only the same 148 tiles read.  So the band
+// tiles run first (the EPI_SUB_CROSS_MID tile body: block g + 1's bands), the rest after them (the
+// EPI_SUB_MID body with both bands skipped), the series workers after the first round, and `np`
+// panel workgroups at the end of the grid: dispatched as the update's last round frees slots,
+// they wait for the band tiles and the series, then claim panel jobs from a counter.  Every job
+// runs binv_panel_job's arithmetic, so W is bit-identical to the separate launches.
+__device__ void tp_panel(const TrailSeriesArgs& a, double* smem) {
+  double* img = smem;  // 4 images of NB x ST doubles, then the hand-off word
+  int* go = reinterpret_cast<int*>(smem + 4 * NB * ST);
+  int* sync = a.ts.sync;
+  if (!ts_wait(sync + TS_BAND, a.nband, go)) return ts_abort(a);
+  if (!ts_wait(sync + TS_FIN, a.ts.workers, go)) return ts_abort(a);
+  if (__hip_atomic_load(&a.st->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ST_RUNNING) return;
+  if (__hip_atomic_load(a.ts.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {  // (the panel launch's test)
+    if (threadIdx.x == 0)
+      __hip_atomic_store(&a.st->status, (int32_t)ST_NEED_GJ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  for (;;) {
+    if (threadIdx.x == 0) *go = __hip_atomic_fetch_add(sync + TS_JOB, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int job = *go;
+    __syncthreads();  // (go is rewritten next round)
+    if (job >= a.njobs) return;
+    binv_panel_job<0>(job, a.Aout, const_cast<double*>(a.Ain), a.D, 256, a.g + 1, a.ts.P, 256, a.tp.Ppe, a.tp.Ppo,
+                      a.tp.pcheck, a.st, a.tp.pf, nullptr, nullptr, img, img + NB * ST, img + 2 * NB * ST,
+                      img + 3 * NB * ST);
+    __syncthreads();  // the images are reused by the next job
+  }
+}
+
+__device__ __forceinline__ void zero_sync2(int* z) {
+  if (threadIdx.x < 8) {
+    const int w = threadIdx.x <= NM_PASSES ? 32 * threadIdx.x
+                                           : (threadIdx.x == 5 ? TS_FIN : threadIdx.x == 6 ? TS_BAND : TS_JOB);
+    __hip_atomic_store(z + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS, 2) void trail_panel_kernel(TrailSeriesArgs a) {
+  if (a.st->status != ST_RUNNING) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int b = blockIdx.x, nw = a.ts.workers;
+  if (b == 0 && a.tp.zsync2) zero_sync2(a.tp.zsync2);  // block g + 2's words, for the next launch
+  if (b >= a.woff && b < a.woff + nw) {
+    ts_worker(a, b - a.woff, smem);
+    return;
+  }
+  const int s = b < a.woff ? b : b - nw;
+  if (s >= a.nband_pad + a.nrest) return tp_panel(a, smem);
+  const int64_t G0 = (int64_t)a.g * 256;
+  const int b0 = 2 * a.g;
+  if (s < a.nband) {
+    gemm_pipe_tile<0, B_PLAIN, EPI_SUB_CROSS_MID>(s, 256, 256, a.tm, 4, a.Ain + G0, a.D, a.Aout + G0 * a.D, a.D,
+                                                  a.Aout, a.D, (int64_t)a.check, const_cast<double*>(a.Ain), b0, 2,
+                                                  a.st, smem);
+    // (the tile decode: s < 2 tm are block g + 1's rows, columns s % tm; b0, b0 + 1 is its diagonal)
+    const bool diag = s < 2 * a.tm && (s % a.tm == b0 || s % a.tm == b0 + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {  // plain stores: one agent release, then the counters
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (diag) __hip_atomic_fetch_add(a.ts.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(a.ts.sync + TS_BAND, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (s >= a.nband_pad) {
+    // the rest: the grid without the pivot band and block g + 1's (4 tile rows and columns from b0)
+    const int r = s - a.nband_pad;
+    gemm_pipe_tile<0, B_PLAIN, EPI_SUB_MID>(xcd_remap(r, a.nrest), 256, 256, a.tm - 2, a.tm - 2, a.Ain + G0, a.D,
+                                            a.Aout + G0 * a.D, a.D, a.Aout, a.D, (int64_t)a.check,
+                                            const_cast<double*>(a.Ain), b0, 4, a.st, smem);
+  }
+}
+
+size_t trail_panel_lds() { return std::max(kGemmPipeLds, (size_t)(4 * NB * ST) * sizeof(double) + 16); }
+
+void launch_trail128_panel(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, State* st,
+                           const TrailSeries& ts, const TrailPanel& tp, hipStream_t stream) {
+  if (D % 128) throw std::invalid_argument("launch_trail128_panel: D must be a multiple of 128");
+  const int tm = (int)((D - 256) / 128), K2 = (int)(D / 256);
+  if (g + 1 >= K2 || tm < 8 || ts.workers <= 0 || ts.workers % 8 || ts.passes < 1 || ts.passes > NM_PASSES ||
+      tp.workers < 0)
+    throw std::invalid_argument("launch_trail128_panel: needs a next block, workers a multiple of 8, 1..4 passes");
+  const int nband = 2 * (2 * tm - 2), nrest = (tm - 2) * (tm - 2);
+  check_mid_shape(256, 256, (int64_t)tm * 4, nband, "launch_trail128_panel");
+  check_mid_shape(256, 256, (int64_t)nrest, nrest, "launch_trail128_panel");
+  TrailSeriesArgs a{};
+  a.Ain = Ain;
+  a.Aout = Aout;
+  a.D = D;
+  a.g = (int)g;
+  a.check = check ? 1 : 0;
+  a.tm = tm;
+  for (int k = 0; k < 4; ++k) a.diag[k] = a.exc_slot[k] = a.exc_tile[k] = -1;
+  a.ts = ts;
+  a.st = st;
+  a.tp = tp;
+  a.np = tp.workers;
+  a.nband = nband;
+  a.nband_pad = (nband + 7) & ~7;  // the rest starts on an XCD boundary (xcd_remap)
+  a.nrest = nrest;
+  const int gb = 256 / NB, mb = (int)(D / NB) - gb;
+  a.njobs = 2 * gb * mb + gb * gb;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int ntiles = a.nband_pad + nrest;
+  a.woff = std::min(ntiles, 2 * cus) & ~7;  // the series workers after the first round of tiles
+  static bool attr = false;
+  if (!attr) {
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(trail_panel_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)trail_panel_lds()));
+    attr = true;
+  }
+  hipLaunchKernelGGL(trail_panel_kernel, dim3((unsigned)(ntiles + ts.workers + tp.workers)), dim3(NTHREADS),
+                     trail_panel_lds(), stream, a);
+  HIP_TRY(hipGetLastError());
 }
 
 // linear index of tile (bm, bn) (pivot band skipped) in gemm_pipe_tile's order for tm x tm tiles

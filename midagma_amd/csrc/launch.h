@@ -158,6 +158,19 @@ struct TrailSeries {
 };
 void launch_trail128_series(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, State* st,
                             const TrailSeries& ts, hipStream_t stream);
+// ... and block g + 1's panel too (B2 = 256): its jobs (binv_panel_job) are claimed by `workers`
+// more workgroups at the end of the grid once block g + 1's band tiles and series are done; the
+// panel launch of block g + 1 is skipped.  pcheck: the panel's domain flags (last block);
+// Ppe / Ppo: block g + 1's warm-start stores; zsync2: block g + 2's counters (zeroed here)
+struct TrailPanel {
+  double* Ppe;
+  double* Ppo;
+  int* zsync2;
+  int pcheck, pf, workers;
+};
+constexpr int TS_FIN = 160, TS_BAND = 192, TS_JOB = 208;  // sync words of the fused launch
+void launch_trail128_panel(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, State* st,
+                           const TrailSeries& ts, const TrailPanel& tp, hipStream_t stream);
 
 // --- dfinv.hip --------------------------------------------------------------
 // The fast slot's blocked inverse as one dataflow launch (tile tasks, host-planned order).

@@ -146,6 +146,33 @@ def test_trail_series_bit_identical(monkeypatch, d):
         assert out[w][2] == out["0"][2]
 
 
+@pytest.mark.parametrize("d", [2000, 3000])
+def test_trail_panel_bit_identical(monkeypatch, d):
+    """Block g + 1's panel inside trailing update g (MIDAGMA_EXP_TRAIL_PANEL = panel workgroups,
+    gemm.hip trail_panel_kernel: band tiles first, the series, then binv_panel_job's jobs claimed
+    from a counter) leaves W, the iterations and the checkpoint objectives bit-identical to the
+    series-inside-the-update path with the panel launches, and to the plain launches.  The series
+    runs inside the update (MIDAGMA_EXP_TRAIL_SERIES=64) at these sizes only when asked;
+    checkpoints every 10 mix pivoted and fast slots; 40 steps."""
+    X, _, _ = make_dataset(d, d + 500, seed=11)
+    Xc = X - X.mean(0)
+    cov = Xc.T @ Xc / X.shape[0]
+    out = {}
+    for ser, pan in (("0", "0"), ("64", "0"), ("64", "128"), ("64", "512")):
+        monkeypatch.setenv("MIDAGMA_EXP_TRAIL_SERIES", ser)
+        monkeypatch.setenv("MIDAGMA_EXP_TRAIL_PANEL", pan)
+        s = _solver(d, cov)
+        W = np.zeros((d, d))
+        r = s.minimize(W, 1.0, 40, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=10, want_checkpoints=True)
+        out[(ser, pan)] = (W, r.iters, [c.obj for c in r.checkpoints])
+        s.close()
+    ref = out[("0", "0")]
+    for k, v in out.items():
+        assert v[1] == ref[1] == 40, k
+        assert np.array_equal(v[0], ref[0]), k
+        assert v[2] == ref[2], k
+
+
 @pytest.mark.parametrize("d", [1000, 3000])
 def test_panel_single_buffered_bit_identical(monkeypatch, d):
     """The panel launch single-buffered at a fixed prefetch depth (MIDAGMA_EXP_PANEL_SB = 1, 2, 3:
