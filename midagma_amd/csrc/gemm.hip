@@ -300,7 +300,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm128_kernel(int64_t K, int64_t
     if (tid < s2) red[tid] += red[tid + s2];
     __syncthreads();
   }
-  if (tid == 0) loss_part[blockIdx.x] = red[0];
+  if (tid == 0) loss_part[EPI == EPI_SIGMOID_SPLIT ? blockIdx.x - per_slice : blockIdx.x] = red[0];
 }
 
 constexpr size_t kGemm128Lds = 4 * G_IMG * sizeof(double);
@@ -645,6 +645,60 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
     return;
   }
   double* Ct = C + (int64_t)z * slice_stride;
+  if (EPI == EPI_SIGMOID_SPLIT) {
+    // serial split-K of the sigmoid GEMM (two K halves; launch_gemm: grids of few tiles): the
+    // first half stores its partial at C + slice_stride and hands it over through the tile's flag
+    // (int words after the partial); the second half adds it while staging the epilogue, which
+    // then runs on the full sum and writes C.  Both halves of a tile sit on one XCD (launch_gemm:
+    // tiles % 8 == 0), and the first halves precede every second half in the grid, so each wait is
+    // on a workgroup already dispatched; the wait is bounded all the same.
+    int* flag = reinterpret_cast<int*>(C + 2 * slice_stride) + rem;
+    if (z == 0) {
+      double* Pt = C + slice_stride;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const int64_t row = m0 + 16 * i + acc_row(lane, tt);
+          const int64_t col = nw + 2 * acc_col(lane);
+          *reinterpret_cast<double2*>(Pt + row * ldc + col) = double2{acc[i][0][tt], acc[i][1][tt]};
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    int* ok = reinterpret_cast<int*>(smem);
+    __syncthreads();  // (every wave is done with the A images)
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int got = 0;
+      for (;;) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 1) {
+          got = 1;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000) break;  // 50 ms
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      *ok = got;
+      if (got) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (*ok == 0) {  // (never expected: reported as a failed step, not a silent half sum)
+      if (tid == 0 && st)
+        __hip_atomic_store(const_cast<int32_t*>(&st->status), (int32_t)ST_SINGULAR, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    Ct = C;
+  }
   if (EPI == EPI_STORE) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -671,8 +725,15 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) {
-      stg[(2 * tt) * 64] = acc[i][0][tt];
-      stg[(2 * tt + 1) * 64] = acc[i][1][tt];
+      if (EPI == EPI_SIGMOID_SPLIT) {  // the first K half's partial + this half (fixed order)
+        const int64_t row = m0 + 16 * i + acc_row(lane, tt), col = nw + 2 * acc_col(lane);
+        const double2 p = *reinterpret_cast<const double2*>(C + slice_stride + row * ldc + col);
+        stg[(2 * tt) * 64] = p.x + acc[i][0][tt];
+        stg[(2 * tt + 1) * 64] = p.y + acc[i][1][tt];
+      } else {
+        stg[(2 * tt) * 64] = acc[i][0][tt];
+        stg[(2 * tt + 1) * 64] = acc[i][1][tt];
+      }
     }
 #pragma unroll 1
     for (int tt = 0; tt < 4; ++tt) {
@@ -698,7 +759,7 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
     if (tid < s2) red[tid] += red[tid + s2];
     __syncthreads();
   }
-  if (tid == 0) loss_part[blockIdx.x] = red[0];
+  if (tid == 0) loss_part[EPI == EPI_SIGMOID_SPLIT ? blockIdx.x - per_slice : blockIdx.x] = red[0];
 }
 
 template <int AMODE, int BMODE, int EPI>
@@ -711,8 +772,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64
                                                                 const State* __restrict__ st) {
   if (st && st->status != ST_RUNNING) return;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  gemm_pipe_tile<AMODE, BMODE, EPI>(xcd_remap(blockIdx.x, gridDim.x), K, kslice, tiles_m, tiles_n, A, lda, B, ldb, C,
-                                    ldc, slice_stride, loss_part, m_valid, n_valid, st, smem);
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  if (EPI == EPI_SIGMOID_SPLIT) {  // (serial split: the K halves in grid order, z-major)
+    const int per = tiles_m * tiles_n, b = blockIdx.x, z = b >= per ? 1 : 0;
+    t = z * per + xcd_remap(b - z * per, per);
+  }
+  gemm_pipe_tile<AMODE, BMODE, EPI>(t, K, kslice, tiles_m, tiles_n, A, lda, B, ldb, C, ldc, slice_stride, loss_part,
+                                    m_valid, n_valid, st, smem);
 }
 
 
@@ -831,6 +897,8 @@ void gemm_setup_attributes() {
   set_attr_pipe<0, B_IMINUS, EPI_STORE>();
   set_attr_pipe<1, B_PLAIN, EPI_SIGMOID>();
   set_attr_pipe<0, B_PLAIN, EPI_SIGMOID>();
+  set_attr_pipe<1, B_PLAIN, EPI_SIGMOID_SPLIT>();
+  set_attr_pipe<0, B_PLAIN, EPI_SIGMOID_SPLIT>();
   set_attr_pipe<0, B_PLAIN, EPI_SUB_BAND>();
   set_attr_pipe<0, B_PLAIN, EPI_SUB_CROSS>();
   set_attr_pipe<0, B_PLAIN, EPI_SUB_CROSS_MID>();
@@ -860,19 +928,26 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
   static const bool force64 = knob_set("MIDAGMA_EXP_GEMM64");  // experiment knobs (knobs.h)
   static const bool no_pipe = knob_set("MIDAGMA_EXP_NO_PIPE");
   if (M % 128 == 0 && N % 128 == 0 && K % 16 == 0 && !force64 && !no_pipe &&
-      (epi == EPI_STORE || (epi == EPI_SIGMOID && split == 1 && bmode == B_PLAIN))) {
+      (epi == EPI_STORE || (epi == EPI_SIGMOID && (split == 1 || split == 2) && bmode == B_PLAIN))) {
     const int64_t ktiles16 = K / 16;
     const int64_t per16 = (ktiles16 + split - 1) / split;
     const int nsplit = (int)((ktiles16 + per16 - 1) / per16);
     const int tm = (int)(M / 128), tn = (int)(N / 128);
     const int64_t nwg = (int64_t)tm * tn * nsplit;
     const int64_t kslice = per16 * 16;
+    if (epi == EPI_SIGMOID && nsplit > 1 && (nsplit != 2 || (tm * tn) % 8 || slice_stride < M * ldc))
+      throw std::invalid_argument("launch_gemm: the serial split sigmoid needs 2 slices, tiles % 8 == 0 and C with "
+                                  "room for the partial and the flags");
 #define MIDAGMA_GEMMP(AM, BM, EP)                                                                         \
   hipLaunchKernelGGL((gemm_pipe_kernel<AM, BM, EP>), dim3((unsigned)nwg), dim3(NTHREADS), kGemmPipeLds, stream, K, \
                      kslice, tm, tn, A, lda, B, ldb, C, ldc, slice_stride, loss_part, m_valid, n_valid, st)
     if (epi == EPI_SIGMOID) {
       if (a_trans && N != K) throw std::invalid_argument("launch_gemm: sigmoid form");
-      if (a_trans)
+      if (nsplit > 1 && a_trans)
+        MIDAGMA_GEMMP(1, B_PLAIN, EPI_SIGMOID_SPLIT);
+      else if (nsplit > 1)
+        MIDAGMA_GEMMP(0, B_PLAIN, EPI_SIGMOID_SPLIT);
+      else if (a_trans)
         MIDAGMA_GEMMP(1, B_PLAIN, EPI_SIGMOID);
       else
         MIDAGMA_GEMMP(0, B_PLAIN, EPI_SIGMOID);

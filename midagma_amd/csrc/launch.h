@@ -393,7 +393,8 @@ enum GemmEpi : int { EPI_STORE = 0, EPI_SIGMOID = 1, EPI_SUB_BAND = 2 /* launch_
                      EPI_SUB_CROSS = 3 /* launch_trail128_split only */,
                      EPI_SUB_PRE = 4 /* EPI_SUB_BAND with C0 preloaded into the accumulators */,
                      EPI_SUB_MID = 5 /* EPI_SUB_BAND with C0 folded in during the 16 k-tiles (B2 = 256) */,
-                     EPI_SUB_CROSS_MID = 6 /* EPI_SUB_CROSS with the EPI_SUB_MID fold */ };
+                     EPI_SUB_CROSS_MID = 6 /* EPI_SUB_CROSS with the EPI_SUB_MID fold */,
+                     EPI_SIGMOID_SPLIT = 7 /* internal: launch_gemm's EPI_SIGMOID with split = 2 */ };
 void gemm_setup_attributes();
 // C[M x N] = op(A) * op(B); op(A) = A ([m][k], lda) or, if a_trans, A stored [k][m] (lda);
 // op(B) = B or (I - B) ([k][n], ldb).  M, N, K multiples of 64.  With split > 1

@@ -118,6 +118,7 @@ struct midagma_solver {
   const double* xw_a() const { return use_xt ? XT.p : X.p; }
   int64_t xw_lda() const { return use_xt ? n_pad : D; }
   int split = 1;
+  int sig_split = 1;  // the logistic sigmoid GEMM's serial split-K (launch_gemm; 2: Y holds the partial too)
   int64_t loss_part_count = 0;
 
   Params* d_params = nullptr;
@@ -442,8 +443,8 @@ struct midagma_solver {
       launch_gemm(n_pad, D, Kd(), xw_a(), xw_lda(), use_xt, iw ? iw : Wp, D, iw ? B_PLAIN : B_IMINUS, Y.p, D, EPI_STORE, 1,
                   0, nullptr, 0, 0, st, stream);
     } else {
-      launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, 1, 0, loss_part.p, n_local, d,
-                  st, stream);
+      launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, sig_split,
+                  sig_split > 1 ? n_pad * D : 0, loss_part.p, n_local, d, st, stream);
       launch_sum_vector(loss_part.p, loss_part_count, zbuf + D * D, st, stream);
     }
     if (split == 1) {
@@ -1176,7 +1177,20 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     s->n_pad = (n_local + 127) / 128 * 128;
     const size_t nx = (size_t)s->n_pad * D;
     s->X.alloc(nx);
-    s->Y.alloc(nx);
+    // logistic with few 128-tiles: the sigmoid GEMM in two serial K halves when its last round of
+    // tiles would be at most half full (n = 1e4, d = 1000: 632 tiles for 512 resident slots)
+    const int64_t sig_tiles = (s->n_pad / 128) * (D / 128);
+    const int sig_rule = (int)knob("MIDAGMA_EXP_SIG_SPLIT", 0);
+    s->sig_split = s->loss == MIDAGMA_LOSS_LOGISTIC && D % 128 == 0 && sig_tiles % 8 == 0 && sig_rule > 0 &&
+                           sig_tiles < 2048 && sig_tiles % 512 != 0 && sig_tiles % 512 <= 256
+                       ? 2
+                       : 1;
+    if (s->sig_split == 2) {  // the output, the first halves' partial, then one flag word per tile
+      s->Y.alloc(2 * nx + (size_t)(sig_tiles + 1) / 2);
+      HIP_TRY(hipMemsetAsync(s->Y.p + 2 * nx, 0, (size_t)(sig_tiles + 1) / 2 * sizeof(double), s->stream));
+    } else {
+      s->Y.alloc(nx);
+    }
     HIP_TRY(hipMemsetAsync(s->X.p, 0, nx * sizeof(double), s->stream));
     HIP_TRY(hipMemcpy2DAsync(s->X.p, D * sizeof(double), X, s->d * sizeof(double), s->d * sizeof(double), n_local,
                              on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s->stream));
@@ -1480,8 +1494,9 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
           launch_gemm(s->n_pad, D, s->Kd(), s->xw_a(), s->xw_lda(), s->use_xt, s->IW.p ? s->IW.p : s->W.p, D,
                       s->IW.p ? B_PLAIN : B_IMINUS, s->Y.p, D, EPI_STORE, 1, 0, nullptr, 0, 0, s->d_state, s->stream);
         else
-          launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID, 1, 0,
-                      s->loss_part.p, s->n_local, s->d, s->d_state, s->stream);
+          launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID,
+                      s->sig_split, s->sig_split > 1 ? s->n_pad * D : 0, s->loss_part.p, s->n_local, s->d,
+                      s->d_state, s->stream);
       });
       ms_out[5] = timed([&] {
         if (s->split == 1)

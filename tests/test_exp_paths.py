@@ -5,6 +5,8 @@ so that their DESIGN.md section 8 measurements stay repeatable.  Not part of the
 
     MIDAGMA_LIB=midagma_amd/libmidagma_hip_exp.so python -m pytest -m experiment tests
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -144,6 +146,42 @@ def test_trail_series_bit_identical(monkeypatch, d):
         assert out[w][1] == out["0"][1] == 40
         assert np.array_equal(out[w][0], out["0"][0])
         assert out[w][2] == out["0"][2]
+
+
+def test_sigmoid_serial_split_score():
+    """The logistic sigmoid GEMM in two serial K halves (MIDAGMA_EXP_SIG_SPLIT=1, gemm.hip: the
+    first half's partial handed to the second through a per-tile flag; d = 1000, n = 1e4: 632
+    tiles) against the one-pass GEMM and numpy: the score gradient within 1e-12 of max|G| and the
+    loss within 1e-12 relative (the halves change the sum order of the pre-activations only)."""
+    from midagma_amd.solver import HipSolver
+    d, n = 1000, 10000
+    rng = np.random.default_rng(3)
+    X = (rng.uniform(size=(n, d)) < 0.3).astype(np.float64)
+    cov = X.T @ X / n
+    W = rng.normal(scale=0.02, size=(d, d))
+    np.fill_diagonal(W, 0.0)
+    out = {}
+    for k in ("0", "1", "0b"):
+        os.environ["MIDAGMA_EXP_SIG_SPLIT"] = k[0]
+        try:
+            s = HipSolver(d, "logistic", "data", device=0)
+            s.set_cov(cov)
+            s.set_data(X, n_global=n)
+            s.score_partial(W)
+            out[k] = s.score_finish()
+            s.close()
+        finally:
+            os.environ.pop("MIDAGMA_EXP_SIG_SPLIT", None)
+    (l0, G0), (l1, G1), (l2, G2) = out["0"], out["1"], out["0b"]
+    assert l0 == l2 and np.array_equal(G0, G2)  # the one-pass path is deterministic
+    scale = np.abs(G0).max()
+    assert np.abs(G1 - G0).max() <= 1e-12 * scale
+    assert abs(l1 - l0) <= 1e-12 * abs(l0)
+    Z = X @ W
+    ref_loss = (np.logaddexp(0.0, Z) - X * Z).sum() / n
+    ref_G = X.T @ (1.0 / (1.0 + np.exp(-Z))) / n - cov
+    assert abs(l1 - ref_loss) <= 1e-10 * abs(ref_loss)
+    assert np.abs(G1 - ref_G).max() <= 1e-10 * np.abs(ref_G).max()
 
 
 @pytest.mark.parametrize("d", [2000, 3000])
