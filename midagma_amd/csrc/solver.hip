@@ -1180,7 +1180,7 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     // logistic with few 128-tiles: the sigmoid GEMM in two serial K halves when its last round of
     // tiles would be at most half full (n = 1e4, d = 1000: 632 tiles for 512 resident slots)
     const int64_t sig_tiles = (s->n_pad / 128) * (D / 128);
-    const int sig_rule = (int)knob("MIDAGMA_EXP_SIG_SPLIT", 0);
+    const int sig_rule = (int)knob("MIDAGMA_EXP_SIG_SPLIT", 1);
     s->sig_split = s->loss == MIDAGMA_LOSS_LOGISTIC && D % 128 == 0 && sig_tiles % 8 == 0 && sig_rule > 0 &&
                            sig_tiles < 2048 && sig_tiles % 512 != 0 && sig_tiles % 512 <= 256
                        ? 2
