@@ -402,6 +402,10 @@ void gemm_setup_attributes();
 // EPI_SIGMOID: C = expit(acc); if loss_part != nullptr and st->ckpt_pending,
 // per-workgroup partials of sum(logaddexp(0,acc) - X*acc) over rows < m_valid,
 // cols < n_valid go to loss_part[blockIdx.y * gridDim.x + blockIdx.x] (X = A).
+// EPI_SIGMOID with split = 2 (128-tile grids with tiles % 8 == 0): the two K halves run in
+// series (EPI_SIGMOID_SPLIT); C must hold the output, the first halves' partial at
+// C + slice_stride (slice_stride >= M ldc) and one int flag per tile at C + 2 slice_stride, the
+// flags zero before the first launch (each launch leaves them zero).
 void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, bool a_trans, const double* B,
                  int64_t ldb, GemmB bmode, double* C, int64_t ldc, GemmEpi epi, int split, int64_t slice_stride,
                  double* loss_part, int64_t m_valid, int64_t n_valid, const State* st, hipStream_t stream);
