@@ -196,16 +196,20 @@ __device__ __noinline__ void small_control(const Params* __restrict__ pr, State&
     ctl.bc2 = S.bc2;
 }
 
-template <int DS, int NW, bool TCC>
+template <int DS, int NW, int TCC>
 __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     const Params* __restrict__ pr, State* __restrict__ stg, double* __restrict__ Wg, double* __restrict__ mg,
     double* __restrict__ vg, const double* __restrict__ covs, const double* __restrict__ minc,
     const double* __restrict__ mexc, const double* __restrict__ bc_table, CkptRec* __restrict__ ckpt,
     int64_t ckpt_cap, double* __restrict__ carry, double* __restrict__ pstore, int64_t n_slots, SmallTcc tc) {
   constexpr int NT = 64 * NW, TPR = DS / 16, TPW = TPR * TPR / NW, E = 4 * TPW;
-  // TCC: tcc_blk.h's body on this workgroup, NB x NB = NT threads (DS = 16: NB = 8, DS = 32: 16)
-  constexpr int TNB = DS / 2;
-  static_assert(!TCC || (TNB * TNB == NT && DS <= 32), "TCC in the small loop: d <= 32");
+  // TCC (0: off): tcc_blk.h's body on this workgroup.  4: NB x NB = NT threads of 4 x 4 blocks
+  // (DS = 16: NB = 8, DS = 32: 16); 5: one wave of 5 x 5 blocks (NB = 8, 2d <= 40: d <= 20), the
+  // other waves along without writes
+  constexpr int TBS = TCC == 5 ? 5 : 4;
+  constexpr int TNB = TCC == 5 ? 8 : DS / 2;
+  static_assert(TCC == 0 || (TCC == 4 && TNB * TNB == NT && DS <= 32) || (TCC == 5 && DS == 32 && NT >= 64),
+                "TCC in the small loop: d <= 32");
   static_assert(TPW * NW == TPR * TPR, "whole tiles per wave");
   constexpr int SW = DS + 2;                         // W, cov images: 16 rows x 4 cols per read
   constexpr int SI = ((DS + 15) / 32) * 32 + 16;     // I - W image: B operand rows, = 16 mod 32
@@ -237,8 +241,8 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   __shared__ State S;                         // the controller's (thread 0's) state
   __shared__ SmallCtl ctl;                    // its decision for the slot, read by every thread
   // TCC: the body's LDS and the regularizer's state words (scal, v, u), loaded at entry
-  __shared__ std::conditional_t<TCC, tccb::TccLds<TNB>, char> TL;
-  __shared__ double tsc[TCC ? 10 : 1], tvp[TCC ? 4 * TNB : 1], tup[TCC ? 4 * TNB : 1];
+  __shared__ std::conditional_t<TCC != 0, tccb::TccLds<TNB, TBS>, char> TL;
+  __shared__ double tsc[TCC ? 10 : 1], tvp[TCC ? TBS * TNB : 1], tup[TCC ? TBS * TNB : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane >> 4, c = lane & 15;
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     bool tcc_ran = false;
     if constexpr (TCC) {
       if (tc.mode == 2 || S.ckpt_pending) {
-        tccb::tcc_blk_body<TNB>([&](int i, int j) { return Wimg[i * SW + j]; },
+        tccb::tcc_blk_body<TNB, TBS>([&](int i, int j) { return Wimg[i * SW + j]; },
                                 [&](int i, int j) { return tc.S[(int64_t)i * D + j]; }, tc.ws, di, tc.mode, tc.eps,
                                 tc.m, tc.weight, tsc, tvp, tup, nullptr, D, TL);
         tcc_ran = true;
@@ -583,7 +587,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
         double gtr = 0.0;
         if constexpr (TCC) {  // Gobj + weight * trek_grad (linear.py:257-258), step.hip's order
           if (tc.mode == 2 && tcc_ran) {
-            gtr = tccb::tcc_grad_elem<TNB>(TL, di, rows[e], cols[e], wo, tc.m, tc.weight);
+            gtr = tccb::tcc_grad_elem<TNB, TBS>(TL, di, rows[e], cols[e], wo, tc.m, tc.weight);
             gobj = gobj + gtr;
           }
         }
@@ -685,6 +689,9 @@ void launch_small_minimize(const Params* pr, State* st, double* W, double* m, do
   const int ds = small_block(d);
   if (ds == 0) throw std::invalid_argument("small_minimize: d > 64");
   if (tcc && ds > 32) throw std::invalid_argument("small_minimize: the TCC regularizer needs d <= 32");
+  // d <= 20 on DS = 32: the one-wave 5 x 5 body (d=20: 10.4k -> 11.7k steps/s; experiment knob
+  // MIDAGMA_EXP_TCC_BS5=0: NB = 16, 4 x 4)
+  const bool bs5 = tcc && ds == 32 && d <= 20 && knob("MIDAGMA_EXP_TCC_BS5", 1) != 0;
   const SmallTcc tc = tcc ? *tcc : SmallTcc{};
 #define MIDAGMA_SMALL(DS_, NW_, TCC_)                                                                           \
   hipLaunchKernelGGL((small_minimize_kernel<DS_, NW_, TCC_>), dim3(1), dim3(64 * NW_), 0, stream, pr, st, W, m, v, \
@@ -692,16 +699,18 @@ void launch_small_minimize(const Params* pr, State* st, double* W, double* m, do
   // one wave per 16 x 16 tile
   if (ds == 16) {
     if (tcc)
-      MIDAGMA_SMALL(16, 1, true);
+      MIDAGMA_SMALL(16, 1, 4);
     else
-      MIDAGMA_SMALL(16, 1, false);
+      MIDAGMA_SMALL(16, 1, 0);
   } else if (ds == 32) {
-    if (tcc)
-      MIDAGMA_SMALL(32, 4, true);
+    if (bs5)
+      MIDAGMA_SMALL(32, 4, 5);
+    else if (tcc)
+      MIDAGMA_SMALL(32, 4, 4);
     else
-      MIDAGMA_SMALL(32, 4, false);
+      MIDAGMA_SMALL(32, 4, 0);
   } else {
-    MIDAGMA_SMALL(64, 16, false);
+    MIDAGMA_SMALL(64, 16, 0);
   }
 #undef MIDAGMA_SMALL
   HIP_TRY(hipGetLastError());

@@ -318,7 +318,7 @@ __global__ __launch_bounds__(NB * NB) void tcc_blk_kernel(const double* __restri
                                                             double* __restrict__ uprev, double* __restrict__ G) {
   if (!(st->status == ST_RUNNING && (mode == 2 || st->ckpt_pending))) return;  // tcc_gate_kernel's rule
   __shared__ TccLds<NB> L;
-  tcc_blk_body<NB>([&](int i, int j) { return W[(int64_t)i * D + j]; },
+  tcc_blk_body<NB, 4>([&](int i, int j) { return W[(int64_t)i * D + j]; },
                    [&](int i, int j) { return S[(int64_t)i * D + j]; }, ws, d, mode, eps, m, weight, scal, vprev,
                    uprev, G, D, L);
 }

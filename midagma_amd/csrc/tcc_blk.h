@@ -35,17 +35,20 @@ struct Max {
 // partials over the NB lanes of the same a by butterfly (fixed order); the vector steps (Noda
 // update, normalisation, value) run in wave 0 with wave reductions.  scal[6] counts the inverses of
 // the call (diagnostic).
-template <int NB>
+// BS: the register block edge (4; 5 for 2d <= 40 on one wave, NB = 8).  With BS = 5 a workgroup
+// may have more threads than NB x NB (the small loop's): the others take block (0, 0)'s
+// addresses, compute along, and write nothing (`act`); BS = 4 callers run exactly NB x NB.
+template <int NB, int BS = 4>
 struct TccBlk {
-  static constexpr int NT = NB * NB;  // threads
-  static constexpr int NM = 4 * NB;   // largest 2d
+  static constexpr int NT = NB * NB;  // active threads
+  static constexpr int NM = BS * NB;  // largest 2d
   static constexpr int VT = NM > 64 ? NM / 64 : 1;  // vector entries per wave-0 lane
 };
 
 // the body's LDS: pivot row / column pairs, transposed-GEMV partials, the vectors, scalars, A
-template <int NB>
+template <int NB, int BS = 4>
 struct TccLds {
-  static constexpr int NM = 4 * NB, LA = NM + 2;
+  static constexpr int NM = BS * NB, LA = NM + 2;
   double rowb[2][NM], colb[2][NM], part[NB * NB / 64][NM];
   double xs[NM], ys[NM], us[NM], zs[NM], scs[16], pivb[2];
   double al[NM * LA];
@@ -60,12 +63,13 @@ __device__ __forceinline__ double wave_reduce(double v, Op op) {
 }
 
 // M (holding A's block) <- sig I - A on the logical block, identity padding
-__device__ __forceinline__ void blk_shift(double (&M)[4][4], int n, int a, int b, double sig) {
+template <int BS>
+__device__ __forceinline__ void blk_shift(double (&M)[BS][BS], int n, int a, int b, double sig) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < BS; ++r)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int i = 4 * a + r, j = 4 * b + c;
+    for (int c = 0; c < BS; ++c) {
+      const int i = BS * a + r, j = BS * b + c;
       M[r][c] = (i < n && j < n) ? ((i == j ? sig : 0.0) - M[r][c]) : (i == j ? 1.0 : 0.0);
     }
 }
@@ -77,68 +81,72 @@ __device__ __forceinline__ void blk_shift(double (&M)[4][4], int n, int a, int b
 // 1 / piv at the pivot (gj.hip's result, in a different rounding).  The pivot loop runs over 4-row
 // blocks with the row inside the block unrolled, so every register index is static; the identity
 // padding up to a multiple of 4 pivots on 1 and changes nothing.
-template <int NB>
-__device__ __forceinline__ void blk_gj_inverse(double (&M)[4][4], int n, int a, int b, double (*rowb)[4 * NB],
-                                               double (*colb)[4 * NB], double* pivb) {
+template <int NB, int BS = 4>
+__device__ __forceinline__ void blk_gj_inverse(double (&M)[BS][BS], int n, int a, int b, bool act,
+                                               double (*rowb)[BS * NB], double (*colb)[BS * NB], double* pivb) {
   auto publish = [&](int q, auto Rc, int buf) {
     constexpr int R = decltype(Rc)::value;
-    if (a == q) {
+    if (act && a == q) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) rowb[buf][4 * b + c] = (b == q && c == R) ? 1.0 : M[R][c];
+      for (int c = 0; c < BS; ++c) rowb[buf][BS * b + c] = (b == q && c == R) ? 1.0 : M[R][c];
     }
     if (b == q) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < BS; ++r) {
         const bool piv = a == q && r == R;
-        colb[buf][4 * a + r] = piv ? M[r][R] - 1.0 : M[r][R];
-        if (piv) pivb[buf] = M[r][R];
+        if (act) {
+          colb[buf][BS * a + r] = piv ? M[r][R] - 1.0 : M[r][R];
+          if (piv) pivb[buf] = M[r][R];
+        }
         M[r][R] = piv ? 1.0 : 0.0;
       }
     }
   };
+  // (the buffer parity is that of p = BS q + R: static for even BS)
   auto step = [&](int q, auto Rc, int nq) {
     constexpr int R = decltype(Rc)::value;
-    constexpr int buf = R & 1;  // the parity of p = 4 q + R
+    const int buf = (BS & 1) ? ((BS * q + R) & 1) : (R & 1);
     __syncthreads();
     const double inv = 1.0 / pivb[buf];
-    double rp[4], cp[4];
+    double rp[BS], cp[BS];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) rp[c] = rowb[buf][4 * b + c] * inv;
+    for (int c = 0; c < BS; ++c) rp[c] = rowb[buf][BS * b + c] * inv;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cp[r] = colb[buf][4 * a + r];
+    for (int r = 0; r < BS; ++r) cp[r] = colb[buf][BS * a + r];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < BS; ++r)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) M[r][c] = M[r][c] - cp[r] * rp[c];
-    if constexpr (R < 3)
+      for (int c = 0; c < BS; ++c) M[r][c] = M[r][c] - cp[r] * rp[c];
+    if constexpr (R < BS - 1)
       publish(q, std::integral_constant<int, R + 1>(), buf ^ 1);
     else if (q + 1 < nq)
       publish(q + 1, std::integral_constant<int, 0>(), buf ^ 1);
   };
-  const int nq = (n + 3) >> 2;
+  const int nq = (n + BS - 1) / BS;
   publish(0, std::integral_constant<int, 0>(), 0);
   for (int q = 0; q < nq; ++q) {
     step(q, std::integral_constant<int, 0>(), nq);
     step(q, std::integral_constant<int, 1>(), nq);
     step(q, std::integral_constant<int, 2>(), nq);
     step(q, std::integral_constant<int, 3>(), nq);
+    if constexpr (BS > 4) step(q, std::integral_constant<int, 4>(), nq);
   }
 }
 
 // y = M x (x, y in LDS, NM entries): each thread's 4 row partials over its 4 columns, summed over
 // the NB threads of its row block (consecutive lanes) by butterfly
-template <int NB>
-__device__ __forceinline__ void blk_gemv(const double (&M)[4][4], int a, int b, bool skip_tr, int d,
+template <int NB, int BS = 4>
+__device__ __forceinline__ void blk_gemv(const double (&M)[BS][BS], int a, int b, bool act, bool skip_tr, int d,
                                          const double* x, double* y) {
-  double xv[4], s[4];
+  double xv[BS], s[BS];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) xv[c] = x[4 * b + c];
+  for (int c = 0; c < BS; ++c) xv[c] = x[BS * b + c];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < BS; ++r) {
     double acc = 0.0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const bool zero = skip_tr && 4 * a + r < d && 4 * b + c >= d;  // B: top-right block 0
+    for (int c = 0; c < BS; ++c) {
+      const bool zero = skip_tr && BS * a + r < d && BS * b + c >= d;  // B: top-right block 0
       acc += zero ? 0.0 : M[r][c] * xv[c];
     }
     s[r] = acc;
@@ -146,40 +154,40 @@ __device__ __forceinline__ void blk_gemv(const double (&M)[4][4], int a, int b, 
 #pragma unroll
   for (int off = 1; off < NB; off <<= 1)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], off);
-  if (b == 0) {
+    for (int r = 0; r < BS; ++r) s[r] += __shfl_xor(s[r], off);
+  if (act && b == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) y[4 * a + r] = s[r];
+    for (int r = 0; r < BS; ++r) y[BS * a + r] = s[r];
   }
   __syncthreads();
 }
 
 // y = M^T u: column partials per thread, summed over the row blocks of a wave by butterfly, then
 // over the waves through LDS (fixed order)
-template <int NB>
-__device__ __forceinline__ void blk_gemv_t(const double (&M)[4][4], int a, int b, const double* u,
-                                           double (*part)[4 * NB], double* y) {
+template <int NB, int BS = 4>
+__device__ __forceinline__ void blk_gemv_t(const double (&M)[BS][BS], int a, int b, bool act, const double* u,
+                                           double (*part)[BS * NB], double* y) {
   constexpr int NW = NB * NB / 64;  // waves
-  double uv[4], t[4];
+  double uv[BS], t[BS];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) uv[r] = u[4 * a + r];
+  for (int r = 0; r < BS; ++r) uv[r] = u[BS * a + r];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < BS; ++c) {
     double acc = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc += M[r][c] * uv[r];
+    for (int r = 0; r < BS; ++r) acc += M[r][c] * uv[r];
     t[c] = acc;
   }
 #pragma unroll
   for (int off = NB; off < 64; off <<= 1)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) t[c] += __shfl_xor(t[c], off);
-  if ((threadIdx.x & 63) < NB) {
+    for (int c = 0; c < BS; ++c) t[c] += __shfl_xor(t[c], off);
+  if (act && (threadIdx.x & 63) < NB) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) part[threadIdx.x >> 6][4 * b + c] = t[c];
+    for (int c = 0; c < BS; ++c) part[threadIdx.x >> 6][BS * b + c] = t[c];
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < 4 * NB; j += NB * NB) {
+  for (int j = threadIdx.x; j < BS * NB; j += NB * NB) {
     double acc = 0.0;
     for (int w = 0; w < NW; ++w) acc += part[w][j];
     y[j] = acc;
@@ -189,13 +197,13 @@ __device__ __forceinline__ void blk_gemv_t(const double (&M)[4][4], int a, int b
 
 // wave 0: warm start (tcc_init_kernel) into out: prev when the last solve converged and is inside
 // the cone, else ones (0 on the padding)
-template <int NB>
+template <int NB, int BS = 4>
 __device__ __forceinline__ void w0_init(const double* __restrict__ prev, int n, bool conv, bool warm_ok,
                                         double* out) {
   const int lane = threadIdx.x;
-  double pv[TccBlk<NB>::VT], mn = INFINITY, mx = 0.0;
+  double pv[TccBlk<NB, BS>::VT], mn = INFINITY, mx = 0.0;
 #pragma unroll
-  for (int t = 0; t < TccBlk<NB>::VT; ++t) {
+  for (int t = 0; t < TccBlk<NB, BS>::VT; ++t) {
     const int e = lane + 64 * t;
     pv[t] = e < n ? prev[e] : 0.0;
     if (e < n) {
@@ -207,19 +215,19 @@ __device__ __forceinline__ void w0_init(const double* __restrict__ prev, int n, 
   mx = wave_reduce(mx, Max());
   const bool warm = warm_ok && conv && mn > 1e-8 * mx && isfinite(mx);
 #pragma unroll
-  for (int t = 0; t < TccBlk<NB>::VT; ++t) {
+  for (int t = 0; t < TccBlk<NB, BS>::VT; ++t) {
     const int e = lane + 64 * t;
-    if (e < TccBlk<NB>::NM) out[e] = e < n ? (warm ? pv[t] : 1.0) : 0.0;
+    if (e < TccBlk<NB, BS>::NM) out[e] = e < n ? (warm ? pv[t] : 1.0) : 0.0;
   }
 }
 
 // wave 0: out = y / |y| with sum(out) > 0 (tcc_normalize_kernel), 0 on the padding
-template <int NB>
+template <int NB, int BS = 4>
 __device__ __forceinline__ void w0_normalize(const double* y, int n, double* out) {
   const int lane = threadIdx.x;
   double ss = 0.0, sm = 0.0;
 #pragma unroll
-  for (int t = 0; t < TccBlk<NB>::VT; ++t) {
+  for (int t = 0; t < TccBlk<NB, BS>::VT; ++t) {
     const int e = lane + 64 * t;
     if (e < n) {
       ss += y[e] * y[e];
@@ -230,7 +238,7 @@ __device__ __forceinline__ void w0_normalize(const double* y, int n, double* out
   sm = wave_reduce(sm, Add());
   const double inv = (sm < 0.0 ? -1.0 : 1.0) / sqrt(ss);
 #pragma unroll
-  for (int t = 0; t < TccBlk<NB>::VT; ++t) {
+  for (int t = 0; t < TccBlk<NB, BS>::VT; ++t) {
     const int e = lane + 64 * t;
     if (e < n) out[e] = y[e] * inv;
   }
@@ -241,12 +249,12 @@ __device__ __forceinline__ void w0_normalize(const double* y, int n, double* out
 // vprev, uprev: the regularizer's state words (global or LDS).  On return (all threads past a
 // barrier) L.xs = v, L.us = u, L.scs[4] = u.v + eps, L.scs[5] = u.u + eps, from which a caller
 // that passes G = nullptr forms the gradient itself (tcc_grad_elem).
-template <int NB, class WGet, class SGet>
+template <int NB, int BS, class WGet, class SGet>
 __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, int d, int mode, double eps, double m,
                                              double weight, double* __restrict__ scal, double* __restrict__ vprev,
                                              double* __restrict__ uprev, double* __restrict__ G, int64_t D,
-                                             TccLds<NB>& L) {
-  constexpr int NM = TccBlk<NB>::NM, VT = TccBlk<NB>::VT, LA = TccLds<NB>::LA;
+                                             TccLds<NB, BS>& L) {
+  constexpr int NM = TccBlk<NB, BS>::NM, VT = TccBlk<NB, BS>::VT, LA = TccLds<NB, BS>::LA;
   auto& rowb = L.rowb;
   auto& colb = L.colb;
   auto& part = L.part;
@@ -257,11 +265,14 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
   double* scs = L.scs;
   double* pivb = L.pivb;
   double* al = L.al;
-  const int tid = threadIdx.x, a = tid / NB, b = tid % NB, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // (BS = 4: every caller runs NB x NB threads, and a run-time `act` there put M in scratch)
+  const bool act = BS == 4 || tid < TccBlk<NB, BS>::NT;
+  const int a = act ? tid / NB : 0, b = act ? tid % NB : 0;
   const bool w0 = tid < 64;
   const int n = 2 * d;
   // A (the logical 2d x 2d block, zero padding) in LDS; registers hold the working matrix only
-  for (int e = tid; e < NM * NM; e += TccBlk<NB>::NT) {  // tcc_build_kernel
+  for (int e = tid; e < NM * NM; e += (int)blockDim.x) {  // tcc_build_kernel
     const int i = e / NM, j = e - i * NM;
     double v = 0.0;
     if (i < d) {
@@ -282,20 +293,20 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
     al[i * LA + j] = v;
   }
   __syncthreads();
-  double M[4][4];
-  auto load_a = [&](double (&T)[4][4]) {
+  double M[BS][BS];
+  auto load_a = [&](double (&T)[BS][BS]) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < BS; ++r)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) T[r][c] = al[(4 * a + r) * LA + 4 * b + c];
+      for (int c = 0; c < BS; ++c) T[r][c] = al[(BS * a + r) * LA + BS * b + c];
   };
   load_a(M);
   double sc[10];
 #pragma unroll
   for (int t = 0; t < 10; ++t) sc[t] = scal[t];
-  if (w0) w0_init<NB>(vprev, n, sc[9] != 0.0, sc[8] != 0.0, xs);
+  if (w0) w0_init<NB, BS>(vprev, n, sc[9] != 0.0, sc[8] != 0.0, xs);
   __syncthreads();
-  blk_gemv<NB>(M, a, b, false, d, xs, ys);
+  blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);
   if (w0) {  // tcc_sigma0_kernel
     double mx = -INFINITY;
 #pragma unroll
@@ -315,9 +326,9 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
   for (int k = 0; k < TCC_NODA_MAX; ++k) {  // tcc_noda_kernel, until the stop rule
     ++ninv;
     load_a(M);
-    blk_shift(M, n, a, b, sc[1]);
-    blk_gj_inverse<NB>(M, n, a, b, rowb, colb, pivb);
-    blk_gemv<NB>(M, a, b, false, d, xs, ys);
+    blk_shift<BS>(M, n, a, b, sc[1]);
+    blk_gj_inverse<NB, BS>(M, n, a, b, act, rowb, colb, pivb);
+    blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);
     if (w0) {
       double rmin = INFINITY, rmax = -INFINITY, ss = 0.0, bad = 0.0;
 #pragma unroll
@@ -369,24 +380,24 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
   }
   // the final inverse just above the root: two sweeps for v (x), two transposed for u
   load_a(M);
-  blk_shift(M, n, a, b, sc[1] * (1.0 + 1e-14));
-  blk_gj_inverse<NB>(M, n, a, b, rowb, colb, pivb);
+  blk_shift<BS>(M, n, a, b, sc[1] * (1.0 + 1e-14));
+  blk_gj_inverse<NB, BS>(M, n, a, b, act, rowb, colb, pivb);
   ++ninv;
   for (int t = 0; t < 2; ++t) {
-    blk_gemv<NB>(M, a, b, false, d, xs, ys);
-    if (w0) w0_normalize<NB>(ys, n, xs);
+    blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);
+    if (w0) w0_normalize<NB, BS>(ys, n, xs);
     __syncthreads();
   }
-  if (w0) w0_init<NB>(uprev, n, sc[9] != 0.0, sc[8] != 0.0, us);
+  if (w0) w0_init<NB, BS>(uprev, n, sc[9] != 0.0, sc[8] != 0.0, us);
   __syncthreads();
   for (int t = 0; t < 2; ++t) {
-    blk_gemv_t<NB>(M, a, b, us, part, ys);
-    if (w0) w0_normalize<NB>(ys, n, us);
+    blk_gemv_t<NB, BS>(M, a, b, act, us, part, ys);
+    if (w0) w0_normalize<NB, BS>(ys, n, us);
     __syncthreads();
   }
   load_a(M);  // the inverse is no longer needed
-  blk_gemv<NB>(M, a, b, false, d, xs, ys);  // A v
-  blk_gemv<NB>(M, a, b, true, d, us, zs);   // B u
+  blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);  // A v
+  blk_gemv<NB, BS>(M, a, b, act, true, d, us, zs);   // B u
   if (w0) {  // tcc_value_kernel
     double uav = 0.0, uv = 0.0, uu = 0.0, ubu = 0.0;
 #pragma unroll
@@ -434,7 +445,7 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
   __syncthreads();  // L.xs, L.us, L.scs[4..5] for every thread
   if (mode == 2 && G) {  // tcc_grad_kernel on the logical d x d block (the padding stays 0)
     const double denA = scs[4], denB = scs[5];
-    for (int e = tid; e < d * d; e += TccBlk<NB>::NT) {
+    for (int e = tid; e < d * d; e += (int)blockDim.x) {
       const int i = e / d, j = e - i * d;
       const double w = wget(i, j);
       double g = 0.0;
@@ -451,8 +462,8 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
 
 // weight * d value / d W[i][j] from the body's results (tcc_grad_kernel's arithmetic), for a
 // caller that forms the gradient per element (w = W[i][j], zero gives zero)
-template <int NB>
-__device__ __forceinline__ double tcc_grad_elem(const TccLds<NB>& L, int d, int i, int j, double w, double m,
+template <int NB, int BS = 4>
+__device__ __forceinline__ double tcc_grad_elem(const TccLds<NB, BS>& L, int d, int i, int j, double w, double m,
                                                 double weight) {
   if (w == 0.0) return 0.0;
   const double denA = L.scs[4], denB = L.scs[5];

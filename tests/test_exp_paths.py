@@ -242,6 +242,18 @@ def test_small_path_tcc_vs_graph_path(d, mode, monkeypatch):
     against the graph-replayed slots with the one-workgroup TCC launch (MIDAGMA_EXP_SMALL_TCC=0):
     same iterations and checkpoints; W within 1e-11 and the checkpoints' objective,
     reg_trek_value and grad_trek_norm within 1e-10 rel after 500 steps (checkpoint every 100)."""
+    _small_vs_graph(d, mode, monkeypatch, [("1", "0"), ("0", "0")])
+
+
+@pytest.mark.parametrize("d", [17, 20])
+@pytest.mark.parametrize("mode", ["opt", "log"])
+def test_small_path_tcc_bs5_vs_graph_path(d, mode, monkeypatch):
+    """The one-wave 5 x 5-block TCC body in the small loop (MIDAGMA_EXP_TCC_BS5=1, d <= 20 on the
+    DS = 32 kernel: 64 of its 256 threads hold the blocks) against the graph path, same bounds."""
+    _small_vs_graph(d, mode, monkeypatch, [("1", "1"), ("0", "0")])
+
+
+def _small_vs_graph(d, mode, monkeypatch, cases):
     X, _, _ = make_dataset(d, max(200, 10 * d), seed=7)
     o = _oracle(X, 100)
     rng = np.random.default_rng(d)
@@ -249,15 +261,16 @@ def test_small_path_tcc_vs_graph_path(d, mode, monkeypatch):
     pairs = iu[rng.uniform(size=len(iu)) < 0.3]
     K = 500
     runs = []
-    for small in ("1", "0"):
+    for small, bs5 in cases:
         monkeypatch.setenv("MIDAGMA_EXP_SMALL_TCC", small)
+        monkeypatch.setenv("MIDAGMA_EXP_TCC_BS5", bs5)
         s = _solver(d, o.cov)
         s.set_trek_tcc(pairs, mode=mode, weight=0.2)
         W = np.zeros((d, d))
         r = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=100, want_checkpoints=True)
         runs.append((W, r))
         s.close()
-    (Wa, ra), (Wb, rb) = runs
+    (Wa, ra), (Wb, rb) = runs[0], runs[-1]
     assert ra.iters == rb.iters == K
     assert np.abs(Wa - Wb).max() <= 1e-11
     assert [c.iter for c in ra.checkpoints] == [c.iter for c in rb.checkpoints]
