@@ -449,7 +449,8 @@ def bench_logistic(args, device, n, steps):
     d = args.d
     dev = torch.device("cuda", device)
     X, n_k, _ = make_shard(d, n, 1, 0, args.seed + 7, dev, sem="logistic")
-    Xh = X.cpu().numpy() if n <= 100_000 else None
+    # the value check's copy of X (n = 1e6: 8 GB of host memory, freed after the check)
+    Xh = X.cpu().numpy() if (n <= 100_000 or not args.no_check) else None
     s = HipSolver(d, "logistic", "data", device=device)
     s.set_data(X, n_global=n)
     del X
@@ -467,10 +468,15 @@ def bench_logistic(args, device, n, steps):
     prof = s.profile_parts(3)
     check = None
     if Xh is not None:
-        Kc = 20
+        # n = 1e4: 20 steps; n = 1e6: 2 steps (an oracle step there takes ~10 s) on the one-pass
+        # sigmoid kernel, where W = 0 makes the first gradient exact and the envelope ~0, so the
+        # bar is 1e-9 (the floor) unless the reference's own order envelope is wider
+        Kc = 20 if n <= 100_000 else 2
         Wc = np.zeros((d, d))
         s.minimize(Wc, 1.0, Kc, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
-        check = dict(W=Wc, X=Xh, cov=s.get_cov(), K=Kc)
+        check = dict(W=Wc, X=Xh, cov=s.get_cov(), K=Kc, floor=1e-5 if n <= 100_000 else 1e-9,
+                     threads=8 if n <= 100_000 else 16)
+    sig_form = s.debug_sig_split()
     s.close()
     flops = 2.0 * n * d * d
     t_sig = prof["gemm_xw"] * 1e-3
@@ -478,7 +484,9 @@ def bench_logistic(args, device, n, steps):
                 verified=(r.status == 0 and r.iters == steps + 3),
                 workload=f"logistic: d={d}, n={n}, data mode (X W GEMM with the sigmoid epilogue, X^T S), 1 GPU",
                 kernel_ms={k: round(v, 4) for k, v in prof.items()},
-                sigmoid_gemm={"kernel": "gemm_pipe_kernel<1, 0, 1> (EPI_SIGMOID)", "ms": prof["gemm_xw"],
+                sigmoid_gemm={"kernel": "gemm_pipe_kernel<1, 0, 1> (EPI_SIGMOID)" if sig_form == 1 else
+                              "gemm_pipe_kernel<1, 0, 7> (EPI_SIGMOID_SPLIT: two serial K halves)",
+                              "ms": prof["gemm_xw"],
                               "achieved_tflops": flops / t_sig / 1e12 if t_sig > 0 else None,
                               "frac_fp64_peak": flops / t_sig / 1e12 / FP64_MFMA_PEAK_TF if t_sig > 0 else None,
                               "algorithmic": f"2*n*d^2 = {flops:.3e} flop + n*d sigmoids"}, _check=check)
@@ -733,8 +741,9 @@ with threadpool_limits(limits=th):
                 from scipy.special import expit
                 S = expit(self.X @ W)
                 Z = np.zeros((self.d, self.d))
-                for c in range(0, self.n, 64):
-                    Z += self.X[c:c + 64].T @ S[c:c + 64]
+                blk = 64 if self.n <= 65536 else 1024  # (64-row products would take minutes at n=1e6)
+                for c in range(0, self.n, blk):
+                    Z += self.X[c:c + blk].T @ S[c:c + blk]
                 return (mu / self.n) * Z - mu * self.cov
 
         o = (Blocked if kind == "logistic_blocked" else LinearOracle)("l2" if kind == "l2" else "logistic")
@@ -833,16 +842,18 @@ def logistic_check(c, threads=8):
     tests/test_gpu_parity.py::test_logistic_data_mode_d100: no entry further than
     max(1e-5, 2x the envelope), no more entries beyond 1e-9 than the envelope moves (+50%)."""
     inp = {"X": c["X"], "cov": c["cov"], "K": c["K"], "lambda1": 0.03}
+    threads = c.get("threads", threads)
+    floor = c.get("floor", 1e-5)
     a = oracle_run("logistic", inp, threads)
     b = oracle_run("logistic_blocked", inp, threads)
     if a is None or b is None:
         return {"ok": False, "max_dW": None, "steps": c["K"], "error": "oracle run failed"}
     diff, env = np.abs(c["W"] - a["W"]), np.abs(b["W"] - a["W"])
     n_diff, n_env = int((diff > 1e-9).sum()), int((env > 1e-9).sum())
-    ok = bool(diff.max() <= max(1e-5, 2 * env.max()) and n_diff <= 1.5 * n_env + 10)
+    ok = bool(diff.max() <= max(floor, 2 * env.max()) and n_diff <= 1.5 * n_env + 10)
     return {"ok": ok, "max_dW": float(diff.max()), "envelope_max": float(env.max()), "entries_beyond_1e-9": n_diff,
-            "envelope_entries_beyond_1e-9": n_env, "steps": c["K"],
-            "oracle": "LinearOracle('logistic') and its 64-row blocked-sum variant (the reference's order envelope)"}
+            "envelope_entries_beyond_1e-9": n_env, "steps": c["K"], "tol": f"max({floor:g}, 2 x envelope)",
+            "oracle": "LinearOracle('logistic') and its row-blocked-sum variant (the reference's order envelope)"}
 
 
 def value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world, fit4=None, tcc_res=None):
@@ -922,8 +933,7 @@ def value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world,
     for lg in logi or []:
         c = lg.pop("_check", None)
         if c is None:
-            lg["value_check"] = {"ok": None, "note": "not checked at this n (the oracle's logistic step at n=1e6 "
-                                 "takes ~10 s); the n=1e4 leg checks the same kernels"}
+            lg["value_check"] = {"ok": None, "note": "skipped (--no-check)"}
         else:
             lg["value_check"] = logistic_check(c)
     for leg in (cov_res, large_res, small_res, mlp_res, tcc_res):

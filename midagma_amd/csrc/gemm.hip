@@ -328,6 +328,51 @@ constexpr int P_S = 132;
 constexpr int P_IMG = 16 * P_S;
 constexpr size_t kGemmPipeLds = 2 * P_IMG * sizeof(double);
 
+// The serial split sigmoid GEMM's per-tile hand-off (EPI_SIGMOID_SPLIT).  Every launch pairs
+// exactly one signal with exactly one take per tile, whatever the status word does during the
+// launch: a first half always signals (SIG_RAN after its partial is stored and released,
+// SIG_SKIPPED when it is gated off), a second half always takes the word and clears it, and uses
+// the partial only after SIG_RAN.  So every word is 0 again when the launch ends, and a take can
+// never see an earlier launch's signal.  Both halves of a tile sit on one XCD (launch_gemm: tiles
+// % 8 == 0), and every first half precedes every second half in the grid, so each wait is on a
+// workgroup already dispatched; the wait is bounded (50 ms) all the same, and an expired one
+// sets ST_HANDOFF_TIMEOUT, on which the host clears the words and raises.
+enum SigSplitWord : int { SIG_RAN = 1, SIG_SKIPPED = 2 };
+
+__device__ __forceinline__ void sig_split_signal(int* flag, int word) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// returns the first half's word (0: the wait expired); sh: one int of LDS
+__device__ __forceinline__ int sig_split_take(int* flag, const State* st, int* sh) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int got = 0;
+    for (;;) {
+      got = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (got != 0) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000) break;  // 50 ms
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (got != 0)
+      __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (st)
+      __hip_atomic_store(const_cast<int32_t*>(&st->status), (int32_t)ST_HANDOFF_TIMEOUT, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    *sh = got;
+  }
+  __syncthreads();
+  return *sh;
+}
+
 // One 128 x 128 output tile (t: its index after the XCD remap) of the pipelined GEMM; smem:
 // kGemmPipeLds bytes.  The body of gemm_pipe_kernel, and of the launch that runs the cov score
 // GEMM beside the blocked inverse's last trailing update (gemm_trail_kernel).
@@ -648,10 +693,8 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
   if (EPI == EPI_SIGMOID_SPLIT) {
     // serial split-K of the sigmoid GEMM (two K halves; launch_gemm: grids of few tiles): the
     // first half stores its partial at C + slice_stride and hands it over through the tile's flag
-    // (int words after the partial); the second half adds it while staging the epilogue, which
-    // then runs on the full sum and writes C.  Both halves of a tile sit on one XCD (launch_gemm:
-    // tiles % 8 == 0), and the first halves precede every second half in the grid, so each wait is
-    // on a workgroup already dispatched; the wait is bounded all the same.
+    // (int words after the partial; protocol: sig_split_signal / sig_split_take); the second half
+    // adds it while staging the epilogue, which then runs on the full sum and writes C.
     int* flag = reinterpret_cast<int*>(C + 2 * slice_stride) + rem;
     if (z == 0) {
       double* Pt = C + slice_stride;
@@ -663,40 +706,11 @@ __device__ __forceinline__ void gemm_pipe_tile(int t, int64_t K, int64_t kslice,
           const int64_t col = nw + 2 * acc_col(lane);
           *reinterpret_cast<double2*>(Pt + row * ldc + col) = double2{acc[i][0][tt], acc[i][1][tt]};
         }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      sig_split_signal(flag, SIG_RAN);
       return;
     }
-    int* ok = reinterpret_cast<int*>(smem);
-    __syncthreads();  // (every wave is done with the A images)
-    if (tid == 0) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int got = 0;
-      for (;;) {
-        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 1) {
-          got = 1;
-          break;
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000) break;  // 50 ms
-        __builtin_amdgcn_s_sleep(2);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *ok = got;
-      if (got) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (*ok == 0) {  // (never expected: reported as a failed step, not a silent half sum)
-      if (tid == 0 && st)
-        __hip_atomic_store(const_cast<int32_t*>(&st->status), (int32_t)ST_SINGULAR, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
+    __syncthreads();  // (every wave is done with the A images: the take's word overlays them)
+    if (sig_split_take(flag, st, reinterpret_cast<int*>(smem)) != SIG_RAN) return;
     Ct = C;
   }
   if (EPI == EPI_STORE) {
@@ -770,12 +784,24 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_pipe_kernel(int64_t K, int64
                                                                 int64_t slice_stride, double* __restrict__ loss_part,
                                                                 int64_t m_valid, int64_t n_valid,
                                                                 const State* __restrict__ st) {
-  if (st && st->status != ST_RUNNING) return;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   int t = xcd_remap(blockIdx.x, gridDim.x);
   if (EPI == EPI_SIGMOID_SPLIT) {  // (serial split: the K halves in grid order, z-major)
     const int per = tiles_m * tiles_n, b = blockIdx.x, z = b >= per ? 1 : 0;
     t = z * per + xcd_remap(b - z * per, per);
+    if (st && st->status != ST_RUNNING) {
+      // a gated-off half still takes part in its tile's hand-off, so every flag a launch sets is
+      // also cleared by it (the status may leave ST_RUNNING mid-launch: a hand-back of the
+      // inverse forked beside this GEMM)
+      int* flag = reinterpret_cast<int*>(C + 2 * slice_stride) + (t - z * per);
+      if (z == 0)
+        sig_split_signal(flag, SIG_SKIPPED);
+      else
+        (void)sig_split_take(flag, st, reinterpret_cast<int*>(smem));
+      return;
+    }
+  } else if (st && st->status != ST_RUNNING) {
+    return;
   }
   gemm_pipe_tile<AMODE, BMODE, EPI>(t, K, kslice, tiles_m, tiles_n, A, lda, B, ldb, C, ldc, slice_stride, loss_part,
                                     m_valid, n_valid, st, smem);

@@ -119,6 +119,7 @@ struct midagma_solver {
   int64_t xw_lda() const { return use_xt ? n_pad : D; }
   int split = 1;
   int sig_split = 1;  // the logistic sigmoid GEMM's serial split-K (launch_gemm; 2: Y holds the partial too)
+  int sig_split_force = 0;  // midagma_debug_sig_split: 0 the size rule, 1 never split, 2 split where the shape allows
   int64_t loss_part_count = 0;
 
   Params* d_params = nullptr;
@@ -993,8 +994,27 @@ struct midagma_solver {
     HIP_TRY(hipMemcpyAsync(&h_state[0], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
     download_matrix(Wh, W.p);
     HIP_TRY(hipStreamSynchronize(stream));
-    fill_result(h_state[0], res);
     begun = false;
+    check_handoff(h_state[0]);
+    fill_result(h_state[0], res);
+  }
+
+  // the serial split sigmoid GEMM's per-tile hand-off words (gemm.hip, sig_split_take): after the
+  // output and the first halves' partial in Y
+  void clear_sig_flags() {
+    if (sig_split != 2) return;
+    const int64_t tiles = (n_pad / 128) * (D / 128);
+    HIP_TRY(hipMemsetAsync(Y.p + 2 * n_pad * D, 0, (size_t)(tiles + 1) / 2 * sizeof(double), stream));
+  }
+  // A bounded in-kernel hand-off wait expired (ST_HANDOFF_TIMEOUT; never expected): the late
+  // first half has finished with its launch, so its word is cleared here, and the call raises
+  // instead of reporting a numerical outcome.
+  void check_handoff(const State& s) {
+    if (s.status != ST_HANDOFF_TIMEOUT) return;
+    begun = false;
+    clear_sig_flags();
+    HIP_TRY(hipStreamSynchronize(stream));
+    throw std::runtime_error("sigmoid GEMM: a K-half hand-off wait timed out (50 ms); the step was not applied");
   }
 
   static void fill_result(const State& s, midagma_result* res) {
@@ -1181,10 +1201,10 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     // tiles would be at most half full (n = 1e4, d = 1000: 632 tiles for 512 resident slots)
     const int64_t sig_tiles = (s->n_pad / 128) * (D / 128);
     const int sig_rule = (int)knob("MIDAGMA_EXP_SIG_SPLIT", 1);
-    s->sig_split = s->loss == MIDAGMA_LOSS_LOGISTIC && D % 128 == 0 && sig_tiles % 8 == 0 && sig_rule > 0 &&
-                           sig_tiles < 2048 && sig_tiles % 512 != 0 && sig_tiles % 512 <= 256
-                       ? 2
-                       : 1;
+    const bool sig_ok = s->loss == MIDAGMA_LOSS_LOGISTIC && D % 128 == 0 && sig_tiles % 8 == 0;
+    s->sig_split = sig_ok && sig_rule > 0 && sig_tiles < 2048 && sig_tiles % 512 != 0 && sig_tiles % 512 <= 256 ? 2 : 1;
+    if (s->sig_split_force == 1) s->sig_split = 1;  // midagma_debug_sig_split (tests)
+    if (s->sig_split_force == 2 && sig_ok) s->sig_split = 2;
     if (s->sig_split == 2) {  // the output, the first halves' partial, then one flag word per tile
       s->Y.alloc(2 * nx + (size_t)(sig_tiles + 1) / 2);
       HIP_TRY(hipMemsetAsync(s->Y.p + 2 * nx, 0, (size_t)(sig_tiles + 1) / 2 * sizeof(double), s->stream));
@@ -1553,6 +1573,7 @@ int midagma_poll(midagma_solver* s, midagma_result* res) {
   return guarded(s, [&] {
     HIP_TRY(hipMemcpyAsync(&s->h_state[1], s->d_state, sizeof(State), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    s->check_handoff(s->h_state[1]);
     midagma_solver::fill_result(s->h_state[1], res);
     return MIDAGMA_OK;
   });
@@ -1566,6 +1587,31 @@ int midagma_end(midagma_solver* s, double* W, midagma_result* res) {
   });
   return singular_or_nonfinite(s, rc, res, W);
 }
+
+// Test hook (not in the public header): choose the logistic sigmoid GEMM's form for the next
+// set_data (0: the size rule, 1: the one-pass kernel, 2: the serial K split wherever the shape
+// allows it; -1: no change).  Returns the form the current data uses (1 or 2).
+extern "C" int midagma_debug_sig_split(midagma_solver* s, int mode) {
+  if (!s || mode < -1 || mode > 2) return -1;
+  if (mode >= 0) s->sig_split_force = mode;
+  return s->sig_split;
+}
+
+// Test hooks (not in the public header) for the hand-back path of the blocked inverse:
+// spoil_warm zeroes the stored diagonal-block inverses of the last two slots, so the next fast
+// slot's warm start is 0, its residual I, and its first product-form pass hands the slot back
+// (ST_NEED_GJ) while the rest of the slot (in data mode: the score GEMMs beside the forked
+// inverse) is running; handbacks counts the hand-backs the scheduler has re-run.
+extern "C" int midagma_debug_spoil_warm(midagma_solver* s) {
+  if (!s || !s->blocked()) return -1;
+  return guarded(s, [&] {
+    for (DevBuf* b : {&s->Pst2, &s->Pst2b})
+      if (b->p) HIP_TRY(hipMemsetAsync(b->p, 0, b->n * sizeof(double), s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MIDAGMA_OK;
+  });
+}
+extern "C" int64_t midagma_debug_handbacks(const midagma_solver* s) { return s ? s->handback_count : -1; }
 
 // Diagnostics of the fast blocked inverse (not in the public header): per outer block g,
 // out[g*(NM_PASSES+2) + 0] = done word, out[... + 1 + p] = ||Q_p||_inf of pass p (stale for

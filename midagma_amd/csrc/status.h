@@ -14,6 +14,8 @@ enum Status : int32_t {
   ST_SINGULAR = 4,      // non-finite inverse                            -> LinAlgError
   ST_NEED_GJ = 5,       // internal: the fast inverse could not run this slot (no usable warm
                         // start, or a log-det is due); the host re-runs it on the GJ path
+  ST_HANDOFF_TIMEOUT = 6,  // internal: a bounded in-kernel hand-off wait expired (never expected);
+                           // the host resets the hand-off words and raises RuntimeError
 };
 
 }  // namespace midagma

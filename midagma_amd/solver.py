@@ -204,6 +204,30 @@ class HipSolver:
             check(self.L.midagma_set_data(self.h, X.ctypes.data_as(C.c_void_p), n_local,
                                           int(n_global or n_local), 0), self.h, "set_data")
 
+    def debug_sig_split(self, mode: int | None = None) -> int:
+        """Test hook (not part of the public header): the logistic sigmoid GEMM's form for the
+        next set_data (None: leave it; 0: the size rule, 1: the one-pass kernel, 2: the serial K
+        split wherever the shape allows).  Returns the form the current data uses (1 or 2)."""
+        fn = self.L.midagma_debug_sig_split
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_int]
+        cur = fn(self.h, -1)
+        if mode is not None and fn(self.h, int(mode)) < 0:
+            raise ValueError(f"debug_sig_split: bad mode {mode!r}")
+        return int(cur)
+
+    def debug_spoil_warm(self):
+        """Test hook: zero the blocked inverse's stored warm starts, so the next fast slot hands
+        back (ST_NEED_GJ) from inside its forked inverse."""
+        fn = self.L.midagma_debug_spoil_warm
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p]
+        check(fn(self.h), self.h, "debug_spoil_warm")
+
+    def debug_handbacks(self) -> int:
+        """Test hook: the hand-backs the slot scheduler has re-run on the pivoted path so far."""
+        fn = self.L.midagma_debug_handbacks
+        fn.restype, fn.argtypes = C.c_int64, [C.c_void_p]
+        return int(fn(self.h))
+
     # fit()'s device data preparation (linear.py:406-428; the CPU test doubles override these)
     def colsum(self, X):
         return colsum_dev(X)
