@@ -46,8 +46,10 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", choices=["data", "cov"], default="data")
-    p.add_argument("--d", type=int, default=1000)
-    p.add_argument("--n", type=int, default=1_000_000)
+    # (--dim / --rows: the same options under names torch.distributed.run does not take for
+    # abbreviations of its own, e.g. --d for --duplicate-stdout-filters)
+    p.add_argument("--d", "--dim", dest="d", type=int, default=1000)
+    p.add_argument("--n", "--rows", dest="n", type=int, default=1_000_000)
     p.add_argument("--cov-n", type=int, default=10_000)
     p.add_argument("--cov-steps", type=int, default=2000)
     p.add_argument("--seed", type=int, default=0)
@@ -73,19 +75,178 @@ def parse():
     return p.parse_args()
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
 def relaunch_ranks(args):
     """`python bench.py --gpus N` (N > 1) outside a launcher: start one rank per GPU under
     torch.distributed.run as a child process (no exec; nothing here has touched the GPU),
-    relay its output (rank 0 prints the JSON line) and exit with its return code."""
-    import socket
+    relay its output (rank 0 prints the JSON line) and exit with its return code.  The ranks
+    supervise their GPU workers themselves (supervise_ranks: the fallback to the host-driven
+    all-reduce lives there, so it also covers an external launcher); this wait is only bounded
+    (MIDAGMA_BENCH_TOTAL_S, default 2 h)."""
     import subprocess
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     log("launching:", " ".join(cmd))
-    sys.exit(subprocess.run(cmd).returncode)
+    try:
+        rc = subprocess.run(cmd, timeout=float(os.environ.get("MIDAGMA_BENCH_TOTAL_S", "7200"))).returncode
+    except subprocess.TimeoutExpired:
+        log("bench ranks exceeded MIDAGMA_BENCH_TOTAL_S")
+        rc = 124
+    sys.exit(rc)
+
+
+def beat(what):
+    """Worker progress mark for the rank supervisor (MIDAGMA_BENCH_HEARTBEAT): a stalled worker
+    (a hung collective) is one whose file has not changed for MIDAGMA_BENCH_STALL_S."""
+    p = os.environ.get("MIDAGMA_BENCH_HEARTBEAT")
+    if p:
+        with open(p, "a") as f:
+            f.write(f"{time.time():.1f} {what}\n")
+
+
+def _run_worker(cmd, env, hb, stall, cap, store, key):
+    """One rank's GPU worker as a child process: its stdout and stderr relayed to this process's
+    stderr (stdout lines kept: rank 0's JSON line), ended when it exits, stalls, overruns, or
+    another rank's worker of the same attempt has failed (the store counter `key`).  Returns
+    (outcome, stdout lines, last stderr lines); outcome "ok" or why it failed."""
+    import signal
+    import subprocess
+    import threading
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    out, err = [], []
+
+    def pump(src, keep):
+        for ln in src:
+            keep.append(ln)
+            sys.stderr.write(ln)
+        sys.stderr.flush()
+    th = [threading.Thread(target=pump, args=(p.stdout, out), daemon=True),
+          threading.Thread(target=pump, args=(p.stderr, err), daemon=True)]
+    for t in th:
+        t.start()
+    t0 = last = time.time()
+    outcome = None
+    while outcome is None:
+        rc = p.poll()
+        if rc is not None:
+            outcome = "ok" if rc == 0 else f"worker exited {rc}"
+            break
+        now = time.time()
+        try:
+            last = max(last, os.path.getmtime(hb))
+        except OSError:
+            pass
+        if now - last > stall:
+            outcome = f"no progress for {stall:.0f} s (last mark: {_last_mark(hb)})"
+        elif now - t0 > cap:
+            outcome = f"still running after {cap:.0f} s"
+        elif int(store.add(key, 0)) > 0:
+            outcome = "stopped: another rank's worker failed"
+        else:
+            time.sleep(0.5)
+    if p.poll() is None:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        p.wait()
+    for t in th:
+        t.join(timeout=10)
+    if outcome != "ok" and not outcome.startswith("stopped"):
+        store.add(key, 1)
+    return outcome, [ln.rstrip("\n") for ln in out], [ln.rstrip("\n") for ln in err[-12:]]
+
+
+def _last_mark(hb):
+    try:
+        with open(hb) as f:
+            lines = f.read().strip().splitlines()
+        return lines[-1].split(" ", 1)[1] if lines else "none"
+    except OSError:
+        return "none"
+
+
+def supervise_ranks(args):
+    """Under torch.distributed.run (WORLD_SIZE > 1) every rank process supervises one GPU worker
+    (this script again, MIDAGMA_BENCH_WORKER=1) and never touches the GPU itself, so a failed or
+    hung multi-GPU path cannot cost the line:
+      * attempt 1: the in-library RCCL communicator (the all-reduce captured in the slot graphs);
+      * if any rank's worker exits non-zero, makes no progress for MIDAGMA_BENCH_STALL_S (300 s)
+        or runs past MIDAGMA_BENCH_ATTEMPT_S (1800 s), every worker of the attempt is killed and
+        attempt 2 runs fresh workers on the host-driven path (MIDAGMA_BENCH_COMM=host:
+        step_partial -> dist.all_reduce -> step_finish), on a fresh rendezvous port;
+      * rank 0 then times the CPU baseline on the host cores (no GPU; the workers are gone) and
+        prints the JSON line with the path taken and every failed attempt (`launch`).
+    The supervisors talk over gloo (CPU) on torchrun's own rendezvous; the workers build their own
+    process group on the port rank 0 picks."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    dist.init_process_group("gloo", timeout=datetime.timedelta(hours=3))
+    store = dist.distributed_c10d._get_default_store()
+    stall = float(os.environ.get("MIDAGMA_BENCH_STALL_S", "300"))
+    cap = float(os.environ.get("MIDAGMA_BENCH_ATTEMPT_S", "1800"))
+    first = os.environ.get("MIDAGMA_BENCH_COMM", "library")
+    paths = [first] if (first == "host" or os.environ.get("MIDAGMA_BENCH_BACKEND", "nccl") != "nccl") \
+        else ["library", "host"]
+    fake = os.environ.get("MIDAGMA_BENCH_WORKER_CMD")  # tests: a stand-in worker (JSON argv)
+    cmd = json.loads(fake) if fake else [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    import tempfile
+    td = tempfile.mkdtemp(prefix=f"midagma_bench_r{rank}_")
+    attempts, line, cov_out = [], None, None
+    for a, path in enumerate(paths):
+        port = [_free_port() if rank == 0 else None]
+        dist.broadcast_object_list(port, src=0)
+        hb = os.path.join(td, f"heartbeat{a}")
+        cov_out = os.path.join(td, f"cov{a}.npy")
+        env = dict(os.environ, MIDAGMA_BENCH_WORKER="1", MASTER_PORT=str(port[0]),
+                   TORCHELASTIC_USE_AGENT_STORE="False", MIDAGMA_BENCH_COMM=path, MIDAGMA_BENCH_HEARTBEAT=hb,
+                   MIDAGMA_BENCH_COV_OUT=cov_out)
+        t0 = time.time()
+        outcome, out, err = _run_worker(cmd, env, hb, stall, cap, store, f"attempt{a}_failed")
+        fails = torch.tensor([0 if outcome == "ok" else 1])
+        dist.all_reduce(fails)
+        per_rank = [None] * world if rank == 0 else None
+        dist.gather_object({"rank": rank, "outcome": outcome, "stderr_tail": err[-6:] if outcome != "ok" else []},
+                           per_rank, dst=0)
+        rec = {"comm_path": path, "failed_ranks": int(fails.item()), "seconds": round(time.time() - t0, 1)}
+        if rank == 0 and int(fails.item()):
+            rec["ranks"] = [r for r in per_rank if r["outcome"] != "ok"]
+        attempts.append(rec)
+        if int(fails.item()) == 0:
+            if rank == 0:
+                js = [x for x in out if x.startswith("{")]
+                line = json.loads(js[-1]) if js else None
+            break
+        log(f"bench attempt {a} ({path}) failed on {int(fails.item())} rank(s): {outcome}")
+    rc = 0
+    if rank == 0:
+        if line is None:
+            line = {"metric": "Adam steps/s, d=1000 linear DAGMA (l2, data mode)", "value": None, "unit": "steps/s",
+                    "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+                    "verified": False, "error": "every multi-GPU attempt failed (see launch.attempts)"}
+            rc = 1
+        line["launch"] = {"supervised": True, "comm_path": attempts[-1]["comm_path"] if line.get("value") else None,
+                          "attempts": attempts,
+                          "note": "each rank process ran its GPU work in a worker child; a failed or stalled "
+                                  "attempt was killed on every rank and the next path started fresh"}
+        if isinstance(line.get("comm"), dict):
+            line["comm"]["path_taken"] = attempts[-1]["comm_path"]
+        if line.get("value") and not args.no_cpu and os.path.exists(cov_out):
+            cpu = cpu_baseline(args, np.load(cov_out))
+            attach_cpu(line, cpu, line["value"])
+        print(json.dumps(line), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return rc
 
 
 def setup_dist(args):
@@ -179,6 +340,7 @@ def bench_data(args, world, rank, local):
     s.set_data(X, n_global=n)
     del X
     torch.cuda.empty_cache()
+    beat("data shard resident")
     allreduce = None
     comm = None
     # N > 1 over RCCL: the solver's own communicator (ABI 7), the score all-reduce captured in the
@@ -224,6 +386,7 @@ def bench_data(args, world, rank, local):
 
     steps(Wm)
     s.sync()
+    beat("warm-up steps done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -234,6 +397,7 @@ def bench_data(args, world, rank, local):
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    beat("timed steps done")
     r = s.poll()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
@@ -272,6 +436,8 @@ def bench_data(args, world, rank, local):
                              "one Python round per step")
         if lib_comm and host_enqueue:
             comm["host_enqueue_ms_per_step"] = sum(host_enqueue) / K * 1e3
+        # the rank count the in-library RCCL communicator itself reports (midagma_comm_ranks)
+        comm["rccl_ranks"] = s.comm_ranks if lib_comm else None
         # W must be bit-identical on every rank: compare (sum, sum of squares) over ranks
         v = np.array([Wf.sum(), (Wf * Wf).sum()])
         t = torch.tensor(np.concatenate([v, -v]), dtype=torch.float64, device=dev)
@@ -297,6 +463,7 @@ def bench_data(args, world, rank, local):
     prof = s.profile_parts(args.profile_reps) if (rank == 0 or lib_comm) else {}
     if rank != 0:
         prof = {}
+    beat("data leg profiled")
     out = dict(ms_per_step=elapsed / K * 1e3, value=K / elapsed, verified_iters=int(r.iters), verified=ok,
                n_local=n_k, prof=prof, D=s.D, sem_gen_s=t_gen, replicas_identical=replicas, comm=comm,
                W=Wf, cov=cov, steps_total=Wm + K)
@@ -606,19 +773,26 @@ def bench_tcc(args, device, with_cpu):
 
 def bench_cov_large(args, device):
     """Config 3: d=5000, n=5e4, l2, cov mode on one GPU -- the inverse-dominated
-    size.  X is generated and reduced to cov = X^T X / n on the GPU (torch plumbing: a CPU
-    generator would take minutes); the solver gets cov as the reference's fit() would."""
+    size.  X is generated on the GPU (csrc/sem.hip) and prepared as fit() prepares a device X
+    (linear.py:411, 428): the product's fixed-order column sums and in-place centring
+    (midagma_colsum_dev, midagma_center_dev), the Gram X^T X on the FP64 MFMA (midagma_gram)
+    and cov = G / n on the device (midagma_set_cov_dev)."""
     import torch
-    from midagma_amd.solver import HipSolver
+    from midagma_amd.solver import HipSolver, center_dev, colsum_dev, gram
     d, n = args.large_d, args.large_n
     dev = torch.device("cuda", device)
     X, _, _ = make_shard(d, n, 1, 0, args.seed, dev)
-    X -= X.mean(dim=0, keepdim=True)
-    cov = (X.T @ X / float(n)).cpu().numpy()
-    del X
-    torch.cuda.empty_cache()
     s = HipSolver(d, "l2", "cov", device=device)
-    s.set_cov(cov)
+    torch.cuda.synchronize(dev)
+    t_prep = time.perf_counter()
+    with torch.cuda.device(dev):
+        center_dev(X, colsum_dev(X), float(n))
+        G = gram(X, device)
+    s.set_cov_gram(G, float(n))
+    t_prep = time.perf_counter() - t_prep
+    del X, G
+    torch.cuda.empty_cache()
+    cov = s.get_cov()
     K = args.large_steps
     s.begin(np.zeros((d, d)), 1.0, K + 1000, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
     s.run_slots(3)
@@ -640,6 +814,8 @@ def bench_cov_large(args, device):
                 workload=f"config3: d={d}, n={n}, l2, cov mode (reference algorithm), 1 GPU",
                 kernel_ms={k: round(v, 4) for k, v in prof.items()},
                 slot_tflops=F / ((t1 - t0) / K) / 1e12, slot_frac_fp64_peak=F / ((t1 - t0) / K) / 1e12 / 78.6,
+                prep={"seconds": t_prep, "what": "centring, Gram and cov on the device through the product "
+                                                  "(midagma_colsum_dev, _center_dev, _gram, _set_cov_dev)"},
                 cov=cov, W_check=Wc, check_steps=Kc, check_iters=int(rc.iters))
 
 
@@ -1125,6 +1301,21 @@ def cpu_baseline(args, cov):
     return res
 
 
+def attach_cpu(line, cpu, value):
+    """The CPU baselines on the line: `cpu_baseline` is the port of the workload's own math at the
+    same n (`vs_cpu`); `cpu_reference_algorithm` is the reference's own algorithm (cov formed once,
+    O(d^3) per step: what the reference's fit() runs at d=1000), and `vs_cpu_reference_algorithm`
+    compares the headline with it -- the like-for-like comparison with the reference's CPU path."""
+    if "workload" in cpu:
+        line["cpu_baseline"] = cpu["workload"]
+        line["vs_cpu"] = value / cpu["workload"]["value"]
+    elif "reference_algorithm" in cpu:
+        line["cpu_baseline"] = cpu["reference_algorithm"]
+    if "reference_algorithm" in cpu:
+        line["cpu_reference_algorithm"] = cpu["reference_algorithm"]
+        line["vs_cpu_reference_algorithm"] = value / cpu["reference_algorithm"]["value"]
+
+
 def _pmc_kernel(kernel, d, n_k):
     """Name under which tools/pmc_summary.py files the data-mode GEMM: both GEMMs are
     gemm_pipe_kernel<1, 0, 0> (A from X^T / X, plain B), told apart by their grids."""
@@ -1159,8 +1350,12 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         relaunch_ranks(args)
+    if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and os.environ.get("MIDAGMA_BENCH_WORKER") != "1"
+            and os.environ.get("MIDAGMA_BENCH_SUPERVISE", "1") == "1"):
+        sys.exit(supervise_ranks(args))
     import torch
     world, rank, local = setup_dist(args)
+    beat("process group up")
     res = bench_data(args, world, rank, local) if args.workload == "data" and not args.no_data else None
     cov_res = None
     if rank == 0 and (args.workload == "cov" or (world == 1 and not args.no_cov)):
@@ -1191,8 +1386,12 @@ def main():
     fit4 = None
     if args.workload == "data" and not args.no_fit4:
         fit4 = bench_fit_config4(args, world, rank, local, res["ms_per_step"] if res else None)
+        beat("full fit (config 4) done")
     if not args.no_check:
         value_checks(res, cov_res, large_res, small_res, mlp_res, logi, rank, world, fit4, tcc_res)
+        beat("value checks done")
+    if rank == 0 and res is not None and os.environ.get("MIDAGMA_BENCH_COV_OUT"):
+        np.save(os.environ["MIDAGMA_BENCH_COV_OUT"], res["cov"])  # the supervisor's CPU baseline
     for leg in (small_res, mlp_res, tcc_res, *(logi or [])):
         if leg is not None:
             leg.pop("_check", None)
@@ -1229,7 +1428,9 @@ def main():
             dom, t_dom = ("gemm_xty", t_xty) if t_xty >= t_xw else ("gemm_xw", t_xw)
             ach = gemm_flops / t_dom / 1e12 if t_dom > 0 else None
             value, ms = res["value"], res["ms_per_step"]
-            metric = "Adam steps/s, d=1000 linear DAGMA (l2, data mode, X row-sharded, RCCL all-reduce per step)"
+            metric = ("Adam steps/s, d=1000 linear DAGMA (l2, data mode, X row-sharded over the GPUs, RCCL "
+                      "all-reduce of the score gradient per step)" if world > 1 else
+                      "Adam steps/s, d=1000 linear DAGMA (l2, data mode, X resident on 1 GPU)")
             cfg = {"workload": f"config4: d={d}, n={args.n} linear-Gaussian SEM, l2, data mode, rows sharded over "
                                f"{world} GPU(s)", "d": d, "n": args.n, "n_per_gpu": n_k,
                    "parallelism": f"dp{world} (row shards, W replicated)"}
@@ -1287,13 +1488,8 @@ def main():
             else:
                 line["cov_mode"] = cr
         if cpu:
-            if "workload" in cpu:
-                line["cpu_baseline"] = cpu["workload"]
-                line["vs_cpu"] = value / cpu["workload"]["value"]
-            elif "reference_algorithm" in cpu:
-                line["cpu_baseline"] = cpu["reference_algorithm"]
+            attach_cpu(line, cpu, value)
             if "reference_algorithm" in cpu and cov_res is not None:
-                line["cpu_reference_algorithm"] = cpu["reference_algorithm"]
                 line["cov_mode_vs_cpu_reference_algorithm"] = cov_res["value"] / cpu["reference_algorithm"]["value"]
         if large_res is not None:
             lr_ = {k: v for k, v in large_res.items() if k not in ("cov", "W_check", "check_steps", "check_iters")}

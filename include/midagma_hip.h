@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 7
+#define MIDAGMA_ABI_VERSION 8
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -89,6 +89,12 @@ int64_t midagma_padded_dim(const midagma_solver* s);
 int midagma_set_cov(midagma_solver* s, const double* cov, int64_t ld);
 /* mask_inc / mask_exc for the next minimize call (linear.py:217-222), host d x d or NULL. */
 int midagma_set_masks(midagma_solver* s, const double* mask_inc, const double* mask_exc);
+/* ABI 8: W's dtype in the reference's arithmetic (DagmaLinear(dtype=...), linear.py:29, 408, 429).
+ * float32 != 0: the loop emulates numpy's float32 array operations on W and Id -- W rounded to
+ * float32 after every in-place update (275, 235, 239), s*Id - W*W and Id - W in float32 (226, 244),
+ * M = inv + 1e-16 and 2 W o M^T in float32 (226, 248) -- with the inverse itself in float64 (a
+ * float32 getrf's bits cannot be reproduced).  Takes effect at the next minimize / begin. */
+int midagma_set_w_float32(midagma_solver* s, int float32);
 /* data mode: this rank's row shard of X (n_local x d, ld = d); n_global = rows over all ranks.
  * on_device != 0: X is a device pointer (copied). */
 int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_t n_global, int on_device);

@@ -63,6 +63,7 @@ EXPORTED = {
     "midagma_padded_dim": (_i64, [_vp]),
     "midagma_set_cov": (_int, [_vp, _dp, _i64]),
     "midagma_set_masks": (_int, [_vp, _dp, _dp]),
+    "midagma_set_w_float32": (_int, [_vp, _int]),
     "midagma_set_data": (_int, [_vp, _vp, _i64, _i64, _int]),
     "midagma_data_gram": (_int, [_vp]),
     "midagma_cov_from_zbuf": (_int, [_vp, _d]),

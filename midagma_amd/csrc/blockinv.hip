@@ -91,7 +91,8 @@ __global__ __launch_bounds__(NTHREADS) void build_resid0_kernel(const double* __
   const int kb = (int)(D / 32), nbuild = kb * kb;
   if ((int)blockIdx.x < nbuild) {
     __shared__ double tile[32][33];
-    build_at_tile<true, 32>((int)blockIdx.x / kb, (int)blockIdx.x % kb, W, ldw, At, D, d, pr->s, nullptr, tile);
+    build_at_tile<true, 32>((int)blockIdx.x / kb, (int)blockIdx.x % kb, W, ldw, At, D, d, pr->s, nullptr, tile,
+                            pr->w32 != 0);
   } else {
     __shared__ double red[4 * 256];
     nm_resid_body<16, 4, true>((int)blockIdx.x - nbuild, nullptr, 0, SFromW{W, ldw, d, pr}, Pe, Po, Y0, Q0, part0,

@@ -38,7 +38,8 @@ struct Params {
   double logit_scale; // 1/n for the logistic loss partial
   double d_log_s;     // d * log(s), host-rounded (linear.py:114)
   int64_t max_iter, checkpoint, d, D, ld_table;
-  int32_t has_inc, has_exc, logistic, pad_;
+  int32_t has_inc, has_exc, logistic;
+  int32_t w32;        // dtype=np.float32: W is float32 in the reference (f32r below)
   double trek_weight;  // PST trek regularizer (linear.py:257-258, 131-133): weight,
   int32_t trek_mode;   //   0 off, 1 'log' (value at checkpoints), 2 'opt' (+ gradient every step)
   int32_t pad2_;
@@ -84,6 +85,33 @@ constexpr int NORM_FIELDS = 10;  // sums of squares first, then the two extrema
 enum NormField : int { NF_GOBJ = 0, NF_GSCORE, NF_GDAG, NF_GL1, NF_GINC, NF_GTREK, NF_GSTEP, NF_W2, NF_WMAX, NF_WMIN };
 
 __host__ __device__ inline int64_t round_up64(int64_t x) { return (x + 63) / 64 * 64; }
+
+// dtype=np.float32 (reference linear.py:29, 408, 429): Id and W are float32, so numpy rounds
+// every array operation on them to float32 while cov and the gradients stay float64.  W is kept
+// in float64 buffers holding float32 values, and each float32 operation is emulated as the
+// float64 operation rounded to float32 (exact: 53 >= 2 * 24 + 2, so the double rounding of +, -,
+// * is innocuous).
+__host__ __device__ inline double f32r(double x) { return (double)(float)x; }
+// one entry of s I - W o W as linear.py:226 forms it (float32: s * Id - W * W in float32)
+__host__ __device__ inline double sw_entry(bool diag, double s, double w, bool w32) {
+  if (!w32) return (diag ? s : 0.0) - w * w;
+  const double ww = f32r(w * w);
+  return diag ? f32r(f32r(s) - ww) : -ww;
+}
+// one entry of I - W (linear.py:244; float32: Id - W rounds the diagonal's 1 - w)
+__host__ __device__ inline double one_minus(bool diag, double w, bool w32) {
+  const double v = (diag ? 1.0 : 0.0) - w;
+  return (w32 && diag) ? f32r(v) : v;
+}
+// the inverse's entry as linear.py:226, 248 use it: M = inv + 1e-16 (float32: the float32
+// inverse, modelled as the float64 one rounded, plus 1e-16 in float32)
+__host__ __device__ inline double m_entry(double inv, bool w32) {
+  return w32 ? f32r(f32r(inv) + f32r(1e-16)) : inv + 1e-16;
+}
+// 2 W o M^T (float32: a float32 product)
+__host__ __device__ inline double h_term(double w, double mt, bool w32) {
+  return w32 ? f32r((2.0 * w) * mt) : (2.0 * w) * mt;
+}
 
 }  // namespace midagma
 

@@ -53,7 +53,7 @@ __global__ __launch_bounds__(NTHREADS) void build_at_kernel(const double* __rest
   // s comes from device Params when given: graph replays must see each call's s
   const double s = pr ? pr->s : s_arg;
   __shared__ double tile[BT][BT + 1];
-  build_at_tile<SQUARE, BT>(blockIdx.y, blockIdx.x, X, ldx, At, D, d, s, IW, tile);
+  build_at_tile<SQUARE, BT>(blockIdx.y, blockIdx.x, X, ldx, At, D, d, s, IW, tile, pr && pr->w32);
 }
 
 // Reciprocal to ~1 ulp: hardware seed + two Newton steps (no IEEE division chain).

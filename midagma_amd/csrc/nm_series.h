@@ -29,15 +29,13 @@ __device__ __forceinline__ void splitk_load_b(const double* __restrict__ B, int6
 // (build_at_tile), so block 0's residual can run in build_at's launch (build_resid0_kernel)
 template <int L>
 __device__ __forceinline__ void splitk_load_a_w(const double* __restrict__ W, int64_t ldw, int64_t d, double s,
-                                                int m0, double (&a)[L]) {
+                                                int m0, double (&a)[L], bool w32) {
   const int64_t i = m0 + (threadIdx.x & 15), k0 = splitk_k0<L>();
 #pragma unroll
   for (int q = 0; q < L; ++q) {
     const int64_t k = k0 + q;
     if (i < d && k < d) {
-      const double x = W[k * ldw + i];
-      const double f = x * x;
-      a[q] = (k == i ? s : 0.0) - f;
+      a[q] = sw_entry(k == i, s, W[k * ldw + i], w32);
     } else {
       a[q] = (k == i) ? 1.0 : 0.0;
     }
@@ -124,7 +122,7 @@ __device__ __forceinline__ void nm_resid_body(int wg, const double* __restrict__
   const bool extrap = st->warm_run >= 2;
   double a[L], b[L];
   if (FROM_W)
-    splitk_load_a_w<L>(sw.W, sw.ldw, sw.d, sw.pr->s, m0, a);
+    splitk_load_a_w<L>(sw.W, sw.ldw, sw.d, sw.pr->s, m0, a, sw.pr->w32 != 0);
   else
     splitk_load_a<L>(S, lds, m0, a);
   splitk_load_b<L>(P1, B2, n0, b);

@@ -298,12 +298,13 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   }
   __syncthreads();
   if (!ctl.run) return;
+  const bool w32 = pr->w32 != 0;  // dtype=np.float32 (common.h f32r)
 #pragma unroll
   for (int e = 0; e < E; ++e)
     if (real[e]) {
       if (!ONE) Wimg[rows[e] * SW + cols[e]] = wv[e];
       if (rows[e] == cols[e]) wdiag[rows[e]] = wv[e];
-      IWimg[rows[e] * SI + cols[e]] = ((rows[e] == cols[e]) ? 1.0 : 0.0) - wv[e];
+      IWimg[rows[e] * SI + cols[e]] = one_minus(rows[e] == cols[e], wv[e], w32);
     }
   const double s_dom = pr->s;
   // the last two slots' inverses (warm start of the product form) and how many are valid;
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
       const int i = rows[e], j = cols[e];
       if (real[e]) {
         const double wji = ONE ? (i == j ? wdiag[i] : -IWimg[j * SI + i]) : Wimg[j * SW + i];
-        a[e] = ((i == j) ? s_dom : 0.0) - wji * wji;
+        a[e] = sw_entry(i == j, s_dom, wji, w32);
       } else {
         a[e] = (i == j) ? 1.0 : 0.0;
       }
@@ -525,7 +526,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 #pragma unroll
     for (int e = 0; e < E; ++e)
       if (real[e]) {
-        if (a[e] + 1e-16 < 0.0) fl |= 1;
+        if (m_entry(a[e], w32) < 0.0) fl |= 1;
         if (!isfinite(a[e])) fl |= 2;
       }
     {
@@ -537,7 +538,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 #pragma unroll
       for (int e = 0; e < E; ++e)
         if (real[e]) {
-          sd += (((rows[e] == cols[e]) ? 1.0 : 0.0) - wv[e]) * z[e];
+          sd += one_minus(rows[e] == cols[e], wv[e], w32) * z[e];
           l1 += fabs(wv[e]);
         }
       const double ld = tid < di ? log(fabs(piv[tid])) : 0.0;
@@ -572,11 +573,11 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
       const double wo = wv[e];
       if (act == ACT_STEP) {
         const int64_t idx = (int64_t)rows[e] * D + cols[e];
-        const double mt = a[e] + 1e-16;
+        const double mt = m_entry(a[e], w32);
         const double gs = pr->zscale * z[e];
         const double sg = sgn(wo);
         const double gl1 = pr->mu_l1 * sg;
-        const double gh = (2.0 * wo) * mt;
+        const double gh = h_term(wo, mt, w32);
         double gobj = gs + gl1;
         gobj = gobj + gh;
         double gi = 0.0;
@@ -597,6 +598,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
         const double vh = vx / bc2;
         const double gd = mh / (sqrt(vh) + 1e-8);
         double wn = wo - lr_a * gd;
+        if (w32) wn = f32r(wn);  // W -= lr * grad into a float32 W (linear.py:275)
         if (has_exc) wn = wn * mexc[idx];
         mv[e] = mm;
         vv[e] = vx;
@@ -615,16 +617,19 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
         }
       } else {
         const double gd = (mv[e] / bc1) / (sqrt(vv[e] / bc2) + 1e-8);
-        if (act == ACT_HALVE) {
-          const double wn = wo + lr_a * gd;
-          wv[e] = wn - lr_b * gd;
+        if (act == ACT_HALVE) {  // (float32 W: each in-place update rounds, linear.py:235, 239)
+          double wn = wo + lr_a * gd;
+          if (w32) wn = f32r(wn);
+          wn = wn - lr_b * gd;
+          wv[e] = w32 ? f32r(wn) : wn;
         } else {
-          wv[e] = wo + lr_a * gd;
+          const double wn = wo + lr_a * gd;
+          wv[e] = w32 ? f32r(wn) : wn;
         }
       }
       if (!ONE) Wimg[rows[e] * SW + cols[e]] = wv[e];
       if (rows[e] == cols[e]) wdiag[rows[e]] = wv[e];
-      IWimg[rows[e] * SI + cols[e]] = ((rows[e] == cols[e]) ? 1.0 : 0.0) - wv[e];
+      IWimg[rows[e] * SI + cols[e]] = one_minus(rows[e] == cols[e], wv[e], w32);
     }
     if (norms) {
 #pragma unroll

@@ -119,7 +119,8 @@ struct midagma_solver {
   int64_t xw_lda() const { return use_xt ? n_pad : D; }
   int split = 1;
   int sig_split = 1;  // the logistic sigmoid GEMM's serial split-K (launch_gemm; 2: Y holds the partial too)
-  int sig_split_force = 0;  // midagma_debug_sig_split: 0 the size rule, 1 never split, 2 split where the shape allows
+  int sig_split_force = 0;
+  bool w32 = false;  // midagma_set_w_float32: the reference's float32 W arithmetic (common.h f32r)  // midagma_debug_sig_split: 0 the size rule, 1 never split, 2 split where the shape allows
   int64_t loss_part_count = 0;
 
   Params* d_params = nullptr;
@@ -683,7 +684,7 @@ struct midagma_solver {
     }
     if (mode == MIDAGMA_MODE_COV) B2 = binv_block(D);
     // cov mode: build_at also writes I - W for the score GEMM's plain-B form
-    if (mode == MIDAGMA_MODE_COV && D % 128 == 0 && cov_iw) IW.alloc(DD);
+    if (mode == MIDAGMA_MODE_COV && ((D % 128 == 0 && cov_iw) || w32)) IW.alloc(DD);
     if (blocked() || data_binv_on()) {
       const int64_t b2 = binv_block(D);
       Malt.alloc(DD);
@@ -821,7 +822,9 @@ struct midagma_solver {
     p.beta2 = b2;
     p.c1 = 1 - b1;
     p.c2 = 1 - b2;
-    p.mu_l1 = mu_ * lambda1;
+    // (float32 W: mu * lambda1 * sign(W) is a float32 array, linear.py:248)
+    p.mu_l1 = w32 ? f32r(mu_ * lambda1) : mu_ * lambda1;
+    p.w32 = w32 ? 1 : 0;
     p.d_log_s = (double)d * std::log(s);
     p.max_iter = max_iter;
     p.checkpoint = checkpoint;
@@ -1233,7 +1236,7 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     } else {
       s->XT.release();
     }
-    if (s->loss == MIDAGMA_LOSS_L2 && D % 128 == 0)
+    if (s->loss == MIDAGMA_LOSS_L2 && (D % 128 == 0 || s->w32))  // (float32 W: I - W from build_at)
       s->IW.alloc((size_t)D * D);
     else
       s->IW.release();
@@ -1586,6 +1589,21 @@ int midagma_end(midagma_solver* s, double* W, midagma_result* res) {
     return MIDAGMA_OK;
   });
   return singular_or_nonfinite(s, rc, res, W);
+}
+
+int midagma_set_w_float32(midagma_solver* s, int float32) {
+  if (!s) return fail(s, MIDAGMA_E_ARG, "null solver");
+  return guarded(s, [&] {
+    const bool on = float32 != 0;
+    if (on && (s->mode == MIDAGMA_MODE_COV || s->loss == MIDAGMA_LOSS_L2) && !s->IW.p) {
+      // the score GEMM's I - W (float32 diagonal) comes from build_at, not the GEMM's staging
+      s->IW.alloc((size_t)s->D * s->D);
+      HIP_TRY(hipMemsetAsync(s->IW.p, 0, (size_t)s->D * s->D * sizeof(double), s->stream));
+      s->graphs_valid = false;
+    }
+    s->w32 = on;
+    return MIDAGMA_OK;
+  });
 }
 
 // Test hook (not in the public header): choose the logistic sigmoid GEMM's form for the next

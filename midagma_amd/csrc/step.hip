@@ -40,10 +40,12 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 __global__ __launch_bounds__(NTHREADS) void reduce_check_kernel(const double* __restrict__ Mt,
                                                                 const double* __restrict__ W,
                                                                 const double* __restrict__ Z,
+                                                                const Params* __restrict__ pr,
                                                                 State* __restrict__ st,
                                                                 double* __restrict__ partials, int64_t d,
                                                                 int64_t D) {
   if (st->status != ST_RUNNING) return;
+  const bool w32 = pr->w32 != 0;
   __shared__ double red[NTHREADS];
   __shared__ int flag_sh;
   if (threadIdx.x == 0) flag_sh = 0;
@@ -54,11 +56,11 @@ __global__ __launch_bounds__(NTHREADS) void reduce_check_kernel(const double* __
     for (int64_t j = threadIdx.x; j < d; j += NTHREADS) {
       const int64_t idx = i * D + j;
       const double m = Mt[idx];
-      if (m + 1e-16 < 0.0) flag |= 1;
+      if (m_entry(m, w32) < 0.0) flag |= 1;
       if (!isfinite(m)) flag |= 2;
       if (ck) {
         const double w = W[idx];
-        sd += (((i == j) ? 1.0 : 0.0) - w) * Z[idx];
+        sd += one_minus(i == j, w, w32) * Z[idx];
         l1 += fabs(w);
       }
     }
@@ -226,12 +228,13 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
   if (j < d) {
     const int64_t idx = i * D + j;
     const double w = W[idx];
-    const double mt = Mt[idx] + 1e-16;
+    const bool w32 = pr->w32 != 0;
+    const double mt = m_entry(Mt[idx], w32);
     double gs = pr->zscale * z_at(Z, zsplit, zstride, idx);
     if (pr->logistic) gs = gs + pr->cscale * cov[idx];
     const double sg = sign_of(w);
     const double gl1 = pr->mu_l1 * sg;
-    const double gh = (2.0 * w) * mt;
+    const double gh = h_term(w, mt, w32);
     double gobj = gs + gl1;
     gobj = gobj + gh;
     double ginc = 0.0;
@@ -250,6 +253,7 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
     const double vh = vv / st->bc2;
     const double gd = mh / (sqrt(vh) + 1e-8);
     double wn = w - st->lr_a * gd;
+    if (w32) wn = f32r(wn);  // W -= lr * grad into a float32 W (linear.py:275)
     if (pr->has_exc) wn = wn * mexc[idx];
     m[idx] = mm;
     v[idx] = vv;
@@ -302,12 +306,13 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
   const int64_t idx = i * D + j;
   if (act == ACT_STEP) {
     const double w = W[idx];
-    const double mt = Mt[idx] + 1e-16;
+    const bool w32 = pr->w32 != 0;
+    const double mt = m_entry(Mt[idx], w32);
     double gs = pr->zscale * z_at(Z, zsplit, zstride, idx);
     if (pr->logistic) gs = gs + pr->cscale * cov[idx];
     const double sg = sign_of(w);
     double gobj = gs + pr->mu_l1 * sg;
-    gobj = gobj + (2.0 * w) * mt;
+    gobj = gobj + h_term(w, mt, w32);
     if (pr->has_inc) gobj = gobj + minc[idx] * sg;
     if (trek) gobj = gobj + trek[idx];
     const double mm = m[idx] * pr->beta1 + pr->c1 * gobj;
@@ -316,6 +321,7 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     const double vh = vv / st->bc2;
     const double gd = mh / (sqrt(vh) + 1e-8);
     double wn = w - st->lr_a * gd;
+    if (w32) wn = f32r(wn);  // W -= lr * grad into a float32 W (linear.py:275)
     if (pr->has_exc) wn = wn * mexc[idx];
     m[idx] = mm;
     v[idx] = vv;
@@ -324,11 +330,16 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     // the last STEP's Adam direction, recomputed from its m, v and bias terms (unchanged
     // since: bit-identical to the value that step applied, so no d x d store per step)
     const double gd = (m[idx] / st->bc1) / (sqrt(v[idx] / st->bc2) + 1e-8);
+    // (float32 W: each in-place update rounds, linear.py:235, 239)
+    const bool w32 = pr->w32 != 0;
     if (act == ACT_HALVE) {
       double wn = W[idx] + st->lr_a * gd;
-      W[idx] = wn - st->lr_b * gd;
+      if (w32) wn = f32r(wn);
+      wn = wn - st->lr_b * gd;
+      W[idx] = w32 ? f32r(wn) : wn;
     } else {  // ACT_REVERT
-      W[idx] = W[idx] + st->lr_a * gd;
+      const double wn = W[idx] + st->lr_a * gd;
+      W[idx] = w32 ? f32r(wn) : wn;
     }
   }
 }
@@ -382,9 +393,9 @@ void launch_any_nonfinite(const double* x, int64_t n, int* flag, hipStream_t str
   HIP_TRY(hipGetLastError());
 }
 
-void launch_reduce_check(const double* Mt, const double* W, const double* Z, const Params*, State* st,
+void launch_reduce_check(const double* Mt, const double* W, const double* Z, const Params* pr, State* st,
                          double* partials, int64_t d, int64_t D, hipStream_t stream) {
-  hipLaunchKernelGGL(reduce_check_kernel, dim3(NRED), dim3(NTHREADS), 0, stream, Mt, W, Z, st, partials, d, D);
+  hipLaunchKernelGGL(reduce_check_kernel, dim3(NRED), dim3(NTHREADS), 0, stream, Mt, W, Z, pr, st, partials, d, D);
   HIP_TRY(hipGetLastError());
 }
 

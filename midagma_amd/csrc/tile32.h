@@ -122,11 +122,13 @@ __device__ __forceinline__ void mma32x2(const double* __restrict__ A1, const dou
 // A^T tile builder: At[J][I] = (I == J ? s : 0) - f(X[I][J]) on the logical d x d block (f =
 // square for W, identity for a given A), identity padding; source tile (rows bi, cols bj) through
 // the LDS tile; IW (nullable) = I - X untransposed (the data-mode score GEMM's B operand).
+// w32: W is float32 (common.h sw_entry / one_minus).
 // build_at_kernel (gj.hip) and the fast slot's build_resid0_kernel (blockinv.hip).
 template <bool SQUARE, int BT = 32>
 __device__ __forceinline__ void build_at_tile(int bi, int bj, const double* __restrict__ X, int64_t ldx,
                                               double* __restrict__ At, int64_t D, int64_t d, double s,
-                                              double* __restrict__ IW, double (&tile)[BT][BT + 1]) {
+                                              double* __restrict__ IW, double (&tile)[BT][BT + 1],
+                                              bool w32 = false) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int it = 0; it < BT * BT / NTHREADS; ++it) {
@@ -136,12 +138,11 @@ __device__ __forceinline__ void build_at_tile(int bi, int bj, const double* __re
     double v;
     const double x = (I < d && J < d) ? X[I * ldx + J] : 0.0;
     if (I < d && J < d) {
-      const double f = SQUARE ? x * x : x;
-      v = (I == J ? s : 0.0) - f;
+      v = SQUARE ? sw_entry(I == J, s, x, w32) : (I == J ? s : 0.0) - x;
     } else {
       v = (I == J) ? 1.0 : 0.0;
     }
-    if (IW) IW[I * D + J] = (I == J ? 1.0 : 0.0) - x;
+    if (IW) IW[I * D + J] = one_minus(I == J, x, w32);
     tile[c][r] = v;
   }
   __syncthreads();

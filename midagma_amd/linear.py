@@ -78,10 +78,11 @@ class DagmaLinear:
         assert loss_type in losses, f"loss_type should be one of {losses}"
         # dtype (linear.py:29, 55): the type of Id, the exclusion mask and W_est (408, 220, 429).  The
         # reference keeps W in that type through its in-place Adam updates while cov, the
-        # gradients and the inverse's products come out float64; here the loop computes in
-        # float64 and W is handed back in dtype after every minimize call, so a float32 fit
-        # agrees with the reference's float32 fit to within the reference's own float32 /
-        # float64 spread (tests/test_gpu_parity.py::test_full_fit_float32_dtype)
+        # gradients and Adam come out float64.  With a float32 W the device loop emulates numpy's
+        # float32 operations (W rounded after every update, s*Id - W*W, Id - W, M + 1e-16 and
+        # 2 W o M^T in float32; csrc/common.h) around a float64 inverse rounded to float32, so a
+        # float32 fit stays within the reference's own float32 perturbation envelope
+        # (tests/test_gpu_parity.py::test_full_fit_float32_dtype, fit_f32_d20_envelope.npz)
         dtype = np.dtype(dtype).type
         if dtype not in (np.float32, np.float64):
             raise ValueError("dtype must be np.float64 or np.float32 (the solver computes in float64)")
@@ -293,6 +294,10 @@ class DagmaLinear:
         W = np.ascontiguousarray(W, dtype=np.float64)
         mask_inc, mask_exc = self._masks(mu)
         self._solver.set_masks(mask_inc, mask_exc)
+        # a float32 W (dtype=np.float32, linear.py:429) is updated in float32 arithmetic, as numpy
+        # updates the reference's float32 W in place (275); the inverse stays float64
+        if hasattr(self._solver, "set_w_float32"):
+            self._solver.set_w_float32(w_type is np.float32)
         logging_on = bool(self._log_cfg.enabled)
         if self.score_mode == "data" and self._allreduce is not None:
             res = run_allreduce_minimize(self._solver, W, mu, max_iter, s, lr, tol, beta_1, beta_2,

@@ -148,6 +148,11 @@ class HipSolver:
         cov = _as_f64(cov)
         check(self.L.midagma_set_cov(self.h, dptr(cov), cov.shape[1]), self.h, "set_cov")
 
+    def set_w_float32(self, on: bool):
+        """W's dtype in the reference's arithmetic for the next minimize (ABI 8): True emulates
+        numpy's float32 operations on a float32 W (linear.py:29, 226, 244, 248, 275)."""
+        check(self.L.midagma_set_w_float32(self.h, 1 if on else 0), self.h, "set_w_float32")
+
     def set_masks(self, mask_inc: np.ndarray | None, mask_exc: np.ndarray | None):
         mi = None if mask_inc is None else _as_f64(mask_inc)
         me = None if mask_exc is None else _as_f64(mask_exc)

@@ -278,6 +278,43 @@ def gen_fit_f32(X):
     np.savez_compressed(os.path.join(HERE, "fit_f32_d20.npz"), **out)
 
 
+class NoisyInv32(NoisyInv):
+    """float32 stand-in: the float32 inverse with one-ulp-scale relative noise (2^-24 N(0, 1)) in
+    every entry -- the size of the difference between two valid float32 inversions."""
+
+    def inv(self, A):
+        M = self._sla.inv(A)
+        if M.dtype != np.float32:
+            return M * (1.0 + 1e-16 * self._rng.standard_normal(M.shape))
+        return (M * (1.0 + 2.0 ** -24 * self._rng.standard_normal(M.shape))).astype(np.float32)
+
+
+def gen_fit_f32_envelope(X, seeds=(7, 11, 13, 17, 19, 23, 29, 31)):
+    """The dtype=np.float32 fit of gen_fit_f32 under float32-scale noise in every inverse
+    (NoisyInv32), one run per seed: the reference's own float32 perturbation envelope, the bar of
+    tests/test_gpu_parity.py::test_full_fit_float32_dtype (the GPU's float32 loop inverts in
+    float64 and rounds, a different valid float32 inversion)."""
+    rows = {"W": [], "h_final": [], "score_final": []}
+
+    def one_fit():
+        m = DagmaLinear(loss_type="l2", verbose=False, dtype=np.float32)
+        W = m.fit(X.copy(), lambda1=0.03, T=3, s=[1.0, .9, .8], warm_iter=4000, max_iter=5000)
+        return m, W
+
+    orig = ref_linear.sla
+    for sd in seeds:
+        ref_linear.sla = NoisyInv32(np.random.default_rng(sd))
+        try:
+            m, W = one_fit()
+        finally:
+            ref_linear.sla = orig
+        rows["W"].append(W.astype(np.float64))
+        rows["h_final"].append(float(m.h_final))
+        rows["score_final"].append(float(m.score_final))
+    np.savez_compressed(os.path.join(HERE, "fit_f32_d20_envelope.npz"), seeds=np.array(seeds),
+                        **{k: np.array(v, dtype=np.float64) for k, v in rows.items()})
+
+
 def gen_trek():
     """PST trek regularizer value and gradient from the reference (notreks.trek_value_grad)
     for every seq and agg it offers, on a small in-domain W."""
@@ -414,6 +451,7 @@ def main():
         gen_fit(X20)
         gen_fit_envelope(X20)
         gen_fit_f32(X20)
+        gen_fit_f32_envelope(X20)
         gen_trek()
         gen_tcc(X20)
         gen_mlp()
@@ -427,6 +465,6 @@ if __name__ == "__main__":
             X20 = np.load(os.path.join(HERE, "data_d20_n1000_seed0.npz"))["X"]
             for name in sys.argv[1:]:
                 fn = globals()[name]
-                fn(X20) if name in ("gen_tcc", "gen_mlp_traj", "gen_fit_f32") else fn()  # e.g. gen_traj_logistic_d100
+                fn(X20) if name in ("gen_tcc", "gen_mlp_traj", "gen_fit_f32", "gen_fit_f32_envelope") else fn()  # e.g. gen_traj_logistic_d100
     else:
         main()

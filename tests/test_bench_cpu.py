@@ -49,8 +49,9 @@ def test_gpus_n_relaunches_as_torchrun_child(bench, monkeypatch):
     class Done:
         returncode = 3
 
-    def fake_run(cmd):
+    def fake_run(cmd, **kw):
         seen["cmd"] = cmd
+        seen["timeout"] = kw.get("timeout")
         return Done()
 
     monkeypatch.setattr(subprocess, "run", fake_run)
@@ -64,6 +65,7 @@ def test_gpus_n_relaunches_as_torchrun_child(bench, monkeypatch):
     assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
     assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    assert seen["timeout"] and seen["timeout"] > 0  # the wait is bounded
 
 
 def test_oracle_check_child_matches_in_process_oracle(bench):
@@ -94,3 +96,56 @@ def test_comm_summary_keys(bench):
         assert k in c, k
     assert abs(c["compute_ms"] - 7.3) < 1e-12 and c["world_size"] == 8
     assert abs(c["algbw_GBps"] - 80.0) < 1e-9 and abs(c["busbw_GBps"] - 140.0) < 1e-9
+
+
+_FAKE_WORKER = r'''
+import json, os, sys, time
+import numpy as np
+rank, path = int(os.environ["RANK"]), os.environ["MIDAGMA_BENCH_COMM"]
+open(os.environ["MIDAGMA_BENCH_HEARTBEAT"], "a").write("1 started\n")
+if path == "library":
+    if rank == 1:
+        sys.exit(3)              # this rank's worker fails at once
+    time.sleep(600)              # rank 0's worker "hangs" in a collective: must be killed
+d = 20
+if rank == 0:
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(500, d))
+    np.save(os.environ["MIDAGMA_BENCH_COV_OUT"], X.T @ X / 500)
+    print(json.dumps({"metric": "m", "value": 2.0, "unit": "steps/s", "n_gpus": 2,
+                      "comm": {"path": "host-driven"}}), flush=True)
+'''
+
+
+def test_supervised_ranks_fall_back_to_host_path(tmp_path):
+    """Under torch.distributed.run every rank supervises a GPU worker child (bench.py
+    supervise_ranks).  Here a stand-in worker fails on rank 1 and hangs on rank 0 on the
+    in-library RCCL path: both are ended, fresh workers run the host-driven path, and rank 0
+    prints one line naming the path taken and the failed attempt, with the CPU baseline timed
+    after the workers (gloo on the CPU, world size 2)."""
+    w = tmp_path / "fake_worker.py"
+    w.write_text(_FAKE_WORKER)
+    env = dict(os.environ, MIDAGMA_BENCH_WORKER_CMD=json.dumps([sys.executable, str(w)]),
+               MIDAGMA_BENCH_STALL_S="60", PYTHONPATH=REPO)
+    env.pop("MIDAGMA_BENCH_COMM", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29581", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--dim", "20", "--rows", "500"]
+    t0 = __import__("time").time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert __import__("time").time() - t0 < 300  # the hung worker was killed, not waited for
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["value"] == 2.0
+    la = line["launch"]
+    assert la["comm_path"] == "host" and line["comm"]["path_taken"] == "host"
+    assert [a["comm_path"] for a in la["attempts"]] == ["library", "host"]
+    first = la["attempts"][0]
+    assert first["failed_ranks"] >= 1
+    assert any(x["rank"] == 1 and "exited 3" in x["outcome"] for x in first["ranks"])
+    assert la["attempts"][1]["failed_ranks"] == 0
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and "sample" in cb
+    assert line["vs_cpu"] > 0 and line["vs_cpu_reference_algorithm"] > 0

@@ -181,22 +181,52 @@ def test_full_fit_d20(hip, golden, parity):
 
 
 def test_full_fit_float32_dtype(hip, golden):
-    """dtype=np.float32 (linear.py:29): the reference keeps W in float32 through its in-place Adam
-    updates, so its float32 and float64 fits differ by float32 rounding (fit_f32_d20.npz: T = 3,
-    max |dW| 1.6e-4, identical support).  The GPU loop computes in float64 and returns W in
-    float32: the support must be the reference's and W within twice the reference's own
-    float32 / float64 spread of its float32 fit (tests/test_dtype_cpu.py: the same Python path over
-    the CPU oracle, 1.3e-4 from the float64 fit: the stage-boundary float32 roundings grow like the
-    reference's own)."""
+    """dtype=np.float32 (linear.py:29): the reference keeps W (and Id) in float32, so numpy rounds
+    every operation on them to float32 (fit_f32_d20.npz: T = 3, max |dW| 1.6e-4 from its float64
+    fit, identical support).  The GPU loop emulates those float32 operations around a float64
+    inverse rounded to float32 (csrc/common.h).  Bar: the reference's own float32 perturbation
+    envelope -- the largest deviation of its float32 fit under 1-ulp noise in every float32
+    inverse over 8 seeds (fit_f32_d20_envelope.npz, 1.9e-4) -- and the identical support."""
     from midagma_amd import DagmaLinear
     f = golden("fit_f32_d20.npz")
+    env = golden("fit_f32_d20_envelope.npz")
     X = golden("data_d20_n1000_seed0.npz")["X"].copy()
     m = DagmaLinear("l2", dtype=np.float32)
     W = m.fit(X, lambda1=0.03, T=3, s=[1.0, .9, .8], warm_iter=4000, max_iter=5000)
     assert W.dtype == np.float32
-    spread = float(np.abs(f["W_f32"] - f["W_f64"]).max())
+    env_w = float(np.abs(env["W"] - f["W_f32"]).max())
     assert np.array_equal(W != 0, f["W_f32"] != 0)
-    assert np.abs(W - f["W_f32"]).max() <= 2 * spread
+    assert np.abs(W - f["W_f32"]).max() <= env_w
+
+
+@pytest.mark.parametrize("d,K,n", [(20, 1000, 1000), (100, 300, 2000), (300, 100, 1000), (1000, 40, 2000)])
+def test_float32_trajectory_matches_reference_float32(hip, d, K, n):
+    """dtype=np.float32 per step: K Adam steps of stage 1 from a float32 W = 0 against the
+    reference's float32 arithmetic (the oracle with dtype=float32, bit-exact to the reference's
+    float32 fit: test_oracle_golden.py::test_float32_fit_bit_exact).  On the CPU the float64
+    inverse rounded to float32 (the GPU's model) stays within 1e-8 of the reference's float32
+    getri over these horizons, while float64 W moves 3e-5 to 1.9e-4 away; bound 1e-7, and at most
+    a tenth of that float32 / float64 spread.  d = 20: the persistent workgroup; 100: one 128
+    outer block; 300, 1000: the blocked two-level inverse (fast and pivoted slots)."""
+    X, _, _ = make_dataset(d, n, seed=d)
+    ref = {}
+    for dt in (np.float32, np.float64):
+        o = LinearOracle("l2", dtype=dt)
+        o.prepare(X.copy(), 0.03, 1000)
+        Wr, tr = o.minimize(np.zeros((d, d), dtype=dt), 1.0, K, 1.0, 3e-4, tol=-1.0)
+        assert tr.iters == K
+        ref[dt] = Wr.astype(np.float64)
+    Xc = X - X.mean(axis=0, keepdims=True)
+    sol = _solver(d, Xc.T @ Xc / n)
+    sol.set_w_float32(True)
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
+    sol.close()
+    assert res.iters == K
+    assert np.array_equal(W, W.astype(np.float32).astype(np.float64))  # float32 values throughout
+    dev = float(np.abs(W - ref[np.float32]).max())
+    spread = float(np.abs(ref[np.float64] - ref[np.float32]).max())
+    assert dev <= min(1e-7, 0.1 * spread), (dev, spread)
 
 
 def test_full_fit_d1000_matches_reference_algorithm(hip, golden, parity):

@@ -145,3 +145,21 @@ def test_fit_d1000_envelope_fixture():
         assert np.all(e[f"s{s}_stages"][:, 2] == 1)  # every stage succeeded
         assert abs(float(e[f"s{s}_h_final"]) - float(f["h_final"])) < 1e-8
         assert abs(float(e[f"s{s}_score_final"]) / float(f["score_final"]) - 1) < 1e-5
+
+
+def test_float32_fit_bit_exact(golden):
+    """dtype=np.float32 (linear.py:29, 408, 429): the oracle's float32 fit (Id, W and mask_exc in
+    float32, so numpy rounds s*Id - W*W, the float32 inverse, M + 1e-16, 2 W o M^T and every
+    in-place update of W to float32) reproduces the reference's own float32 fit bit for bit
+    (fit_f32_d20.npz), and its float32 perturbation envelope (fit_f32_d20_envelope.npz: 1-ulp
+    noise in every float32 inverse) keeps that fit's support."""
+    f = golden("fit_f32_d20.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    o = LinearOracle("l2", dtype=np.float32)
+    W = o.fit(X, lambda1=0.03, T=3, s=[1.0, .9, .8], warm_iter=4000, max_iter=5000)
+    assert W.dtype == np.float32
+    assert np.array_equal(W, f["W_f32"])
+    assert float(o.h_final) == float(f["h_final_f32"]) and float(o.score_final) == float(f["score_final_f32"])
+    env = golden("fit_f32_d20_envelope.npz")
+    for Wn in env["W"]:
+        assert np.array_equal(Wn != 0, f["W_f32"] != 0)
