@@ -195,8 +195,10 @@ def supervise_ranks(args):
     stall = float(os.environ.get("MIDAGMA_BENCH_STALL_S", "300"))
     cap = float(os.environ.get("MIDAGMA_BENCH_ATTEMPT_S", "1800"))
     first = os.environ.get("MIDAGMA_BENCH_COMM", "library")
-    paths = [first] if (first == "host" or os.environ.get("MIDAGMA_BENCH_BACKEND", "nccl") != "nccl") \
-        else ["library", "host"]
+    if os.environ.get("MIDAGMA_BENCH_BACKEND", "nccl") != "nccl":
+        paths = ["host"]  # (gloo: the workers take the host-driven all-reduce, bench_data)
+    else:
+        paths = ["host"] if first == "host" else ["library", "host"]
     fake = os.environ.get("MIDAGMA_BENCH_WORKER_CMD")  # tests: a stand-in worker (JSON argv)
     cmd = json.loads(fake) if fake else [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     import tempfile

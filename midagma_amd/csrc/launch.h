@@ -224,7 +224,7 @@ struct SmallTcc {
 void launch_small_minimize(const Params* pr, State* st, double* W, double* m, double* v, const double* covs,
                            const double* minc, const double* mexc, const double* bc_table, CkptRec* ckpt,
                            int64_t ckpt_cap, double* carry, double* pstore, int64_t d, int64_t n_slots,
-                           hipStream_t stream, const SmallTcc* tcc = nullptr);
+                           hipStream_t stream, const SmallTcc* tcc = nullptr, bool w32 = false);
 
 // --- trek.hip ---------------------------------------------------------------
 enum TrekSeq : int { TREK_EXP = 0, TREK_INV = 1, TREK_LOG = 2, TREK_BINOM = 3 };

@@ -196,7 +196,7 @@ __device__ __noinline__ void small_control(const Params* __restrict__ pr, State&
     ctl.bc2 = S.bc2;
 }
 
-template <int DS, int NW, int TCC>
+template <int DS, int NW, int TCC, bool W32 = false>
 __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     const Params* __restrict__ pr, State* __restrict__ stg, double* __restrict__ Wg, double* __restrict__ mg,
     double* __restrict__ vg, const double* __restrict__ covs, const double* __restrict__ minc,
@@ -298,7 +298,8 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   }
   __syncthreads();
   if (!ctl.run) return;
-  const bool w32 = pr->w32 != 0;  // dtype=np.float32 (common.h f32r)
+  constexpr bool w32 = W32;  // dtype=np.float32 (common.h f32r; a template argument: the float64
+                             // loop carries none of its selects, 5.5 -> 5.8 us a step at d = 20)
 #pragma unroll
   for (int e = 0; e < E; ++e)
     if (real[e]) {
@@ -690,32 +691,39 @@ int small_block(int64_t d) {
 void launch_small_minimize(const Params* pr, State* st, double* W, double* m, double* v, const double* covs,
                            const double* minc, const double* mexc, const double* bc_table, CkptRec* ckpt,
                            int64_t ckpt_cap, double* carry, double* pstore, int64_t d, int64_t n_slots,
-                           hipStream_t stream, const SmallTcc* tcc) {
+                           hipStream_t stream, const SmallTcc* tcc, bool w32) {
   const int ds = small_block(d);
   if (ds == 0) throw std::invalid_argument("small_minimize: d > 64");
   if (tcc && ds > 32) throw std::invalid_argument("small_minimize: the TCC regularizer needs d <= 32");
+  if (tcc && w32) throw std::invalid_argument("small_minimize: float32 W with TCC runs on the graph path");
   // d <= 20 on DS = 32: the one-wave 5 x 5 body (d=20: 10.4k -> 11.7k steps/s; experiment knob
   // MIDAGMA_EXP_TCC_BS5=0: NB = 16, 4 x 4)
   const bool bs5 = tcc && ds == 32 && d <= 20 && knob("MIDAGMA_EXP_TCC_BS5", 1) != 0;
   const SmallTcc tc = tcc ? *tcc : SmallTcc{};
-#define MIDAGMA_SMALL(DS_, NW_, TCC_)                                                                           \
-  hipLaunchKernelGGL((small_minimize_kernel<DS_, NW_, TCC_>), dim3(1), dim3(64 * NW_), 0, stream, pr, st, W, m, v, \
-                     covs, minc, mexc, bc_table, ckpt, ckpt_cap, carry, pstore, n_slots, tc)
+#define MIDAGMA_SMALL(DS_, NW_, TCC_, W32_)                                                                \
+  hipLaunchKernelGGL((small_minimize_kernel<DS_, NW_, TCC_, W32_>), dim3(1), dim3(64 * NW_), 0, stream, pr, st, W, \
+                     m, v, covs, minc, mexc, bc_table, ckpt, ckpt_cap, carry, pstore, n_slots, tc)
   // one wave per 16 x 16 tile
   if (ds == 16) {
     if (tcc)
-      MIDAGMA_SMALL(16, 1, 4);
+      MIDAGMA_SMALL(16, 1, 4, false);
+    else if (w32)
+      MIDAGMA_SMALL(16, 1, 0, true);
     else
-      MIDAGMA_SMALL(16, 1, 0);
+      MIDAGMA_SMALL(16, 1, 0, false);
   } else if (ds == 32) {
     if (bs5)
-      MIDAGMA_SMALL(32, 4, 5);
+      MIDAGMA_SMALL(32, 4, 5, false);
     else if (tcc)
-      MIDAGMA_SMALL(32, 4, 4);
+      MIDAGMA_SMALL(32, 4, 4, false);
+    else if (w32)
+      MIDAGMA_SMALL(32, 4, 0, true);
     else
-      MIDAGMA_SMALL(32, 4, 0);
+      MIDAGMA_SMALL(32, 4, 0, false);
+  } else if (w32) {
+    MIDAGMA_SMALL(64, 16, 0, true);
   } else {
-    MIDAGMA_SMALL(64, 16, 0);
+    MIDAGMA_SMALL(64, 16, 0, false);
   }
 #undef MIDAGMA_SMALL
   HIP_TRY(hipGetLastError());

@@ -77,7 +77,7 @@ struct midagma_solver {
   // (the TCC regularizer runs inside it up to d = 32, tcc_blk.h; PST keeps the graph-replayed slots)
   bool small_on() const {
     return use_small && mode == MIDAGMA_MODE_COV && loss == MIDAGMA_LOSS_L2 && small_block(d) > 0 &&
-           (!trek_on || (trek_tcc && small_block(d) <= 32 && small_tcc));
+           (!trek_on || (trek_tcc && small_block(d) <= 32 && small_tcc && !w32));
   }
   // PST trek regularizer (trek.hip)
   TrekCfg tcfg{};
@@ -952,7 +952,7 @@ struct midagma_solver {
         tc = SmallTcc{cw.S, ccfg.w, ccfg.eps, (double)ccfg.m, ccfg.weight, ccfg.mode, cw.scal, cw.vprev, cw.uprev};
       launch_small_minimize(d_params, d_state, W.p, m.p, v.p, covs.p, has_inc ? minc.p : nullptr,
                             has_exc ? mexc.p : nullptr, bc_table.p, d_ckpt, ckpt_cap, scarry.p, sprev.p, d, B,
-                            stream, trek_on && trek_tcc ? &tc : nullptr);
+                            stream, trek_on && trek_tcc ? &tc : nullptr, w32);
       launched += B;
       HIP_TRY(hipMemcpyAsync(&h_state[1], d_state, sizeof(State), hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
