@@ -422,6 +422,17 @@ void launch_trail128_band(const double* Ain, double* Aout, int64_t D, int64_t B2
 // The same update with the accumulators preloaded from C0 (experiments build, tools/micro/trail_micro.hip)
 void launch_trail128_pre(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
                          const State* st, hipStream_t stream);
+// The B2 = 256 update (EPI_SUB_MID tiles) on `nwg` persistent workgroups: static round robin over
+// the tiles (ctr == nullptr), or tiles claimed from the counter *ctr (zero before the launch)
+void launch_trail128_persist(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, const State* st,
+                             int nwg, int* ctr, hipStream_t stream);
+// The B2 = 256 update as data-parallel tiles plus a stream-K remainder: the first `dp` tiles (of
+// xcd_remap's order) one per workgroup (EPI_SUB_MID), the other ntiles - dp tiles' 16 K-tiles each
+// split evenly over `nsk` workgroups; a partial tile goes to ws (2 nsk 128 x 128 slots), the
+// workgroup holding a tile's last K-tile sums its partials in K order (flags: nsk words, zero before
+// the first launch; each launch leaves them zero) and writes C = C0 - sum
+void launch_trail128_sk(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, const State* st, int dp,
+                        int nsk, double* ws, int* flags, hipStream_t stream);
 #endif
 // The same update in two launches: part 0 the tiles in block g + 1's row and column bands, part 1
 // the rest (no domain check: the look-ahead runs on steps before the last).

@@ -347,54 +347,57 @@ class DagmaLinear:
             raise ValueError("gram must be 'auto', 'host' or 'device'")
         t_start = time.perf_counter()
         sharded = n_global is not None
-        self._sharded = sharded
-        world, rank = self._world()
-        on_dev = is_device_tensor(X)
-        self.X, self.lambda1, self.checkpoint = X, lambda1, checkpoint
-        self.n, self.d = (int(n_global), int(X.shape[1])) if sharded else (int(X.shape[0]), int(X.shape[1]))
-        self.Id = np.eye(self.d).astype(self.dtype)
-        if on_dev and gram == "host":
-            raise ValueError("gram='host' needs a host X")
-        gram_device = self.score_mode == "cov" and (
-            gram == "device" or (gram == "auto" and (on_dev or sharded or
-                                                     float(X.shape[0]) * self.d * self.d >= 1e11)))
-        if sharded and self.score_mode == "cov" and not gram_device:
-            raise ValueError("fit(X_shard, n_global=...) in cov mode forms cov on the device (gram='device')")
-        solver = self._solver_factory(self.d, self.loss_type, self.score_mode, device=self.device)
-        if self.loss_type == 'l2':
-            if on_dev:  # the centring on the device: column sums (all-reduced over shards), X -= mean
-                colsum = self._allreduce_tensor(solver.colsum(X)) if sharded else solver.colsum(X)
-                solver.center(X, colsum, float(self.n))
-            elif sharded:  # the global column mean from the ranks' column sums
-                colsum = X.sum(axis=0)
-                if world > 1:
-                    colsum = self._allreduce_host(colsum)
-                self.X -= (colsum / float(self.n))[None, :]
-            else:
-                self.X -= X.mean(axis=0, keepdims=True)
-        self.exc_r, self.exc_c = None, None
-        self.inc_r, self.inc_c = None, None
-        if exclude_edges is not None:
-            if type(exclude_edges) is tuple and type(exclude_edges[0]) is tuple and \
-                    np.all(np.array([len(e) for e in exclude_edges]) == 2):
-                self.exc_r, self.exc_c = zip(*exclude_edges)
-            else:
-                ValueError("blacklist should be a tuple of edges, e.g., ((1,2), (2,3))")
-        if include_edges is not None:
-            if type(include_edges) is tuple and type(include_edges[0]) is tuple and \
-                    np.all(np.array([len(e) for e in include_edges]) == 2):
-                self.inc_r, self.inc_c = zip(*include_edges)
-            else:
-                ValueError("whitelist should be a tuple of edges, e.g., ((1,2), (2,3))")
-        # data mode over several ranks (or a shard, or a device X): cov from the device Gram
-        # matrices, no rank multiplies another rank's rows; one host X keeps the reference's product
-        cov_on_device = self.score_mode == "data" and (sharded or world > 1 or on_dev)
-        X_local = X if sharded else None
-        if not cov_on_device and not gram_device:
-            self.cov = X.T @ X / float(self.n)
-        self.W_est = np.zeros((self.d, self.d)).astype(self.dtype)
-        self._setup_solver(solver, X_local=X_local, cov_on_device=cov_on_device, gram_device=gram_device)
-        self._sharded = False  # the loop itself: replicated in cov mode, no collective
+        # (preparation under try/finally: _world() must not keep seeing a shard after a failure)
+        try:
+            self._sharded = sharded
+            world, rank = self._world()
+            on_dev = is_device_tensor(X)
+            self.X, self.lambda1, self.checkpoint = X, lambda1, checkpoint
+            self.n, self.d = (int(n_global), int(X.shape[1])) if sharded else (int(X.shape[0]), int(X.shape[1]))
+            self.Id = np.eye(self.d).astype(self.dtype)
+            if on_dev and gram == "host":
+                raise ValueError("gram='host' needs a host X")
+            gram_device = self.score_mode == "cov" and (
+                gram == "device" or (gram == "auto" and (on_dev or sharded or
+                                                         float(X.shape[0]) * self.d * self.d >= 1e11)))
+            if sharded and self.score_mode == "cov" and not gram_device:
+                raise ValueError("fit(X_shard, n_global=...) in cov mode forms cov on the device (gram='device')")
+            solver = self._solver_factory(self.d, self.loss_type, self.score_mode, device=self.device)
+            if self.loss_type == 'l2':
+                if on_dev:  # the centring on the device: column sums (all-reduced over shards), X -= mean
+                    colsum = self._allreduce_tensor(solver.colsum(X)) if sharded else solver.colsum(X)
+                    solver.center(X, colsum, float(self.n))
+                elif sharded:  # the global column mean from the ranks' column sums
+                    colsum = X.sum(axis=0)
+                    if world > 1:
+                        colsum = self._allreduce_host(colsum)
+                    self.X -= (colsum / float(self.n))[None, :]
+                else:
+                    self.X -= X.mean(axis=0, keepdims=True)
+            self.exc_r, self.exc_c = None, None
+            self.inc_r, self.inc_c = None, None
+            if exclude_edges is not None:
+                if type(exclude_edges) is tuple and type(exclude_edges[0]) is tuple and \
+                        np.all(np.array([len(e) for e in exclude_edges]) == 2):
+                    self.exc_r, self.exc_c = zip(*exclude_edges)
+                else:
+                    ValueError("blacklist should be a tuple of edges, e.g., ((1,2), (2,3))")
+            if include_edges is not None:
+                if type(include_edges) is tuple and type(include_edges[0]) is tuple and \
+                        np.all(np.array([len(e) for e in include_edges]) == 2):
+                    self.inc_r, self.inc_c = zip(*include_edges)
+                else:
+                    ValueError("whitelist should be a tuple of edges, e.g., ((1,2), (2,3))")
+            # data mode over several ranks (or a shard, or a device X): cov from the device Gram
+            # matrices, no rank multiplies another rank's rows; one host X keeps the reference's product
+            cov_on_device = self.score_mode == "data" and (sharded or world > 1 or on_dev)
+            X_local = X if sharded else None
+            if not cov_on_device and not gram_device:
+                self.cov = X.T @ X / float(self.n)
+            self.W_est = np.zeros((self.d, self.d)).astype(self.dtype)
+            self._setup_solver(solver, X_local=X_local, cov_on_device=cov_on_device, gram_device=gram_device)
+        finally:
+            self._sharded = False  # the loop itself: replicated in cov mode, no collective
         t_prep = time.perf_counter()
         mu = mu_init
         if type(s) == list:

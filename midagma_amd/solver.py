@@ -84,17 +84,20 @@ def colsum_dev(X):
     import torch
     n, d, ld = _rows(X)
     out = torch.empty(d, dtype=torch.float64, device=X.device)
-    check(_lib.lib().midagma_colsum_dev(C.c_void_p(X.data_ptr()), n, d, ld, C.c_void_p(out.data_ptr()),
-                                        _cur_stream(X.device)), None, "colsum_dev")
+    with torch.cuda.device(X.device):  # (the library's scratch on X's device, not the current one)
+        check(_lib.lib().midagma_colsum_dev(C.c_void_p(X.data_ptr()), n, d, ld, C.c_void_p(out.data_ptr()),
+                                            _cur_stream(X.device)), None, "colsum_dev")
     return out
 
 
 def center_dev(X, colsum, nrows: float):
     """X -= colsum / nrows in place on the device (the l2 centring, linear.py:411)."""
+    import torch
     n, d, ld = _rows(X)
     assert colsum.numel() == d and colsum.device == X.device
-    check(_lib.lib().midagma_center_dev(C.c_void_p(X.data_ptr()), n, d, ld, C.c_void_p(colsum.data_ptr()),
-                                        float(nrows), _cur_stream(X.device)), None, "center_dev")
+    with torch.cuda.device(X.device):
+        check(_lib.lib().midagma_center_dev(C.c_void_p(X.data_ptr()), n, d, ld, C.c_void_p(colsum.data_ptr()),
+                                            float(nrows), _cur_stream(X.device)), None, "center_dev")
 
 
 def gram(X, device: int | None = None):

@@ -110,6 +110,53 @@ int main(int argc, char** argv) {
     // Infinity Cache up to D ~ 5600; timing only: the column band is read while other tiles write)
     const double us_ip = time_us([&] { launch_trail128_band(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
     const double us_ip_pre = time_us([&] { launch_trail128_pre(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
+    // persistent workgroups (launch_trail128_persist): static round robin and a claimed-tile queue
+    double* Aout4;
+    int* ctr;
+    CK(hipMalloc(&Aout4, sizeof(double) * D * D));
+    CK(hipMalloc(&ctr, sizeof(int)));
+    CK(hipMemcpy(Aout4, Aout3, sizeof(double) * D * D, hipMemcpyDeviceToDevice));
+    double us_ps[3], us_pd[3], rd_ps = 0, rd_pd = 0;
+    const int nwgs[3] = {256, 512, 1024};
+    for (int k = 0; k < 3; ++k) {
+      us_ps[k] = time_us([&] { launch_trail128_persist(Ain, Aout4, D, g, false, nullptr, nwgs[k], nullptr, 0); }, reps);
+      CK(hipDeviceSynchronize());
+      rd_ps = fmax(rd_ps, reldiff(Aout4, Aout3, D * D));
+      us_pd[k] = time_us([&] {
+        CK(hipMemsetAsync(ctr, 0, sizeof(int), 0));
+        launch_trail128_persist(Ain, Aout4, D, g, false, nullptr, nwgs[k], ctr, 0);
+      }, reps);
+      CK(hipDeviceSynchronize());
+      rd_pd = fmax(rd_pd, reldiff(Aout4, Aout3, D * D));
+    }
+    const double us_memset = time_us([&] { CK(hipMemsetAsync(ctr, 0, sizeof(int), 0)); }, reps);
+    // stream-K remainder: dp = whole rounds of 512 tiles, the rest over nsk workgroups
+    const int ntl = (int)(((D - B2) / 128) * ((D - B2) / 128));
+    double* ws;
+    int* flg;
+    CK(hipMalloc(&ws, sizeof(double) * 2 * 1024 * 16384));
+    CK(hipMalloc(&flg, sizeof(int) * 1024));
+    CK(hipMemset(flg, 0, sizeof(int) * 1024));
+    double us_sk[3], rd_sk = 0;
+    const int nsks[3] = {256, 512, 1024};
+    for (int q = 0; q < 3; ++q) {
+      const int dp = (ntl / 512) * 512;
+      us_sk[q] = time_us([&] { launch_trail128_sk(Ain, Aout4, D, g, false, nullptr, dp, nsks[q], ws, flg, 0); }, reps);
+      CK(hipDeviceSynchronize());
+      rd_sk = fmax(rd_sk, reldiff(Aout4, Aout3, D * D));
+    }
+    const double us_sk0 = time_us([&] { launch_trail128_sk(Ain, Aout4, D, g, false, nullptr, ntl, 512, ws, flg, 0); },
+                                  reps);
+    printf("D=%5ld stream-K remainder (dp %d of %d tiles) over 256/512/1024 wgs %8.2f %8.2f %8.2f us | dp only "
+           "%8.2f us | max rel diff vs mid %.1e\n", (long)D, (ntl / 512) * 512, ntl, us_sk[0], us_sk[1], us_sk[2],
+           us_sk0, rd_sk);
+    CK(hipFree(ws));
+    CK(hipFree(flg));
+    printf("D=%5ld persistent static 256/512/1024 wgs %8.2f %8.2f %8.2f us | claimed %8.2f %8.2f %8.2f us (incl. "
+           "a %.2f us memset) | rel diff vs mid %.1e %.1e\n", (long)D, us_ps[0], us_ps[1], us_ps[2], us_pd[0],
+           us_pd[1], us_pd[2], us_memset, rd_ps, rd_pd);
+    CK(hipFree(Aout4));
+    CK(hipFree(ctr));
     const int tiles = (int)((t / 128) * (t / 128));
     printf("D=%5ld tiles=%5d (%.2f rounds of 512)  lib %8.2f us %5.1f TF | pre %8.2f us %5.1f TF | "
            "mid %8.2f us %5.1f TF | no-C0 store %8.2f us %5.1f TF | in place %8.2f / pre %8.2f us | max rel diff "
