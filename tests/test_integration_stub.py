@@ -73,6 +73,16 @@ def test_stub_minimize_gpu():
     s.minimize(W2, 1.0, 300, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
     s.close()
     assert ok and np.array_equal(W, W2)
+    # a float32 W: the stub turns on the float32 arithmetic (ABI 8), as HipSolver.set_w_float32 does
+    W32 = np.zeros((20, 20), dtype=np.float32)
+    W32, ok32 = ns["minimize"](obj, W32, 1.0, 300, 1.0, 3e-4, tol=-1.0)
+    s = HipSolver(20)
+    s.set_cov(o.cov)
+    s.set_w_float32(True)
+    W3 = np.zeros((20, 20))
+    s.minimize(W3, 1.0, 300, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
+    s.close()
+    assert ok32 and W32.dtype == np.float32 and np.array_equal(W32.astype(np.float64), W3)
     Wn = np.zeros((20, 20))
     Wn[3, 4] = np.nan
     with pytest.raises(ValueError):
