@@ -310,6 +310,46 @@ def test_checkpoint_early_stop_matches_oracle(hip, golden):
         assert abs(h - h2) <= 1e-9 + 1e-9 * abs(h2)
 
 
+@pytest.mark.parametrize("d,loss", [(100, "l2"), (300, "l2"), (64, "logistic")])
+def test_float32_data_mode_matches_reference_float32(hip, d, loss):
+    """dtype=np.float32 in data mode (X on the device): l2 at d = 100 (D = 128) and 300 (the
+    blocked inverse forked beside the GEMMs, I - W with its float32 diagonal from build_at), and
+    logistic (X W with a float32-valued W; continuous X and lambda1 = 0, so no L1-kink chaos), 60
+    steps from a float32 W = 0 against the oracle's float32 arithmetic (bit-exact to the
+    reference's float32 fit).  Data mode sums X^T X (I - W) in another order than cov mode, so a
+    float32 rounding may flip by an ulp: bound 1e-7 (the GPU's model, a float64 inverse rounded
+    to float32, is within 2e-9 on the CPU), and where float64 W is measurably away from the float32
+    trajectory (d = 300: 6e-5) at most 1% of that spread."""
+    K, n = 60, 2000
+    if loss == "l2":
+        X, _, _ = make_dataset(d, n, seed=d + 7)
+        lam = 0.03
+    else:
+        X = np.random.default_rng(d).normal(size=(n, d)) * 0.5
+        lam = 0.0
+    ref = {}
+    for dt in (np.float32, np.float64):
+        o = LinearOracle(loss, dtype=dt)
+        o.prepare(X.copy(), lam, 1000)
+        Wr, tr = o.minimize(np.zeros((d, d), dtype=dt), 1.0, K, 1.0, 3e-4, tol=-1.0)
+        assert tr.iters == K
+        ref[dt] = Wr.astype(np.float64)
+        Xd = o.X  # (centred in place for l2)
+    sol = _solver(d, Xd.T @ Xd / n, loss=loss, mode="data")
+    sol.set_data(np.ascontiguousarray(Xd), n_global=n)
+    sol.set_w_float32(True)
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=lam)
+    sol.close()
+    assert res.iters == K
+    assert np.array_equal(W, W.astype(np.float32).astype(np.float64))
+    dev = float(np.abs(W - ref[np.float32]).max())
+    spread = float(np.abs(ref[np.float64] - ref[np.float32]).max())
+    assert dev <= 1e-7, (dev, spread)
+    if spread > 1e-6:
+        assert dev <= 0.01 * spread, (dev, spread)
+
+
 # --------------------------------------------------------------------------- data mode / logistic
 class _BlockedOracle(LinearOracle):
     """The oracle with X^T sigmoid(XW) summed in 64-row blocks: a summation order as
