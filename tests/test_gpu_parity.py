@@ -310,6 +310,28 @@ def test_checkpoint_early_stop_matches_oracle(hip, golden):
         assert abs(h - h2) <= 1e-9 + 1e-9 * abs(h2)
 
 
+@pytest.mark.parametrize("d,K,s_dom", [(20, 100, 1.0), (300, 60, 1.0), (20, 50, 0.9)])
+def test_float32_line_search_branches(hip, d, K, s_dom):
+    """The domain line search on a float32 W (linear.py:230-241: revert W += lr g, lr /= 2,
+    re-step W -= lr g, each rounded to float32) and the out-of-domain return: lr = 0.3 gives one
+    halving at d = 20 and three at d = 300 (the blocked path), and s = 0.9 leaves the domain at
+    iteration 2.  Iterations, halvings, the final lr and success equal the reference's float32
+    arithmetic (the oracle with dtype=float32); W within 1e-6."""
+    X, _, _ = make_dataset(d, 1000, seed=0)
+    o = LinearOracle("l2", dtype=np.float32)
+    o.prepare(X.copy(), 0.03, 1000)
+    Wr, tr = o.minimize(np.zeros((d, d), dtype=np.float32), 1.0, K, s_dom, 0.3, tol=-1.0)
+    sol = _solver(d, o.cov)
+    sol.set_w_float32(True)
+    W = np.zeros((d, d))
+    res = sol.minimize(W, 1.0, K, s_dom, 0.3, tol=-1.0, lambda1=0.03)
+    sol.close()
+    assert (res.iters, res.halvings, res.success) == (tr.iters, tr.halvings, tr.success)
+    assert res.lr_final == tr.lr_final
+    assert np.array_equal(W, W.astype(np.float32).astype(np.float64))
+    assert np.abs(W - Wr.astype(np.float64)).max() <= 1e-6
+
+
 @pytest.mark.parametrize("d,loss", [(100, "l2"), (300, "l2"), (64, "logistic")])
 def test_float32_data_mode_matches_reference_float32(hip, d, loss):
     """dtype=np.float32 in data mode (X on the device): l2 at d = 100 (D = 128) and 300 (the
