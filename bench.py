@@ -136,14 +136,18 @@ def _run_worker(cmd, env, hb, stall, cap, store, key):
     while outcome is None:
         rc = p.poll()
         if rc is not None:
-            outcome = "ok" if rc == 0 else f"worker exited {rc}"
+            # (a worker that failed only in teardown, after its last mark "done", finished its work)
+            outcome = "ok" if rc == 0 or _last_mark(hb) == "done" else f"worker exited {rc}"
             break
         now = time.time()
         try:
             last = max(last, os.path.getmtime(hb))
         except OSError:
             pass
-        if now - last > stall:
+        if _last_mark(hb) == "done" and now - last > min(stall, 60.0):
+            outcome = "ok"  # the worker finished its work (rank 0: the line is out) and hangs in teardown
+            sys.stderr.write(f"bench worker still in teardown {now - last:.0f} s after its last mark: ended\n")
+        elif now - last > stall:
             outcome = f"no progress for {stall:.0f} s (last mark: {_last_mark(hb)})"
         elif now - t0 > cap:
             outcome = f"still running after {cap:.0f} s"
@@ -1545,6 +1549,7 @@ def main():
                 fr["vs_cpu_projected"] = fr["cpu_projected_wall_s"] / fr["wall_s"]
             line["full_fit"] = fr
         print(json.dumps(line), flush=True)
+    beat("done")
     if world > 1:
         import torch.distributed as dist
         dist.barrier()

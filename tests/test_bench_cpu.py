@@ -114,6 +114,9 @@ if rank == 0:
     np.save(os.environ["MIDAGMA_BENCH_COV_OUT"], X.T @ X / 500)
     print(json.dumps({"metric": "m", "value": 2.0, "unit": "steps/s", "n_gpus": 2,
                       "comm": {"path": "host-driven"}}), flush=True)
+open(os.environ["MIDAGMA_BENCH_HEARTBEAT"], "a").write("2 done\n")
+if rank == 1:
+    time.sleep(600)              # finished its work, then hangs in teardown: taken as done
 '''
 
 
@@ -126,7 +129,7 @@ def test_supervised_ranks_fall_back_to_host_path(tmp_path):
     w = tmp_path / "fake_worker.py"
     w.write_text(_FAKE_WORKER)
     env = dict(os.environ, MIDAGMA_BENCH_WORKER_CMD=json.dumps([sys.executable, str(w)]),
-               MIDAGMA_BENCH_STALL_S="60", PYTHONPATH=REPO)
+               MIDAGMA_BENCH_STALL_S="20", PYTHONPATH=REPO)
     env.pop("MIDAGMA_BENCH_COMM", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", "29581", os.path.join(REPO, "bench.py"),
