@@ -110,6 +110,9 @@ int main(int argc, char** argv) {
     // Infinity Cache up to D ~ 5600; timing only: the column band is read while other tiles write)
     const double us_ip = time_us([&] { launch_trail128_band(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
     const double us_ip_pre = time_us([&] { launch_trail128_pre(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
+    // in place with C0 folded in during the K loop (the product's tile body; timing only)
+    const double us_ip_mid = time_us([&] { launch_trail128(Aout2, Aout2, D, B2, g, false, nullptr, 0); }, reps);
+    printf("D=%5ld in place, C0 folded (mid) %8.2f us (ping-pong mid above)\n", (long)D, us_ip_mid);
     // persistent workgroups (launch_trail128_persist): static round robin and a claimed-tile queue
     double* Aout4;
     int* ctr;
