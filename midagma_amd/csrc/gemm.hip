@@ -1509,6 +1509,72 @@ void launch_trail128_persist(const double* Ain, double* Aout, int64_t D, int64_t
   HIP_TRY(hipGetLastError());
 }
 
+// The pipelined GEMM on the CUs of the first `ses` shader engines of each XCD (experiments build;
+// launch_gemm_cupart).  HW_REG_HW_ID bits 13-15 hold the shader engine (4 per XCD on MI355X, 8 CUs
+// each: tools/micro/hwid_probe.hip).
+template <int AMODE, int BMODE>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_cupart_kernel(int64_t K, int64_t kslice, int tiles_m, int tiles_n,
+                                                                 int ntasks, const double* __restrict__ A, int64_t lda,
+                                                                 const double* __restrict__ B, int64_t ldb,
+                                                                 double* __restrict__ C, int64_t ldc,
+                                                                 int64_t slice_stride, const State* __restrict__ st,
+                                                                 int ses, int* __restrict__ ctr) {
+  if (st && st->status != ST_RUNNING) return;
+  const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
+  if ((int)((hw >> 13) & 7) >= ses) return;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int claim;
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) claim = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = claim;
+    if (t >= ntasks) break;
+    gemm_pipe_tile<AMODE, BMODE, EPI_STORE>(t, K, kslice, tiles_m, tiles_n, A, lda, B, ldb, C, ldc, slice_stride,
+                                            nullptr, 0, 0, st, smem);
+  }
+}
+
+void launch_gemm_cupart(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, bool a_trans, const double* B,
+                        int64_t ldb, GemmB bmode, double* C, int64_t ldc, int split, int64_t slice_stride,
+                        const State* st, int ses, int* ctr, hipStream_t stream) {
+  if (M % 128 || N % 128 || K % 16 || split < 1 || ses < 1) throw std::invalid_argument("launch_gemm_cupart: bad shape");
+  const int64_t ktiles16 = K / 16, per16 = (ktiles16 + split - 1) / split;
+  const int nsplit = (int)((ktiles16 + per16 - 1) / per16);
+  const int tm = (int)(M / 128), tn = (int)(N / 128);
+  static int cus = 0;
+  static bool attr = false;
+  if (!cus) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  if (!attr) {
+    for (const void* f : {reinterpret_cast<const void*>(gemm_cupart_kernel<1, B_PLAIN>),
+                          reinterpret_cast<const void*>(gemm_cupart_kernel<1, B_IMINUS>),
+                          reinterpret_cast<const void*>(gemm_cupart_kernel<0, B_PLAIN>),
+                          reinterpret_cast<const void*>(gemm_cupart_kernel<0, B_IMINUS>)})
+      HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmPipeLds));
+    attr = true;
+  }
+  HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(int), stream));
+  const int ntasks = tm * tn * nsplit;
+  const dim3 grid((unsigned)(2 * cus));
+#define MIDAGMA_CP(AM, BM)                                                                                    \
+  hipLaunchKernelGGL((gemm_cupart_kernel<AM, BM>), grid, dim3(NTHREADS), kGemmPipeLds, stream, K, per16 * 16, tm, \
+                     tn, ntasks, A, lda, B, ldb, C, ldc, slice_stride, st, ses, ctr)
+  if (a_trans && bmode == B_PLAIN)
+    MIDAGMA_CP(1, B_PLAIN);
+  else if (a_trans)
+    MIDAGMA_CP(1, B_IMINUS);
+  else if (bmode == B_PLAIN)
+    MIDAGMA_CP(0, B_PLAIN);
+  else
+    MIDAGMA_CP(0, B_IMINUS);
+#undef MIDAGMA_CP
+  HIP_TRY(hipGetLastError());
+}
+
 // Stream-K remainder of the B2 = 256 trailing update (experiments build; launch_trail128_sk).
 struct TrailSkArgs {
   const double* Ain;

@@ -426,6 +426,14 @@ void launch_trail128_pre(const double* Ain, double* Aout, int64_t D, int64_t B2,
 // the tiles (ctr == nullptr), or tiles claimed from the counter *ctr (zero before the launch)
 void launch_trail128_persist(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, const State* st,
                              int nwg, int* ctr, hipStream_t stream);
+// The pipelined GEMM (EPI_STORE, split-K slices as launch_gemm) on a subset of the CUs: 2 workgroups
+// per CU are launched, those on a shader engine >= `ses` of their XCD exit at once, the others
+// claim tiles from *ctr (zeroed by a memset node before the launch, on `stream`), so the other
+// launches of the slot keep the remaining CUs to themselves (the cov score GEMM forked beside the
+// inverse, MIDAGMA_EXP_COV_FORK=2 with MIDAGMA_EXP_GEMM_SES)
+void launch_gemm_cupart(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, bool a_trans, const double* B,
+                        int64_t ldb, GemmB bmode, double* C, int64_t ldc, int split, int64_t slice_stride,
+                        const State* st, int ses, int* ctr, hipStream_t stream);
 // The B2 = 256 update as data-parallel tiles plus a stream-K remainder: the first `dp` tiles (of
 // xcd_remap's order) one per workgroup (EPI_SUB_MID), the other ntiles - dp tiles' 16 K-tiles each
 // split evenly over `nsk` workgroups; a partial tile goes to ws (2 nsk 128 x 128 slots), the

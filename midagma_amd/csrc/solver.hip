@@ -120,6 +120,7 @@ struct midagma_solver {
   int split = 1;
   int sig_split = 1;  // the logistic sigmoid GEMM's serial split-K (launch_gemm; 2: Y holds the partial too)
   int sig_split_force = 0;
+  DevBuf cupart_ctr;  // experiments: launch_gemm_cupart's tile counter
   bool w32 = false;  // midagma_set_w_float32: the reference's float32 W arithmetic (common.h f32r)  // midagma_debug_sig_split: 0 the size rule, 1 never split, 2 split where the shape allows
   int64_t loss_part_count = 0;
 
@@ -165,7 +166,7 @@ struct midagma_solver {
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &nmSync, &npart, &XT, &IW, &scarry,
-                      &sprev})
+                      &sprev, &cupart_ctr})
       b->release();
 #ifdef MIDAGMA_EXPERIMENTS
     for (DevBuf* b : {&dfA, &dfY, &dfQ, &dfP, &dfCtl, &dfTasks[0], &dfTasks[1], &dfWoff[0], &dfWoff[1], &dfStamps})
@@ -429,6 +430,19 @@ struct midagma_solver {
   // (bmode B_PLAIN: Wp already holds I - W)
   void enqueue_cov_gemm(const double* Cm, const double* Wp, double* out, const State* st, bool sum = true,
                         bool a_trans = false, GemmB bmode = B_IMINUS) {
+#ifdef MIDAGMA_EXPERIMENTS
+    // experiment: the forked score GEMM confined to the first MIDAGMA_EXP_GEMM_SES shader engines of
+    // every XCD, so the inverse's launches on the side stream keep the other CUs to themselves
+    static const int gemm_ses = (int)knob("MIDAGMA_EXP_GEMM_SES", 0);
+    if (gemm_ses > 0 && cov_fork_on() && D % 128 == 0) {
+      if (!cupart_ctr.p) throw std::logic_error("cupart counter not allocated");
+      double* dst = cov_split > 1 ? cov_parts.p : out;
+      launch_gemm_cupart(D, D, Kd(), Cm, D, a_trans, Wp, D, bmode, dst, D, cov_split, D * D, st, gemm_ses,
+                         reinterpret_cast<int*>(cupart_ctr.p), stream);
+      if (cov_split > 1 && sum) launch_sum_slices(cov_parts.p, cov_split, D * D, D * D, out, st, stream);
+      return;
+    }
+#endif
     if (cov_split > 1) {
       launch_gemm(D, D, Kd(), Cm, D, a_trans, Wp, D, bmode, cov_parts.p, D, EPI_STORE, cov_split, D * D, nullptr, 0,
                   0, st, stream);
@@ -717,6 +731,7 @@ struct midagma_solver {
       HIP_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+      if (kExperiments) cupart_ctr.alloc(1);  // (launch_gemm_cupart's counter; not while capturing)
     }
   }
 
