@@ -8,6 +8,8 @@
 // Without MIDAGMA_KSTAMPS every macro is empty.
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 namespace midagma {
 
 enum KStampKind : int { KS_RESID = 0, KS_PASS = 1, KS_PANEL = 2, KS_TRAIL = 3, KS_KINDS = 4 };

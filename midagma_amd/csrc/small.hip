@@ -32,6 +32,40 @@
 #include "tcc_blk.h"
 
 namespace midagma {
+
+// Phase stamps of the persistent slot loop (diagnostic build only: `make kstamps`, -DMIDAGMA_KSTAMPS;
+// tools/small_stamps.py): thread 0 reads the shader clock at the slot's phase points and sums each
+// phase over the launch's slots; without MIDAGMA_KSTAMPS the macros are empty.
+#ifdef MIDAGMA_KSTAMPS
+__device__ unsigned long long g_small_stamps[16];  // [0..11] phase sums, [12] slots, [13] real time
+#define SS_DECL                                                     \
+  unsigned long long ss_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+  unsigned long long ss_t = __builtin_amdgcn_s_memtime();            \
+  const unsigned long long ss_rt0 = __builtin_amdgcn_s_memrealtime(); \
+  unsigned long long ss_n = 0
+#define SS_MARK(p)                                                  \
+  {                                                                 \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+    ss_acc[p] += t_ - ss_t;                                         \
+    ss_t = t_;                                                      \
+  }
+#define SS_COUNT(p, c) ss_acc[p] += (c)
+#define SS_SLOT() ++ss_n
+#define SS_END()                                                                                 \
+  if (threadIdx.x == 0) {                                                                        \
+    for (int p_ = 0; p_ < 12; ++p_) atomicAdd(&g_small_stamps[p_], ss_acc[p_]);                  \
+    atomicAdd(&g_small_stamps[12], ss_n);                                                        \
+    atomicAdd(&g_small_stamps[13], __builtin_amdgcn_s_memrealtime() - ss_rt0);                  \
+  }
+#else
+#define SS_DECL \
+  do {          \
+  } while (0)
+#define SS_MARK(p)
+#define SS_COUNT(p, c)
+#define SS_SLOT()
+#define SS_END()
+#endif
 namespace {
 
 __device__ __forceinline__ double sgn(double w) { return w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : w); }
@@ -78,14 +112,25 @@ struct SmallCtl {
   double lr_a, lr_b, bc1, bc2;
 };
 
+// The Params fields the controller reads, copied once per launch into LDS (read through the
+// out-of-line controller's pointer argument, Params were vector-memory loads on every slot; passed
+// by value, the struct went through the stack).  next_ck: the next multiple of `checkpoint` above
+// the iteration (the controller advances it), in place of a 64-bit remainder per slot.
+struct SmallCtlParams {
+  double d_log_s, score_scale, mu, lambda1, trek_weight, tol, s;
+  int64_t max_iter, checkpoint;
+  int32_t trek_mode, pad_;
+};
+
 // The controller: step.hip's control_kernel decisions (linear.py:230-241, 279-331) on the
 // State in LDS, run by thread 0 once per slot.  Kept out of line: inlined into the slot loop,
 // its code raised the kernel to 230+ VGPRs (DS = 64 spilled inside the Gauss-Jordan loop).
 template <int NW>
-__device__ __noinline__ void small_control(const Params* __restrict__ pr, State& S, SmallCtl& ctl,
+__device__ __noinline__ void small_control(const SmallCtlParams& pr_, State& S, SmallCtl& ctl,
                                            const double (*red)[NW], const double (*nred)[NW], const int* flw,
                                            CkptRec* __restrict__ ckpt, int64_t ckpt_cap, double bc1n,
-                                           double bc2n, const double* trek_val) {
+                                           double bc2n, const double* trek_val, int64_t& next_ck) {
+    const SmallCtlParams* const pr = &pr_;
     int flags = 0;
 #pragma unroll 1
     for (int x = 0; x < NW; ++x) flags |= flw[x];
@@ -183,7 +228,9 @@ __device__ __noinline__ void small_control(const Params* __restrict__ pr, State&
         S.lr_a = S.lr;
         act = ACT_STEP;
         S.iter = it;
-        if (it % pr->checkpoint == 0 || it == pr->max_iter) S.ckpt_pending = 1;
+        const bool at_ck = it == next_ck;  // (it % checkpoint == 0)
+        if (at_ck) next_ck += pr->checkpoint;
+        if (at_ck || it == pr->max_iter) S.ckpt_pending = 1;
       }
     }
     S.action = act;
@@ -261,8 +308,13 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   const int di = (int)d;
   const bool has_inc = pr->has_inc != 0, has_exc = pr->has_exc != 0;
 
+  __shared__ SmallCtlParams cp;  // (thread 0's)
+  __shared__ int64_t next_ck;
   if (tid == 0) {
+    cp = SmallCtlParams{pr->d_log_s, pr->score_scale, pr->mu, pr->lambda1, pr->trek_weight, pr->tol,
+                        pr->s,       pr->max_iter,    pr->checkpoint, pr->trek_mode, 0};
     S = *stg;
+    next_ck = (S.iter / cp.checkpoint + 1) * cp.checkpoint;
     ctl.run = S.status == ST_RUNNING && n_slots > 0;
     if (S.ckpt_pending)  // the pending checkpoint step's norms, reduced by the last launch
       for (int f = 0; f < NORM_FIELDS; ++f) {
@@ -321,7 +373,9 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   }
   __syncthreads();
 
+  SS_DECL;
   for (int64_t slot = 0; slot < n_slots; ++slot) {
+    SS_SLOT();
     // the TCC regularizer of this slot's W (linear.py:251-258; tcc_gate_kernel's rule: every slot
     // in 'opt' mode, checkpoint slots in 'log' mode)
     bool tcc_ran = false;
@@ -357,6 +411,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     // inv(S) = X0 (I + R)(I + R^2)[(I + R^4)], R = I - S X0, from the linear extrapolation
     // X0 = 2 P1 - P2 of the last two inverses (P1 alone after a halving), on the matrix cores
     // (blockinv.hip's fast path at one-workgroup scale; d ||R||max bounds ||R||inf).
+    SS_MARK(0)  // TCC (when on), the table read issued, (sI - W o W)^T built
     bool gj = S.ckpt_pending != 0 || warm == 0;
     if (!gj) {
       double x0[E], r[E];
@@ -395,6 +450,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 #pragma unroll
       for (int x = 0; x < NW; ++x) nr = fmax(nr, nrm[x]);
       nr *= (double)di;
+      SS_MARK(7)  // warm start, residual R = I - S X0, its norm (wave max, barrier)
       if (nr <= 1e-2) {
         const bool three = !(nr <= 1e-4);  // ||R||^4 > 1e-16: one more factor
         double y[E], r2[E];
@@ -419,6 +475,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
           if (three) PR[1][rows[e] * SW + cols[e]] = r2[e];
         }
         __syncthreads();
+        SS_MARK(8)  // pass 1: Y = X0 + X0 R, R^2, images, barrier
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
           const int row0 = 16 * tr[u], col0 = cols[4 * u] - c;
@@ -433,6 +490,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
             r2[e] = real[e] ? rv[t] : 0.0;
           }
         }
+        SS_MARK(9)  // pass 2: Y + Y R^2 (and R^4)
         if (three) {
           if (ONE) __syncthreads();
 #pragma unroll
@@ -507,6 +565,8 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
       p1[e] = a[e];
     }
     warm = warm < 2 ? warm + 1 : 2;
+    SS_MARK(1)  // the inverse (product form, or Gauss-Jordan on checkpoint / cold slots)
+    SS_COUNT(6, gj ? 1 : 0);
 
     // ---- rhs = ((-mu) cov) @ (I - W)  (linear.py:244) on the matrix cores
     double z[E];
@@ -522,6 +582,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
       for (int t = 0; t < 4; ++t) z[4 * u + t] = acc[t];
     }
 
+    SS_MARK(2)  // the score product on the matrix cores
     // ---- domain test (linear.py:226-230) and, when due, the checkpoint objective's sums
     int fl = 0;
 #pragma unroll
@@ -555,8 +616,11 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     __syncthreads();
 
     // ---- control, thread 0 (step.hip control_kernel; linear.py:230-241, 279-331)
-    if (tid == 0) small_control<NW>(pr, S, ctl, red, nred, flw, ckpt, ckpt_cap, bc1n, bc2n, TCC ? tsc : nullptr);
+    SS_MARK(3)  // domain flags and checkpoint sums, barrier
+    if (tid == 0)
+      small_control<NW>(cp, S, ctl, red, nred, flw, ckpt, ckpt_cap, bc1n, bc2n, TCC ? tsc : nullptr, next_ck);
     __syncthreads();
+    SS_MARK(4)  // the controller (thread 0), barrier
     const int act = ctl.act;
     if (act == ACT_NOOP) break;  // terminal: nothing of this slot is applied
     if (act == ACT_HALVE) warm = 1;  // W turns back: the last two inverses do not extrapolate
@@ -641,8 +705,10 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     }
     const bool more = ctl.run != 0;
     __syncthreads();
+    SS_MARK(5)  // G_obj, Adam, update (and the checkpoint norms), barrier
     if (!more) break;
   }
+  SS_END();
 
   // write back: the state, this lane's elements, the pending checkpoint step's norms
 #pragma unroll
@@ -680,6 +746,18 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 }
 
 }  // namespace
+
+#ifdef MIDAGMA_KSTAMPS
+// the phase sums of the small loop since the last call (then zeroed): [0..5], [7..9] shader-clock
+// cycles per phase, [6] Gauss-Jordan slots, [12] slots, [13] real-time (100 MHz) span of the launches
+extern "C" int midagma_debug_small_stamps(unsigned long long* out) {
+  const size_t bytes = 16 * sizeof(unsigned long long);
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_small_stamps), bytes) != hipSuccess) return -1;
+  static const unsigned long long zero[16] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_small_stamps), zero, bytes) != hipSuccess) return -1;
+  return 0;
+}
+#endif
 
 // d <= 64 (DS = 64: single-buffered images, 16 waves; MIDAGMA_EXP_SMALL64=0 keeps 32 < d <= 64 on
 // the graph-replayed slots)
