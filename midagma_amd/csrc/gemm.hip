@@ -968,7 +968,7 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
   hipLaunchKernelGGL((gemm_pipe_kernel<AM, BM, EP>), dim3((unsigned)nwg), dim3(NTHREADS), kGemmPipeLds, stream, K, \
                      kslice, tm, tn, A, lda, B, ldb, C, ldc, slice_stride, loss_part, m_valid, n_valid, st)
     if (epi == EPI_SIGMOID) {
-      if (a_trans && N != K) throw std::invalid_argument("launch_gemm: sigmoid form");
+      if (K > N) throw std::invalid_argument("launch_gemm: sigmoid form (op(A) is X: K <= N)");
       if (nsplit > 1 && a_trans)
         MIDAGMA_GEMMP(1, B_PLAIN, EPI_SIGMOID_SPLIT);
       else if (nsplit > 1)

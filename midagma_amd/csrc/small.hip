@@ -373,6 +373,19 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   }
   __syncthreads();
 
+  // the update's constants in registers (read through pr in the loop, they were reloaded every
+  // slot: the out-of-line controller may write memory), and the lane's mask entries, fixed for
+  // the launch (linear.py:217-222)
+  const double c_zscale = pr->zscale, c_mu_l1 = pr->mu_l1, c_beta1 = pr->beta1, c_c1 = pr->c1,
+               c_beta2 = pr->beta2, c_c2 = pr->c2;
+  double incv[E], excv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int64_t idx = (int64_t)rows[e] * D + cols[e];
+    incv[e] = has_inc && real[e] ? minc[idx] : 0.0;
+    excv[e] = has_exc && real[e] ? mexc[idx] : 1.0;
+  }
+
   SS_DECL;
   for (int64_t slot = 0; slot < n_slots; ++slot) {
     SS_SLOT();
@@ -632,55 +645,77 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     double qf[NORM_FIELDS];
 #pragma unroll
     for (int f = 0; f < NORM_FIELDS; ++f) qf[f] = f == NF_WMIN ? INFINITY : 0.0;
+    if (act == ACT_STEP) {
+      // straight-line over the lane's E elements (selects, no per-element branches), so that
+      // the four elements' division and square-root chains interleave: one wave per SIMD has no
+      // other wave to hide their latency (d = 20: 3762 -> 2839 cycles a slot in this phase)
+      double gs[E], gl1[E], gh[E], gi[E], gtr[E], gob[E], mm[E], vx[E], gd[E], wn[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      if (!real[e]) continue;
-      const double wo = wv[e];
-      if (act == ACT_STEP) {
-        const int64_t idx = (int64_t)rows[e] * D + cols[e];
+      for (int e = 0; e < E; ++e) {
+        const double wo = wv[e];
         const double mt = m_entry(a[e], w32);
-        const double gs = pr->zscale * z[e];
+        gs[e] = c_zscale * z[e];
         const double sg = sgn(wo);
-        const double gl1 = pr->mu_l1 * sg;
-        const double gh = h_term(wo, mt, w32);
-        double gobj = gs + gl1;
-        gobj = gobj + gh;
-        double gi = 0.0;
-        if (has_inc) {
-          gi = minc[idx] * sg;
-          gobj = gobj + gi;
-        }
-        double gtr = 0.0;
+        gl1[e] = c_mu_l1 * sg;
+        gh[e] = h_term(wo, mt, w32);
+        double g = gs[e] + gl1[e];
+        g = g + gh[e];
+        gi[e] = has_inc ? incv[e] * sg : 0.0;
+        g = has_inc ? g + gi[e] : g;
+        gtr[e] = 0.0;
         if constexpr (TCC) {  // Gobj + weight * trek_grad (linear.py:257-258), step.hip's order
           if (tc.mode == 2 && tcc_ran) {
-            gtr = tccb::tcc_grad_elem<TNB, TBS>(TL, di, rows[e], cols[e], wo, tc.m, tc.weight);
-            gobj = gobj + gtr;
+            gtr[e] = tccb::tcc_grad_elem<TNB, TBS>(TL, di, rows[e], cols[e], wo, tc.m, tc.weight);
+            g = g + gtr[e];
           }
         }
-        const double mm = mv[e] * pr->beta1 + pr->c1 * gobj;
-        const double vx = vv[e] * pr->beta2 + pr->c2 * (gobj * gobj);
-        const double mh = mm / bc1;
-        const double vh = vx / bc2;
-        const double gd = mh / (sqrt(vh) + 1e-8);
-        double wn = wo - lr_a * gd;
-        if (w32) wn = f32r(wn);  // W -= lr * grad into a float32 W (linear.py:275)
-        if (has_exc) wn = wn * mexc[idx];
-        mv[e] = mm;
-        vv[e] = vx;
-        wv[e] = wn;
-        if (norms) {
-          qf[NF_GOBJ] += gobj * gobj;
-          qf[NF_GSCORE] += gs * gs;
-          qf[NF_GDAG] += gh * gh;
-          qf[NF_GL1] += gl1 * gl1;
-          qf[NF_GINC] += gi * gi;
-          qf[NF_GTREK] += gtr * gtr;
-          qf[NF_GSTEP] += gd * gd;
-          qf[NF_W2] += wn * wn;
-          qf[NF_WMAX] = fmax(qf[NF_WMAX], fabs(wn));
-          if (wn != 0.0) qf[NF_WMIN] = fmin(qf[NF_WMIN], fabs(wn));
+        gob[e] = g;
+        mm[e] = mv[e] * c_beta1 + c_c1 * g;
+        vx[e] = vv[e] * c_beta2 + c_c2 * (g * g);
+      }
+      double mh[E], vh[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        mh[e] = mm[e] / bc1;
+        vh[e] = vx[e] / bc2;
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) vh[e] = sqrt(vh[e]) + 1e-8;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        gd[e] = mh[e] / vh[e];
+        double x = wv[e] - lr_a * gd[e];
+        if (w32) x = f32r(x);  // W -= lr * grad into a float32 W (linear.py:275)
+        wn[e] = has_exc ? x * excv[e] : x;
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (real[e]) {
+          mv[e] = mm[e];
+          vv[e] = vx[e];
+          wv[e] = wn[e];
         }
-      } else {
+      if (norms) {
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (real[e]) {
+            qf[NF_GOBJ] += gob[e] * gob[e];
+            qf[NF_GSCORE] += gs[e] * gs[e];
+            qf[NF_GDAG] += gh[e] * gh[e];
+            qf[NF_GL1] += gl1[e] * gl1[e];
+            qf[NF_GINC] += gi[e] * gi[e];
+            qf[NF_GTREK] += gtr[e] * gtr[e];
+            qf[NF_GSTEP] += gd[e] * gd[e];
+            qf[NF_W2] += wn[e] * wn[e];
+            qf[NF_WMAX] = fmax(qf[NF_WMAX], fabs(wn[e]));
+            if (wn[e] != 0.0) qf[NF_WMIN] = fmin(qf[NF_WMIN], fabs(wn[e]));
+          }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (!real[e]) continue;
+        const double wo = wv[e];
         const double gd = (mv[e] / bc1) / (sqrt(vv[e] / bc2) + 1e-8);
         if (act == ACT_HALVE) {  // (float32 W: each in-place update rounds, linear.py:235, 239)
           double wn = wo + lr_a * gd;
@@ -692,10 +727,14 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
           wv[e] = w32 ? f32r(wn) : wn;
         }
       }
-      if (!ONE) Wimg[rows[e] * SW + cols[e]] = wv[e];
-      if (rows[e] == cols[e]) wdiag[rows[e]] = wv[e];
-      IWimg[rows[e] * SI + cols[e]] = one_minus(rows[e] == cols[e], wv[e], w32);
     }
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (real[e]) {
+        if (!ONE) Wimg[rows[e] * SW + cols[e]] = wv[e];
+        if (rows[e] == cols[e]) wdiag[rows[e]] = wv[e];
+        IWimg[rows[e] * SI + cols[e]] = one_minus(rows[e] == cols[e], wv[e], w32);
+      }
     if (norms) {
 #pragma unroll
       for (int f = 0; f < NORM_FIELDS; ++f) {
@@ -796,6 +835,8 @@ void launch_small_minimize(const Params* pr, State* st, double* W, double* m, do
       MIDAGMA_SMALL(32, 4, 4, false);
     else if (w32)
       MIDAGMA_SMALL(32, 4, 0, true);
+    else if (knob("MIDAGMA_EXP_SMALL_NW", 4) == 2)
+      MIDAGMA_SMALL(32, 2, 0, false);
     else
       MIDAGMA_SMALL(32, 4, 0, false);
   } else if (w32) {

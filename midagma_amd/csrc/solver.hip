@@ -459,7 +459,7 @@ struct midagma_solver {
       launch_gemm(n_pad, D, Kd(), xw_a(), xw_lda(), use_xt, iw ? iw : Wp, D, iw ? B_PLAIN : B_IMINUS, Y.p, D, EPI_STORE, 1,
                   0, nullptr, 0, 0, st, stream);
     } else {
-      launch_gemm(n_pad, D, D, xw_a(), xw_lda(), use_xt, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, sig_split,
+      launch_gemm(n_pad, D, Kd(), xw_a(), xw_lda(), use_xt, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, sig_split,
                   sig_split > 1 ? n_pad * D : 0, loss_part.p, n_local, d, st, stream);
       launch_sum_vector(loss_part.p, loss_part_count, zbuf + D * D, st, stream);
     }
@@ -1532,7 +1532,7 @@ int midagma_profile_parts(midagma_solver* s, int reps, double* ms_out) {
           launch_gemm(s->n_pad, D, s->Kd(), s->xw_a(), s->xw_lda(), s->use_xt, s->IW.p ? s->IW.p : s->W.p, D,
                       s->IW.p ? B_PLAIN : B_IMINUS, s->Y.p, D, EPI_STORE, 1, 0, nullptr, 0, 0, s->d_state, s->stream);
         else
-          launch_gemm(s->n_pad, D, D, s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID,
+          launch_gemm(s->n_pad, D, s->Kd(), s->xw_a(), s->xw_lda(), s->use_xt, s->W.p, D, B_PLAIN, s->Y.p, D, EPI_SIGMOID,
                       s->sig_split, s->sig_split > 1 ? s->n_pad * D : 0, s->loss_part.p, s->n_local, s->d,
                       s->d_state, s->stream);
       });
