@@ -99,11 +99,14 @@ __device__ __forceinline__ dbl4 tile_mma(const double* __restrict__ A, const dou
                                                  acc, 0, 0, 0);
     return acc;
   }
+  // DS <= 32: all DS / 4 k-steps, unguarded (the k >= d terms are the exact zeros above): the
+  // operand reads of a branch-free unrolled chain issue together, where a guard per k-step
+  // serialised read, wait and MFMA (d = 20: 5 guarded steps cost more than 8 pipelined ones)
+  (void)kd;
 #pragma unroll
   for (int kk = 0; kk < DS / 4; ++kk)
-    if (4 * kk < kd)
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(row0 + c) * SA_ + 4 * kk + q], B[(4 * kk + q) * SB_ + col0 + c],
-                                                 acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(row0 + c) * SA_ + 4 * kk + q], B[(4 * kk + q) * SB_ + col0 + c],
+                                               acc, 0, 0, 0);
   return acc;
 }
 
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   double* const PA[2] = {PAbuf, ONE ? PAbuf : PAbuf + DS * SW};
   double* const PR[2] = {PRbuf, ONE ? PRbuf : PRbuf + DS * SW};
   double* const PB[2] = {ONE ? PRbuf : PBbuf, ONE ? PRbuf : PBbuf + DS * SI};
-  __shared__ double nrm[NW];
+  __shared__ int nrm[NW];                     // per wave: residual above 1e-2 (bit 0), 1e-4 (bit 1)
   __shared__ double red[3][NW];               // checkpoint objective: (I - W) o Z, |W|, log|pivot|
   __shared__ double nred[NORM_FIELDS][NW];    // the checkpoint step's norms, per wave
   __shared__ int flw[NW];
@@ -382,9 +385,19 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int64_t idx = (int64_t)rows[e] * D + cols[e];
-    incv[e] = has_inc && real[e] ? minc[idx] : 0.0;
-    excv[e] = has_exc && real[e] ? mexc[idx] : 1.0;
+    incv[e] = !ONE && has_inc && real[e] ? minc[idx] : 0.0;  // (DS = 64: read in the loop)
+    excv[e] = !ONE && has_exc && real[e] ? mexc[idx] : 1.0;
   }
+  // the controller's state every thread keeps (wave-uniform copies of S's fields): a plain Adam
+  // step (no checkpoint due, no domain or finiteness flag) is decided by every thread from these,
+  // thread 0 mirroring the State in LDS without a barrier; other slots go through small_control
+  // (thread 0, then a barrier) and reload them.  Not at DS = 64, whose 16 waves have 128 VGPRs
+  // each: the copies spill there (d = 48: 46.4k -> 43.0k steps/s)
+  constexpr bool RC = !ONE;
+  const int64_t c_ld_table = pr->ld_table, c_max_iter = cp.max_iter, c_checkpoint = cp.checkpoint;
+  int64_t r_iter = S.iter, r_slots = S.slots, r_next = next_ck;
+  double r_lr = S.lr;
+  int r_ckpt = S.ckpt_pending, r_wrun = S.warm_run;
 
   SS_DECL;
   for (int64_t slot = 0; slot < n_slots; ++slot) {
@@ -393,7 +406,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     // in 'opt' mode, checkpoint slots in 'log' mode)
     bool tcc_ran = false;
     if constexpr (TCC) {
-      if (tc.mode == 2 || S.ckpt_pending) {
+      if (tc.mode == 2 || (RC ? r_ckpt : S.ckpt_pending)) {
         tccb::tcc_blk_body<TNB, TBS>([&](int i, int j) { return Wimg[i * SW + j]; },
                                 [&](int i, int j) { return tc.S[(int64_t)i * D + j]; }, tc.ws, di, tc.mode, tc.eps,
                                 tc.m, tc.weight, tsc, tvp, tup, nullptr, D, TL);
@@ -402,9 +415,10 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     }
     // 1 - beta^it for it = iter + 1 from the host table (read early: latency under the inverse)
     double bc1n = 1.0, bc2n = 1.0;
-    if (tid == 0 && S.iter < pr->ld_table) {
-      bc1n = bc_table[2 * S.iter];
-      bc2n = bc_table[2 * S.iter + 1];
+    if (RC ? r_iter < c_ld_table : (tid == 0 && S.iter < c_ld_table)) {
+      const int64_t it0 = RC ? r_iter : S.iter;
+      bc1n = bc_table[2 * it0];
+      bc2n = bc_table[2 * it0 + 1];
     }
 
     // ---- (sI - W o W)^T, identity padding (linear.py:226, 113)
@@ -412,12 +426,10 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = rows[e], j = cols[e];
-      if (real[e]) {
-        const double wji = ONE ? (i == j ? wdiag[i] : -IWimg[j * SI + i]) : Wimg[j * SW + i];
-        a[e] = sw_entry(i == j, s_dom, wji, w32);
-      } else {
-        a[e] = (i == j) ? 1.0 : 0.0;
-      }
+      // (read unconditionally, then selected: a read per element under its own exec mask
+      // serialised the reads)
+      const double wji = ONE ? (i == j ? wdiag[i] : -IWimg[j * SI + i]) : Wimg[j * SW + i];
+      a[e] = real[e] ? sw_entry(i == j, s_dom, wji, w32) : ((i == j) ? 1.0 : 0.0);
     }
     // ---- a <- inv(A^T) = inv(A)^T.  Checkpoint slots (log|det| needs the pivots), the first
     // slot of a launch and unconverged warm starts: Gauss-Jordan.  Otherwise the product form
@@ -425,10 +437,13 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     // X0 = 2 P1 - P2 of the last two inverses (P1 alone after a halving), on the matrix cores
     // (blockinv.hip's fast path at one-workgroup scale; d ||R||max bounds ||R||inf).
     SS_MARK(0)  // TCC (when on), the table read issued, (sI - W o W)^T built
-    bool gj = S.ckpt_pending != 0 || warm == 0;
+    bool gj = (RC ? r_ckpt : S.ckpt_pending) != 0 || warm == 0;
     if (!gj) {
       double x0[E], r[E];
-      double mx = 0.0;
+      // ||R||: d max|R_ij| against 1e-2 (the series converges in the passes below) and 1e-4
+      // (a third pass); rounding of d x is monotone, so max_ij(d |R_ij|) = d max_ij |R_ij| and
+      // the two tests are lane tests, reduced by ballots (a wave max took 6 dependent shuffles)
+      bool big2 = false, big4 = false;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = rows[e], j = cols[e];
@@ -445,8 +460,9 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
         for (int t = 0; t < 4; ++t) {
           const int e = 4 * u + t;
           r[e] = real[e] ? (((rows[e] == cols[e]) ? 1.0 : 0.0) - t4[t]) : 0.0;
-          const double ar = fabs(r[e]);
-          mx = ar != ar ? INFINITY : fmax(mx, ar);
+          const double dr = (double)di * fabs(r[e]);  // (NaN: fails both tests, as a NaN max did)
+          big2 = big2 || !(dr <= 1e-2);
+          big4 = big4 || !(dr <= 1e-4);
         }
       }
       if (ONE) __syncthreads();  // every wave is done reading the images it overwrites
@@ -456,16 +472,17 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
         PB[0][rows[e] * SB + cols[e]] = r[e];
         PR[0][rows[e] * SW + cols[e]] = r[e];
       }
-      mx = wave_max(mx);
-      if (lane == 0) nrm[w] = mx;
+      {
+        const unsigned long long b2 = __ballot(big2), b4 = __ballot(big4);
+        if (lane == 0) nrm[w] = (b2 ? 1 : 0) | (b4 ? 2 : 0);
+      }
       __syncthreads();
-      double nr = 0.0;
+      int nfl = 0;
 #pragma unroll
-      for (int x = 0; x < NW; ++x) nr = fmax(nr, nrm[x]);
-      nr *= (double)di;
-      SS_MARK(7)  // warm start, residual R = I - S X0, its norm (wave max, barrier)
-      if (nr <= 1e-2) {
-        const bool three = !(nr <= 1e-4);  // ||R||^4 > 1e-16: one more factor
+      for (int x = 0; x < NW; ++x) nfl |= nrm[x];
+      SS_MARK(7)  // warm start, residual R = I - S X0, its norm (ballots, barrier)
+      if (!(nfl & 1)) {
+        const bool three = (nfl & 2) != 0;  // ||R||^4 > 1e-16: one more factor
         double y[E], r2[E];
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
@@ -588,7 +605,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
       dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int kk = 0; kk < DS / 4; ++kk)
-        if (4 * kk < di)
+        if (!ONE || 4 * kk < di)  // (DS <= 32 unguarded, as tile_mma; cov's padding is zero)
           acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Cimg[(16 * tr[u] + c) * SW + 4 * kk + q],
                                                      IWimg[(4 * kk + q) * SI + cols[4 * u]], acc, 0, 0, 0);
 #pragma unroll
@@ -608,7 +625,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
       const unsigned long long b1 = __ballot(fl & 1), b2 = __ballot(fl & 2);
       if (lane == 0) flw[w] = (b1 ? 1 : 0) | (b2 ? 2 : 0);
     }
-    if (S.ckpt_pending) {
+    if (RC ? r_ckpt : S.ckpt_pending) {
       double sd = 0.0, l1 = 0.0;
 #pragma unroll
       for (int e = 0; e < E; ++e)
@@ -628,24 +645,73 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     }
     __syncthreads();
 
-    // ---- control, thread 0 (step.hip control_kernel; linear.py:230-241, 279-331)
+    // ---- control (step.hip control_kernel; linear.py:230-241, 279-331): checkpoint slots and
+    // flagged slots on thread 0 (small_control), the plain step by every thread
     SS_MARK(3)  // domain flags and checkpoint sums, barrier
-    if (tid == 0)
-      small_control<NW>(cp, S, ctl, red, nred, flw, ckpt, ckpt_cap, bc1n, bc2n, TCC ? tsc : nullptr, next_ck);
-    __syncthreads();
-    SS_MARK(4)  // the controller (thread 0), barrier
-    const int act = ctl.act;
+    int fl_all = 0;
+    if (RC)
+#pragma unroll
+      for (int x = 0; x < NW; ++x) fl_all |= flw[x];
+    int act;
+    bool norms, more;
+    double lr_a, lr_b, bc1, bc2;
+    if (!RC || r_ckpt || fl_all) {
+      if (tid == 0)
+        small_control<NW>(cp, S, ctl, red, nred, flw, ckpt, ckpt_cap, bc1n, bc2n, TCC ? tsc : nullptr, next_ck);
+      __syncthreads();
+      act = ctl.act;
+      norms = ctl.norms != 0;
+      more = ctl.run != 0;
+      lr_a = ctl.lr_a;
+      lr_b = ctl.lr_b;
+      bc1 = ctl.bc1;
+      bc2 = ctl.bc2;
+      r_iter = S.iter;
+      r_slots = S.slots;
+      r_lr = S.lr;
+      r_ckpt = S.ckpt_pending;
+      r_wrun = S.warm_run;
+      r_next = next_ck;
+    } else {  // small_control's ACT_STEP branch, state in registers
+      const int64_t it = r_iter + 1;
+      const bool at_ck = it == r_next;  // (it % checkpoint == 0)
+      if (at_ck) r_next += c_checkpoint;
+      r_ckpt = (at_ck || it == c_max_iter) ? 1 : 0;
+      r_wrun = r_wrun < 2 ? r_wrun + 1 : 2;
+      if (tid == 0) {
+        if (r_slots == 0) S.t0 = __builtin_amdgcn_s_memrealtime();
+        S.slots = r_slots + 1;
+        S.warm_valid = 1;
+        S.warm_run = r_wrun;
+        S.flags = 0;
+        S.bc1 = bc1n;
+        S.bc2 = bc2n;
+        S.lr_a = r_lr;
+        S.iter = it;
+        S.action = ACT_STEP;
+        S.ckpt_pending = r_ckpt;
+        next_ck = r_next;
+      }
+      r_slots += 1;
+      r_iter = it;
+      act = ACT_STEP;
+      norms = r_ckpt != 0;
+      more = true;
+      lr_a = r_lr;
+      lr_b = 0.0;
+      bc1 = bc1n;
+      bc2 = bc2n;
+    }
+    SS_MARK(4)  // the controller (thread 0 and a barrier on checkpoint / flagged slots)
     if (act == ACT_NOOP) break;  // terminal: nothing of this slot is applied
     if (act == ACT_HALVE) warm = 1;  // W turns back: the last two inverses do not extrapolate
-    const bool norms = ctl.norms != 0;
-    const double lr_a = ctl.lr_a, lr_b = ctl.lr_b, bc1 = ctl.bc1, bc2 = ctl.bc2;
 
     // ---- G_obj -> Adam -> update (linear.py:248, 138-163, 275-276), or the line search's
     // revert / halving with the last step's direction recomputed from m, v (step.hip)
     double qf[NORM_FIELDS];
 #pragma unroll
     for (int f = 0; f < NORM_FIELDS; ++f) qf[f] = f == NF_WMIN ? INFINITY : 0.0;
-    if (act == ACT_STEP) {
+    if (RC && act == ACT_STEP) {
       // straight-line over the lane's E elements (selects, no per-element branches), so that
       // the four elements' division and square-root chains interleave: one wave per SIMD has no
       // other wave to hide their latency (d = 20: 3762 -> 2839 cycles a slot in this phase)
@@ -716,6 +782,43 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
       for (int e = 0; e < E; ++e) {
         if (!real[e]) continue;
         const double wo = wv[e];
+        if (act == ACT_STEP) {  // (DS = 64: per element, the form above spills there)
+          const double mt = m_entry(a[e], w32);
+          const double gs = c_zscale * z[e];
+          const double sg = sgn(wo);
+          const double gl1 = c_mu_l1 * sg;
+          const double gh = h_term(wo, mt, w32);
+          double gobj = gs + gl1;
+          gobj = gobj + gh;
+          double gi = 0.0;
+          if (has_inc) {
+            gi = minc[(int64_t)rows[e] * D + cols[e]] * sg;
+            gobj = gobj + gi;
+          }
+          const double mm = mv[e] * c_beta1 + c_c1 * gobj;
+          const double vx = vv[e] * c_beta2 + c_c2 * (gobj * gobj);
+          const double mh = mm / bc1;
+          const double vh = vx / bc2;
+          const double gd = mh / (sqrt(vh) + 1e-8);
+          double wn = wo - lr_a * gd;
+          if (w32) wn = f32r(wn);
+          if (has_exc) wn = wn * mexc[(int64_t)rows[e] * D + cols[e]];
+          mv[e] = mm;
+          vv[e] = vx;
+          wv[e] = wn;
+          if (norms) {
+            qf[NF_GOBJ] += gobj * gobj;
+            qf[NF_GSCORE] += gs * gs;
+            qf[NF_GDAG] += gh * gh;
+            qf[NF_GL1] += gl1 * gl1;
+            qf[NF_GINC] += gi * gi;
+            qf[NF_GSTEP] += gd * gd;
+            qf[NF_W2] += wn * wn;
+            qf[NF_WMAX] = fmax(qf[NF_WMAX], fabs(wn));
+            if (wn != 0.0) qf[NF_WMIN] = fmin(qf[NF_WMIN], fabs(wn));
+          }
+          continue;
+        }
         const double gd = (mv[e] / bc1) / (sqrt(vv[e] / bc2) + 1e-8);
         if (act == ACT_HALVE) {  // (float32 W: each in-place update rounds, linear.py:235, 239)
           double wn = wo + lr_a * gd;
@@ -742,7 +845,6 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
         if (lane == 0) nred[f][w] = x;
       }
     }
-    const bool more = ctl.run != 0;
     __syncthreads();
     SS_MARK(5)  // G_obj, Adam, update (and the checkpoint norms), barrier
     if (!more) break;
@@ -835,8 +937,6 @@ void launch_small_minimize(const Params* pr, State* st, double* W, double* m, do
       MIDAGMA_SMALL(32, 4, 4, false);
     else if (w32)
       MIDAGMA_SMALL(32, 4, 0, true);
-    else if (knob("MIDAGMA_EXP_SMALL_NW", 4) == 2)
-      MIDAGMA_SMALL(32, 2, 0, false);
     else
       MIDAGMA_SMALL(32, 4, 0, false);
   } else if (w32) {
