@@ -203,7 +203,20 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
 __device__ __forceinline__ double sign_of(double w) { return w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : w); }
 
 // the score partial at idx: one buffer, or split-K slices summed as sum_slices_kernel does
+// (up to 4 slices, the cov score GEMM's split at every size: the loads issue together; a loop
+// over a run-time count waited for each before the next)
 __device__ __forceinline__ double z_at(const double* __restrict__ Z, int zsplit, int64_t zstride, int64_t idx) {
+  if (zsplit <= 4) {
+    const double z0 = Z[idx];
+    const double z1 = zsplit > 1 ? Z[zstride + idx] : 0.0;
+    const double z2 = zsplit > 2 ? Z[2 * zstride + idx] : 0.0;
+    const double z3 = zsplit > 3 ? Z[3 * zstride + idx] : 0.0;
+    double acc = z0;
+    if (zsplit > 1) acc += z1;
+    if (zsplit > 2) acc += z2;
+    if (zsplit > 3) acc += z3;
+    return acc;
+  }
   double acc = Z[idx];
   for (int z = 1; z < zsplit; ++z) acc += Z[z * zstride + idx];
   return acc;
@@ -305,24 +318,32 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
   if (j >= d) return;
   const int64_t idx = i * D + j;
   if (act == ACT_STEP) {
-    const double w = W[idx];
+    // every operand load first (the optional ones behind uniform selects), then the arithmetic:
+    // with the loads among the branches the compiler waited for each before the next
+    const bool logistic = pr->logistic != 0, has_inc = pr->has_inc != 0, has_exc = pr->has_exc != 0;
+    const double w = W[idx], mtr = Mt[idx], mo = m[idx], vo = v[idx];
+    const double zs = z_at(Z, zsplit, zstride, idx);
+    const double cv = logistic ? cov[idx] : 0.0;
+    const double ci = has_inc ? minc[idx] : 0.0;
+    const double tk = trek ? trek[idx] : 0.0;
+    const double ce = has_exc ? mexc[idx] : 1.0;
     const bool w32 = pr->w32 != 0;
-    const double mt = m_entry(Mt[idx], w32);
-    double gs = pr->zscale * z_at(Z, zsplit, zstride, idx);
-    if (pr->logistic) gs = gs + pr->cscale * cov[idx];
+    const double mt = m_entry(mtr, w32);
+    double gs = pr->zscale * zs;
+    if (logistic) gs = gs + pr->cscale * cv;
     const double sg = sign_of(w);
     double gobj = gs + pr->mu_l1 * sg;
     gobj = gobj + h_term(w, mt, w32);
-    if (pr->has_inc) gobj = gobj + minc[idx] * sg;
-    if (trek) gobj = gobj + trek[idx];
-    const double mm = m[idx] * pr->beta1 + pr->c1 * gobj;
-    const double vv = v[idx] * pr->beta2 + pr->c2 * (gobj * gobj);
+    if (has_inc) gobj = gobj + ci * sg;
+    if (trek) gobj = gobj + tk;
+    const double mm = mo * pr->beta1 + pr->c1 * gobj;
+    const double vv = vo * pr->beta2 + pr->c2 * (gobj * gobj);
     const double mh = mm / st->bc1;
     const double vh = vv / st->bc2;
     const double gd = mh / (sqrt(vh) + 1e-8);
     double wn = w - st->lr_a * gd;
     if (w32) wn = f32r(wn);  // W -= lr * grad into a float32 W (linear.py:275)
-    if (pr->has_exc) wn = wn * mexc[idx];
+    if (has_exc) wn = wn * ce;
     m[idx] = mm;
     v[idx] = vv;
     W[idx] = wn;
