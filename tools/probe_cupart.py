@@ -16,7 +16,7 @@ import torch  # noqa: F401
 from midagma_amd.simulate import make_dataset
 from midagma_amd.solver import HipSolver
 
-tag = f"FORK={os.environ.get('MIDAGMA_EXP_COV_FORK', '0')} SES={os.environ.get('MIDAGMA_EXP_GEMM_SES', '0')}"
+tag = " ".join(f"{k[12:]}={os.environ[k]}" for k in sorted(os.environ) if k.startswith("MIDAGMA_EXP_")) or "product"
 for d in [int(x) for x in sys.argv[1:]] or [1000]:
     X, _, _ = make_dataset(d, 2 * d, seed=0)
     X -= X.mean(0)
