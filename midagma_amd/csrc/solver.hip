@@ -1260,6 +1260,7 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     const int64_t ktiles = s->n_pad / 64;
     int split = (int)std::max<int64_t>(1, std::min<int64_t>(ktiles / 8, (1024 + tiles - 1) / tiles));
     s->split = std::min(split, 32);
+    if (knob_set("MIDAGMA_EXP_DATA_SPLIT")) s->split = (int)knob("MIDAGMA_EXP_DATA_SPLIT", s->split);
     if (s->split > 1) s->Zparts.alloc((size_t)s->split * D * D);
     s->loss_part_count = (s->n_pad / 64) * (D / 64);
     // small shards run the cov-mode slot structure: the warm-started fast blocked inverse in
