@@ -45,13 +45,34 @@ __global__ __launch_bounds__(NTHREADS) void mlp_tail_fwd_kernel(const double* __
   extern __shared__ double sw[];  // d m1 products, then the reduction scratch
   const int64_t row = blockIdx.x, dm = d * m1;
   const double* z = Z + row * dm;
-  for (int64_t c = threadIdx.x; c < dm; c += NTHREADS) sw[c] = sigmoid(b1 ? z[c] + b1[c] : z[c]) * w2[c];
+  // (thread j < d: its b2 and X entries loaded ahead of the staging, not after its barrier)
+  const int64_t j0 = threadIdx.x;
+  const double b2j = j0 < d ? b2[j0] : 0.0, xj = j0 < d ? X[row * d + j0] : 0.0;
+  // the row's operands in groups of SU per thread, every load of a group issued before its
+  // arithmetic (a loop of load-then-use waited out one memory round trip per column)
+  constexpr int SU = 8;
+  for (int64_t c0 = threadIdx.x; c0 < dm; c0 += SU * NTHREADS) {
+    double zv[SU], bv[SU], wv[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int64_t c = c0 + u * NTHREADS;
+      const bool ok = c < dm;
+      zv[u] = ok ? z[c] : 0.0;
+      bv[u] = ok && b1 ? b1[c] : 0.0;
+      wv[u] = ok ? w2[c] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int64_t c = c0 + u * NTHREADS;
+      if (c < dm) sw[c] = sigmoid(b1 ? zv[u] + bv[u] : zv[u]) * wv[u];
+    }
+  }
   __syncthreads();
   double r2 = 0.0;
   for (int64_t j = threadIdx.x; j < d; j += NTHREADS) {
     double acc = 0.0;
     for (int m = 0; m < m1; ++m) acc += sw[j * m1 + m];
-    const double r = (acc + b2[j]) - X[row * d + j];
+    const double r = (acc + (j == j0 ? b2j : b2[j])) - (j == j0 ? xj : X[row * d + j]);
     R[row * d + j] = r;
     r2 += r * r;
   }
@@ -101,6 +122,26 @@ __global__ __launch_bounds__(NTHREADS) void mlp_tail_bwd_kernel(const double* __
                                                                 double* __restrict__ pw, double* __restrict__ pb,
                                                                 double* __restrict__ pz, ObjGrad og) {
   const int64_t dm = d * m1;
+  const int64_t c = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  const bool live = c < dm;
+  const int64_t j = live ? c / m1 : 0;
+  const int m = live ? (int)(c % m1) : 0;
+  const int64_t r0 = (int64_t)blockIdx.y * TAIL_ROWS, r1 = r0 + TAIL_ROWS < n ? r0 + TAIL_ROWS : n;
+  // a whole chunk's R and Z loads are issued first, ahead of the objective's reduction below and
+  // of any arithmetic (in groups of 8 rows the loop waited out four memory round trips)
+  const bool full = r1 - r0 == TAIL_ROWS;
+  double rv[TAIL_ROWS], zv[TAIL_ROWS];
+  double w = 0.0, bias = 0.0;
+  if (live) {
+    w = w2[c];
+    bias = b1 ? b1[c] : 0.0;
+    if (full)
+#pragma unroll
+      for (int u = 0; u < TAIL_ROWS; ++u) {
+        rv[u] = R[(r0 + u) * d + j];
+        zv[u] = Z[(r0 + u) * dm + c];
+      }
+  }
   double gs;
   if (og.part) {  // every workgroup reduces the partials (before any thread leaves)
     __shared__ double red[NTHREADS];
@@ -108,43 +149,30 @@ __global__ __launch_bounds__(NTHREADS) void mlp_tail_bwd_kernel(const double* __
   } else {
     gs = g[0];
   }
-  const int64_t c = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
-  if (c >= dm) return;
-  const int64_t j = c / m1;
-  const int m = (int)(c % m1);
-  const double w = w2[c], g2 = 2.0 * gs, bias = b1 ? b1[c] : 0.0;
-  const int64_t r0 = (int64_t)blockIdx.y * TAIL_ROWS, r1 = r0 + TAIL_ROWS < n ? r0 + TAIL_ROWS : n;
+  if (!live) return;
+  const double g2 = 2.0 * gs;
   double aw = 0.0, ab = 0.0, az = 0.0;
-  // rows in groups of 8 with every load of the group issued first (the loop was one dependent
-  // load round trip per row); the partial sums keep the row order
-  constexpr int U = 8;
-  int64_t row = r0;
-  for (; row + U <= r1; row += U) {
-    double rv[U], zv[U];
+  if (full) {  // (the partial sums keep the row order)
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      rv[u] = R[(row + u) * d + j];
-      zv[u] = Z[(row + u) * dm + c];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < TAIL_ROWS; ++u) {
       const double dxh = g2 * rv[u];
       const double s = sigmoid(b1 ? zv[u] + bias : zv[u]);
       const double dz = dxh * w * (s * (1.0 - s));
-      dZ[(row + u) * dm + c] = dz;
+      dZ[(r0 + u) * dm + c] = dz;
       aw += dxh * s;
       ab += dxh;
       az += dz;
     }
-  }
-  for (; row < r1; ++row) {
-    const double dxh = g2 * R[row * d + j];
-    const double s = sigmoid(b1 ? Z[row * dm + c] + bias : Z[row * dm + c]);
-    const double dz = dxh * w * (s * (1.0 - s));
-    dZ[row * dm + c] = dz;
-    aw += dxh * s;
-    ab += dxh;
-    az += dz;
+  } else {
+    for (int64_t row = r0; row < r1; ++row) {
+      const double dxh = g2 * R[row * d + j];
+      const double s = sigmoid(b1 ? Z[row * dm + c] + bias : Z[row * dm + c]);
+      const double dz = dxh * w * (s * (1.0 - s));
+      dZ[row * dm + c] = dz;
+      aw += dxh * s;
+      ab += dxh;
+      az += dz;
+    }
   }
   pw[(int64_t)blockIdx.y * dm + c] = aw;
   if (m == 0) pb[(int64_t)blockIdx.y * d + j] = ab;
