@@ -118,6 +118,36 @@ def test_small_path_launch_boundaries_bit_identical(d):
     b.close()
 
 
+@pytest.mark.parametrize("d", [20, 48])
+def test_small_path_unaligned_launches_bit_identical(d):
+    """run_slots in chunks of 37 with checkpoint = 50 and max_iter = 333 (not a multiple of it):
+    launches start mid-interval, so the next checkpoint iteration each launch derives from the
+    State (small.hip's next_ck) and the plain steps decided from register copies of the State must
+    agree with one minimize call, bit for bit, including the final non-multiple checkpoint."""
+    o = _oracle(d)
+    K = 333
+    a = _solver(d, o.cov)
+    Wa = np.zeros((d, d))
+    ra = a.minimize(Wa, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=50, want_checkpoints=True)
+    b = _solver(d, o.cov)
+    b.begin(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=50)
+    for _ in range(K // 37 + 3):
+        b.run_slots(37)
+    Wb = np.zeros((d, d))
+    rb = b.end(Wb)
+    cb = b.checkpoints()
+    assert rb.iters == ra.iters == K
+    assert [c.iter for c in cb] == [c.iter for c in ra.checkpoints] == list(range(50, K, 50)) + [K]
+    assert np.array_equal(Wa, Wb)
+    for x, y in zip(ra.checkpoints, cb):
+        for f in REC_FIELDS:
+            assert getattr(x, f) == getattr(y, f), (x.iter, f)
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    assert np.abs(Wa - Wr).max() <= 1e-9
+    a.close()
+    b.close()
+
+
 def test_small_path_long_trajectory_d20(golden, parity):
     """10000 steps at d=20 against the reference's own trajectory (traj_d20.npz): ~9990
     product-form slots between the Gauss-Jordan checkpoint slots."""
