@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 8
+#define MIDAGMA_ABI_VERSION 9
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -300,6 +300,18 @@ int midagma_mlp_tail_bwd_obj(const double* Z, const double* b1, const double* w2
                              void* stream);
 int midagma_fc1_terms_bwd_obj(const double* W1, int64_t d, int64_t m1, const double* gA, const double* gobj, double mu,
                               double lambda1, const double* lin, int64_t nlin, double* dW1, void* stream);
+/* ABI 9: one replayed DagmaNonlinear step of a [d, m1, 1] model closed in one launch
+ * (nonlinear.py:198-236): the tail's dw2 / db2 / db1 sums from the chunk partials that
+ * midagma_mlp_tail_bwd_obj leaves in scratch when dw2 = db2 = db1 = NULL, fc1's weight gradient
+ * (midagma_fc1_terms_bwd_obj's arithmetic), the gated table Adam step of the four parameters
+ * (params / exp_avg / exp_avg_sq: fc1.weight, fc1.bias, fc2.weight, fc2.bias;
+ * midagma_adam_step_table_multi's arithmetic) and the next step's fc1 terms (A, l1part as
+ * midagma_fc1_terms computes them, from the updated weights).  Bit-identical to those launches. */
+int midagma_mlp_step(double* const* params, double* const* exp_avg, double* const* exp_avg_sq, int64_t n, int64_t d,
+                     int64_t m1, const double* gA, const double* gobj, double mu, double lambda1, const double* lin,
+                     int64_t nlin, const double* scratch, const double* table, const int64_t* counter, double w1,
+                     double beta2, double c2, double eps, double wd, const double* gate, double* A, double* l1part,
+                     void* stream);
 int midagma_mlp_objective(const double* ssq, const double* l1part, int64_t np, const double* h, double mu,
                           double lambda1, double half_d, double inv_n, double* obj, void* stream);
 int midagma_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, double mu, double lambda1, double half_d,

@@ -121,6 +121,8 @@ EXPORTED = {
     "midagma_mlp_tail_bwd_obj": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _d, _d, _d, _i64, _i64, _i64, _vp, _vp, _vp,
                                         _vp, _vp, _vp]),
     "midagma_fc1_terms_bwd_obj": (_int, [_vp, _i64, _i64, _vp, _vp, _d, _d, _vp, _i64, _vp, _vp]),
+    "midagma_mlp_step": (_int, [C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), _i64, _i64, _i64, _vp, _vp, _d, _d,
+                                _vp, _i64, _vp, _vp, _vp, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp]),
     "midagma_mlp_tail_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "midagma_mlp_tail_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
 }

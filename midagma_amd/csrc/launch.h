@@ -309,7 +309,8 @@ void launch_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, co
 void launch_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R, const double* g,
                          int64_t n, int64_t d, int m1, double* dZ, double* dw2, double* db2, double* db1,
                          double* scratch, hipStream_t stream, const double* part = nullptr,
-                         const double* gobj = nullptr, double mu = 0.0, double half_d = 0.0, double inv_n = 0.0);
+                         const double* gobj = nullptr, double mu = 0.0, double half_d = 0.0, double inv_n = 0.0,
+                         bool sums = true);
 
 // fc1 terms of the [d, m1, 1] DagmaMLP: A[i, j] = sum_m W1[j m1 + m, i]^2, |W1| partial sums
 // (fc1_terms_parts(d) of them); backward dW1 = 2 W1 gA^T + gl1part sign(W1)
@@ -345,6 +346,16 @@ void launch_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, do
                               double inv_n, double* gssq, double* gl1part, double* gh, hipStream_t stream);
 
 // --- adam.hip ---------------------------------------------------------------
+// the [d, m1, 1] DagmaMLP step's closing launch (mlp.hip mlp_step_kernel): the tail's dw sums, fc1's
+// weight gradient, Adam over the four parameters and the next step's fc1 terms
+struct MlpStepPtrs {
+  double *W1, *b1, *w2, *b2;
+  double *mW1, *vW1, *mb1, *vb1, *mw2, *vw2, *mb2, *vb2;
+};
+void launch_mlp_step(const MlpStepPtrs& p, int64_t n, int64_t d, int m1, const double* gA, const double* gobj,
+                     double mu, double lambda1, const double* lin, int nlin, const double* scratch,
+                     const double* table, const int64_t* counter, double w1, double beta2, double c2, double eps,
+                     double wd, const double* gate, double* A, double* l1part, hipStream_t stream);
 struct AdamCoef {  // host-rounded as torch.optim.Adam computes them in Python floats
   double step_size, w1, beta2, c2, bc2_sqrt, eps, wd;
 };

@@ -232,14 +232,19 @@ void launch_mlp_tail_fwd(const double* Z, const double* b1, const double* w2, co
 void launch_mlp_tail_bwd(const double* Z, const double* b1, const double* w2, const double* R, const double* g,
                          int64_t n, int64_t d, int m1, double* dZ, double* dw2, double* db2, double* db1,
                          double* scratch, hipStream_t stream, const double* part, const double* gobj, double mu,
-                         double half_d, double inv_n) {
+                         double half_d, double inv_n, bool sums) {
   const int64_t dm = d * m1, chunks = (n + TAIL_ROWS - 1) / TAIL_ROWS;
   double* pw = scratch;
   double* pb = scratch + chunks * dm;
-  double* pz = db1 ? pb + chunks * d : nullptr;
+  // (sums == false: the partials only, b1's too, for launch_mlp_step to sum)
+  double* pz = db1 || (!sums && b1) ? pb + chunks * d : nullptr;
   hipLaunchKernelGGL(mlp_tail_bwd_kernel, dim3((unsigned)((dm + NTHREADS - 1) / NTHREADS), (unsigned)chunks),
                      dim3(NTHREADS), 0, stream, Z, b1, w2, R, g, n, d, m1, dZ, pw, pb, pz,
                      ObjGrad{part, n, gobj, mu, half_d, inv_n});
+  if (!sums) {
+    HIP_TRY(hipGetLastError());
+    return;
+  }
   const int64_t cols = dm + d + (db1 ? dm : 0);
   hipLaunchKernelGGL(mlp_tail_dw_kernel, dim3((unsigned)((cols + NTHREADS - 1) / NTHREADS)), dim3(NTHREADS), 0,
                      stream, pw, pb, pz, chunks, d, m1, dw2, db2, db1);
@@ -400,6 +405,195 @@ __global__ __launch_bounds__(NTHREADS) void mlp_objective_bwd_kernel(const doubl
   }
 }
 
+// One torch-Adam step of a [d, m1, 1] DagmaMLP's four parameters in one launch, closing the step
+// (DagmaNonlinear.minimize, nonlinear.py:198-236; BASELINE config 5).  It does the work of four
+// launches with their arithmetic unchanged:
+//   - mlp_tail_dw: the gradients of fc2's weight and bias and fc1's bias from the tail backward's
+//     chunk partials;
+//   - fc1_terms_bwd_elem: fc1's weight gradient;
+//   - adam_gated_table_multi: the Adam update of all four tensors;
+//   - the next step's fc1_terms: A = sum_m fc1^2 and the |fc1| partials of the updated weights.
+// Workgroups [0, nA) hold the (j, i) pairs of fc1_terms' grid (so the l1 partials are the same sums
+// in the same order); each thread walks its m1 weights.  The rest hold b1, w2 and b2 elementwise.
+// Gated off (*gate < 0) nothing moves, and A and l1part come from the weights as they are.
+struct MlpStepArgs {
+  double *W1, *b1, *w2, *b2;
+  double *mW1, *vW1, *mb1, *vb1, *mw2, *vw2, *mb2, *vb2;
+  int64_t d, m1, nchunk;
+  const double *gA, *gobj;
+  double mu, lambda1;
+  const double* lin;
+  int nlin, nA;
+  const double *pw, *pb, *pz;
+  const double* table;
+  const int64_t* counter;
+  double w1, beta2, c2, eps, wd;
+  const double* gate;
+  double *A, *l1part;
+};
+
+// adam_gated_table_multi_kernel's element update
+__device__ __forceinline__ double adam_elem(double pi, double& m, double& v, double gi, const MlpStepArgs& a,
+                                            double step_size, double bc2_sqrt) {
+  if (a.wd != 0.0) gi = gi + a.wd * pi;
+  const double mi = m + a.w1 * (gi - m);
+  const double vi = v * a.beta2 + a.c2 * gi * gi;
+  const double denom = sqrt(vi) / bc2_sqrt + a.eps;
+  m = mi;
+  v = vi;
+  return pi + (-step_size) * mi / denom;
+}
+
+// mlp_tail_dw_kernel's fixed-order sum of the chunk partials of one column (up to 32 chunks: every
+// load first, then the same four chains)
+__device__ __forceinline__ double chunk_sum(const double* __restrict__ src, int64_t stride, int64_t nchunk) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  constexpr int KU = 32;
+  if (nchunk <= KU) {
+    double x[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) x[u] = u < nchunk ? src[u * stride] : 0.0;
+#pragma unroll
+    for (int u = 0; u + 4 <= KU; u += 4)
+      if (u + 4 <= nchunk) {
+        a0 += x[u];
+        a1 += x[u + 1];
+        a2 += x[u + 2];
+        a3 += x[u + 3];
+      }
+#pragma unroll
+    for (int u = 0; u < KU; ++u)
+      if (u >= nchunk / 4 * 4 && u < nchunk) a0 += x[u];
+    return (a0 + a1) + (a2 + a3);
+  }
+  int64_t k = 0;
+  for (; k + 4 <= nchunk; k += 4) {
+    a0 += src[k * stride];
+    a1 += src[(k + 1) * stride];
+    a2 += src[(k + 2) * stride];
+    a3 += src[(k + 3) * stride];
+  }
+  for (; k < nchunk; ++k) a0 += src[k * stride];
+  return (a0 + a1) + (a2 + a3);
+}
+
+__global__ __launch_bounds__(NTHREADS) void mlp_step_kernel(MlpStepArgs a) {
+  __shared__ double red[NTHREADS];
+  const bool go = !(a.gate && !(*a.gate >= 0.0));
+  double step_size = 0.0, bc2_sqrt = 1.0;
+  if (go) {
+    const int64_t t = *a.counter;
+    step_size = a.table[2 * t];
+    bc2_sqrt = a.table[2 * t + 1];
+  }
+  const int64_t d = a.d, m1 = a.m1, dm = d * m1;
+  if ((int)blockIdx.x < a.nA) {
+    const int64_t tt = (int64_t)blockIdx.x * NTHREADS + threadIdx.x, dd = dm * d;
+    double al = 0.0;
+    if (tt < d * d) {
+      const int64_t j = tt / d, i = tt % d;
+      const double g0 = a.gobj[0];
+      const double ga = g0 * a.gA[i * d + j];
+      const double gl = (g0 * a.mu) * a.lambda1;
+      double acc = 0.0;
+      constexpr int MU = 16, LU = 4;
+      if (m1 <= MU && a.nlin <= LU) {
+        // (every load of the thread's m1 weights first: a loop of load, update, store waited out
+        // one memory round trip per weight)
+        double wv[MU], mv[MU], vv[MU], lv[LU][MU];
+#pragma unroll
+        for (int m = 0; m < MU; ++m) {
+          const int64_t e = (j * m1 + m) * d + i;
+          const bool ok = m < m1;
+          wv[m] = ok ? a.W1[e] : 0.0;
+          mv[m] = ok && go ? a.mW1[e] : 0.0;
+          vv[m] = ok && go ? a.vW1[e] : 0.0;
+#pragma unroll
+          for (int q = 0; q < LU; ++q) lv[q][m] = ok && go && q < a.nlin ? a.lin[q * dd + e] : 0.0;
+        }
+#pragma unroll
+        for (int m = 0; m < MU; ++m) {
+          if (m >= m1) break;
+          const int64_t e = (j * m1 + m) * d + i;
+          const double w = wv[m];
+          double pn = w;
+          if (go) {
+            const double sg = w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : 0.0);
+            double g = ga * (2.0 * w) + gl * sg;
+            if (a.nlin > 0) {
+              double s = lv[0][m];
+#pragma unroll
+              for (int q = 1; q < LU; ++q)
+                if (q < a.nlin) s += lv[q][m];
+              g = s + g;
+            }
+            double mm = mv[m], vq = vv[m];
+            pn = adam_elem(w, mm, vq, g, a, step_size, bc2_sqrt);
+            a.mW1[e] = mm;
+            a.vW1[e] = vq;
+            a.W1[e] = pn;
+          }
+          acc += pn * pn;
+          al += fabs(pn);
+        }
+      } else {
+        for (int64_t m = 0; m < m1; ++m) {
+          const int64_t e = (j * m1 + m) * d + i;
+          const double w = a.W1[e];
+          double pn = w;
+          if (go) {
+            const double sg = w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : 0.0);
+            double g = ga * (2.0 * w) + gl * sg;
+            if (a.nlin > 0) {
+              double s = a.lin[e];
+              for (int q = 1; q < a.nlin; ++q) s += a.lin[q * dd + e];
+              g = s + g;
+            }
+            double mm = a.mW1[e], vq = a.vW1[e];
+            pn = adam_elem(w, mm, vq, g, a, step_size, bc2_sqrt);
+            a.mW1[e] = mm;
+            a.vW1[e] = vq;
+            a.W1[e] = pn;
+          }
+          acc += pn * pn;
+          al += fabs(pn);
+        }
+      }
+      a.A[i * d + j] = acc;
+    }
+    red[threadIdx.x] = al;
+    __syncthreads();
+    for (int s = NTHREADS / 2; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) a.l1part[blockIdx.x] = red[0];
+    return;
+  }
+  if (!go) return;
+  // b1 (the partials pz), w2 (pw), b2 (pb): mlp_tail_dw's sums, then the Adam update
+  const int64_t c = (int64_t)(blockIdx.x - a.nA) * NTHREADS + threadIdx.x;
+  double *p, *m, *v;
+  double g;
+  int64_t k;
+  if (c < dm) {
+    k = c, p = a.b1, m = a.mb1, v = a.vb1;
+    g = chunk_sum(a.pz + k, dm, a.nchunk);
+  } else if (c < 2 * dm) {
+    k = c - dm, p = a.w2, m = a.mw2, v = a.vw2;
+    g = chunk_sum(a.pw + k, dm, a.nchunk);
+  } else if (c < 2 * dm + d) {
+    k = c - 2 * dm, p = a.b2, m = a.mb2, v = a.vb2;
+    g = chunk_sum(a.pb + k, d, a.nchunk);
+  } else {
+    return;
+  }
+  double mm = m[k], vv = v[k];
+  p[k] = adam_elem(p[k], mm, vv, g, a, step_size, bc2_sqrt);
+  m[k] = mm;
+  v[k] = vv;
+}
+
 }  // namespace
 
 int64_t fc1_terms_parts(int64_t d) { return (d * d + NTHREADS - 1) / NTHREADS; }
@@ -407,6 +601,27 @@ int64_t fc1_terms_parts(int64_t d) { return (d * d + NTHREADS - 1) / NTHREADS; }
 void launch_fc1_terms(const double* W1, int64_t d, int m1, double* A, double* l1part, hipStream_t stream) {
   hipLaunchKernelGGL(fc1_terms_kernel, dim3((unsigned)fc1_terms_parts(d)), dim3(NTHREADS), 0, stream, W1, d, m1, A,
                      l1part);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_mlp_step(const MlpStepPtrs& p, int64_t n, int64_t d, int m1, const double* gA, const double* gobj,
+                     double mu, double lambda1, const double* lin, int nlin, const double* scratch,
+                     const double* table, const int64_t* counter, double w1, double beta2, double c2, double eps,
+                     double wd, const double* gate, double* A, double* l1part, hipStream_t stream) {
+  const int64_t dm = d * m1, nchunk = (n + TAIL_ROWS - 1) / TAIL_ROWS;
+  MlpStepArgs a{};
+  a.W1 = p.W1, a.b1 = p.b1, a.w2 = p.w2, a.b2 = p.b2;
+  a.mW1 = p.mW1, a.vW1 = p.vW1, a.mb1 = p.mb1, a.vb1 = p.vb1, a.mw2 = p.mw2, a.vw2 = p.vw2, a.mb2 = p.mb2,
+  a.vb2 = p.vb2;
+  a.d = d, a.m1 = m1, a.nchunk = nchunk;
+  a.gA = gA, a.gobj = gobj, a.mu = mu, a.lambda1 = lambda1, a.lin = lin, a.nlin = nlin;
+  a.nA = (int)fc1_terms_parts(d);
+  // the tail backward's partials (launch_mlp_tail_bwd's layout: pw, pb, pz)
+  a.pw = scratch, a.pb = scratch + nchunk * dm, a.pz = a.pb + nchunk * d;
+  a.table = table, a.counter = counter, a.w1 = w1, a.beta2 = beta2, a.c2 = c2, a.eps = eps, a.wd = wd;
+  a.gate = gate, a.A = A, a.l1part = l1part;
+  const int64_t nsmall = (2 * dm + d + NTHREADS - 1) / NTHREADS;
+  hipLaunchKernelGGL(mlp_step_kernel, dim3((unsigned)(a.nA + nsmall)), dim3(NTHREADS), 0, stream, a);
   HIP_TRY(hipGetLastError());
 }
 

@@ -2284,12 +2284,33 @@ extern "C" int midagma_mlp_tail_bwd_obj(const double* Z, const double* b1, const
                                         const double* part, const double* gobj, double mu, double half_d,
                                         double inv_n, int64_t n, int64_t d, int64_t m1, double* dZ, double* dw2,
                                         double* db2, double* db1, double* scratch, void* stream) {
-  if (!Z || !w2 || !R || !part || !gobj || !dZ || !dw2 || !db2 || !scratch || n < 1 || d < 1 || m1 < 1 ||
-      d * m1 > MLP_TAIL_MAX_DM)
+  // (ABI 9: dw2 = db2 = db1 = NULL leaves the chunk partials in scratch for midagma_mlp_step)
+  const bool sums = dw2 || db2 || db1;
+  if (!Z || !w2 || !R || !part || !gobj || !dZ || (sums && (!dw2 || !db2)) || !scratch || n < 1 || d < 1 ||
+      m1 < 1 || d * m1 > MLP_TAIL_MAX_DM)
     return fail(nullptr, MIDAGMA_E_ARG, "mlp_tail_bwd_obj: bad arguments");
   return guarded(nullptr, [&] {
     launch_mlp_tail_bwd(Z, b1, w2, R, nullptr, n, d, (int)m1, dZ, dw2, db2, db1, scratch,
-                        reinterpret_cast<hipStream_t>(stream), part, gobj, mu, half_d, inv_n);
+                        reinterpret_cast<hipStream_t>(stream), part, gobj, mu, half_d, inv_n, sums);
+    return MIDAGMA_OK;
+  });
+}
+
+extern "C" int midagma_mlp_step(double* const* params, double* const* exp_avg, double* const* exp_avg_sq, int64_t n,
+                                int64_t d, int64_t m1, const double* gA, const double* gobj, double mu,
+                                double lambda1, const double* lin, int64_t nlin, const double* scratch,
+                                const double* table, const int64_t* counter, double w1, double beta2, double c2,
+                                double eps, double wd, const double* gate, double* A, double* l1part, void* stream) {
+  if (!params || !exp_avg || !exp_avg_sq || !gA || !gobj || !scratch || !table || !counter || !A || !l1part ||
+      n < 1 || d < 1 || m1 < 1 || d * m1 > MLP_TAIL_MAX_DM || nlin < 0 || (nlin > 0 && !lin))
+    return fail(nullptr, MIDAGMA_E_ARG, "mlp_step: bad arguments");
+  for (int q = 0; q < 4; ++q)
+    if (!params[q] || !exp_avg[q] || !exp_avg_sq[q]) return fail(nullptr, MIDAGMA_E_ARG, "mlp_step: bad tensor");
+  const MlpStepPtrs p{params[0], params[1], params[2], params[3], exp_avg[0], exp_avg_sq[0], exp_avg[1],
+                      exp_avg_sq[1], exp_avg[2], exp_avg_sq[2], exp_avg[3], exp_avg_sq[3]};
+  return guarded(nullptr, [&] {
+    launch_mlp_step(p, n, d, (int)m1, gA, gobj, mu, lambda1, lin, (int)nlin, scratch, table, counter, w1, beta2, c2,
+                    eps, wd, gate, A, l1part, reinterpret_cast<hipStream_t>(stream));
     return MIDAGMA_OK;
   });
 }

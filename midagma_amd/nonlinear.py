@@ -154,7 +154,7 @@ class _MLPObjective(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, X, W1, b1, w2, b2, d: int, m1: int, s: float, mu: float, lambda1: float,
-                overlap: bool = False, ld=None, exact: bool = True, counter=None):
+                overlap: bool = False, ld=None, exact: bool = True, counter=None, step=None):
         L = _lib.lib()
         dev = X.device
         X, W1, b1, w2, b2 = X.contiguous(), W1.contiguous(), b1.contiguous(), w2.contiguous(), b2.contiguous()
@@ -167,8 +167,12 @@ class _MLPObjective(torch.autograd.Function):
         # fused: fc1's GEMM and the tail forward in one MFMA launch (midagma_mlp_fc1_tail_fwd), Z then
         # holds sigmoid(X W1^T + b1) (what the fused backward reads), else fc1's pre-activation X W1^T
         Z = torch.empty((n, d * m1), **f64) if fused else X @ W1.t()
-        A = torch.empty((d, d), **f64)
-        l1part = torch.empty(int(L.midagma_fc1_terms_parts(d)), **f64)
+        if step is not None and fused:
+            raise _lib.HipSolverError("the one-launch step (_MlpStep) runs on the product tail, not the fused MFMA one")
+        # step (_MlpStep): the fc1 terms of the current weights were left by the last step's closing
+        # launch (midagma_mlp_step), which also takes this step's backward, Adam and next terms
+        A = step.A if step is not None else torch.empty((d, d), **f64)
+        l1part = step.l1part if step is not None else torch.empty(int(L.midagma_fc1_terms_parts(d)), **f64)
         Mt = torch.empty((d, d), **f64)
         h = torch.empty((), **f64)
         R = torch.empty_like(X)
@@ -178,7 +182,8 @@ class _MLPObjective(torch.autograd.Function):
         ctr = _vp(counter) if counter is not None else None
         ctx.chain = None
         with torch.cuda.device(dev):
-            _lib.check(L.midagma_fc1_terms(_vp(W1), d, m1, _vp(A), _vp(l1part), st), None, "fc1_terms")
+            if step is None:
+                _lib.check(L.midagma_fc1_terms(_vp(W1), d, m1, _vp(A), _vp(l1part), st), None, "fc1_terms")
             if overlap:
                 # The log-det chain (latency-bound) depends on fc1 only: it runs on a side stream
                 # beside the tail forward and the backward up to the weight gradient, which never
@@ -216,6 +221,8 @@ class _MLPObjective(torch.autograd.Function):
         ctx.save_for_backward(X, W1, b1, w2, Z, R, Mt, part, scratch)
         ctx.consts = (n, d, m1, float(mu), float(lambda1), l1part.numel())
         ctx.fused = fused
+        ctx.step = step
+        ctx.h = h if step is not None else None  # (the step's default Adam gate: h >= 0)
         ctx.set_materialize_grads(False)  # h's own gradient stays None (no zero fill and add)
         return h, obj
 
@@ -249,9 +256,14 @@ class _MLPObjective(torch.autograd.Function):
                     chain.enqueue(2)
             else:
                 dZ = torch.empty_like(Z)
+                step = ctx.step
+                # (step: the chunk partials only; midagma_mlp_step sums them)
                 _lib.check(L.midagma_mlp_tail_bwd_obj(_vp(Z), _vp(b1), _vp(w2), _vp(R), _vp(part), _vp(g), mu,
-                                                      0.5 * d, 1 / n, n, d, m1, _vp(dZ), _vp(dw2), _vp(db2),
-                                                      _vp(db1), _vp(scratch), st), None, "mlp_tail_bwd_obj")
+                                                      0.5 * d, 1 / n, n, d, m1, _vp(dZ),
+                                                      None if step is not None else _vp(dw2),
+                                                      None if step is not None else _vp(db2),
+                                                      None if step is not None else _vp(db1), _vp(scratch), st),
+                           None, "mlp_tail_bwd_obj")
                 if chain is not None:
                     chain.enqueue(2)
                 ks = LIN_SPLIT
@@ -265,6 +277,12 @@ class _MLPObjective(torch.autograd.Function):
             if chain is not None:  # the rest of the chain and the objective, then join
                 torch.cuda.current_stream(dev).wait_event(chain.finish())
                 ctx.chain = None
+            if ctx.step is not None:
+                if gh_out is not None:
+                    raise _lib.HipSolverError("the one-launch step takes d obj only (h's gradient is not an input)")
+                ctx.step.close_step(Mt, g, mu, lambda1, lin, nlin, scratch, n, ctx.h, st)
+                ctx.step, ctx.h = None, None
+                return (None,) * 15
             if gh_out is None:
                 _lib.check(L.midagma_fc1_terms_bwd_obj(_vp(W1), d, m1, _vp(Mt), _vp(g), mu, lambda1, _vp(lin), nlin,
                                                        _vp(dW1), st), None, "fc1_terms_bwd_obj")
@@ -276,10 +294,52 @@ class _MLPObjective(torch.autograd.Function):
                 gh = gh + gh_out
                 _lib.check(L.midagma_fc1_terms_bwd(_vp(W1), d, m1, _vp(Mt), _vp(gh), _vp(gl1), _vp(lin), nlin,
                                                    _vp(dW1), st), None, "fc1_terms_bwd")
-        return None, dW1, db1, dw2, db2, None, None, None, None, None, None, None, None, None
+        return None, dW1, db1, dw2, db2, None, None, None, None, None, None, None, None, None, None
 
 
 _SIDE: dict = {}
+
+
+class _MlpStep:
+    """The replayed DagmaNonlinear step of a [d, m1, 1] model closed by one launch
+    (midagma_mlp_step, ABI 9): the tail's parameter-gradient sums, fc1's weight gradient, torch
+    Adam over the four parameters (nonlinear.py:212-236) and the next step's fc1 terms, whose A and
+    |fc1| partials the next forward then takes instead of launching fc1_terms.  Bit-identical to
+    the separate launches (mlp_tail_dw, fc1_terms_bwd, adam_gated_table_multi, fc1_terms); the
+    parameters' .grad stay None."""
+
+    def __init__(self, L, model, params, exp_avg, exp_avg_sq, table, counter, beta1, beta2, eps, wd):
+        fc = model.fc2[0]
+        want = [model.fc1.weight, model.fc1.bias, fc.weight, fc.bias]
+        if len(params) != 4 or any(p is not q for p, q in zip(params, want)):
+            raise ValueError("_MlpStep: the parameters must be fc1.weight, fc1.bias, fc2.weight, fc2.bias")
+        self.L, self.d, self.m1 = L, model.d, model.dims[1]
+        arr = lambda ts: (C.c_void_p * 4)(*[C.c_void_p(t.data_ptr()) for t in ts])  # noqa: E731
+        self.keep = (params, exp_avg, exp_avg_sq, table, counter)
+        self.p, self.m, self.v = arr(params), arr(exp_avg), arr(exp_avg_sq)
+        self.table, self.counter = table, counter
+        self.coef = (1 - beta1, beta2, 1 - beta2, eps, wd)
+        dev = params[0].device
+        self.A = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
+        self.l1part = torch.empty(int(L.midagma_fc1_terms_parts(self.d)), dtype=torch.float64, device=dev)
+        self.gate = None  # None: this step's h (the reference's h < 0 exit); else a tensor (< 0: no step)
+        self.refresh()
+
+    def refresh(self):
+        """A and the |fc1| partials of the current weights (before the first step of a call)."""
+        W1 = self.keep[0][0]
+        stream = torch.cuda.current_stream(W1.device).cuda_stream
+        with torch.cuda.device(W1.device):
+            _lib.check(self.L.midagma_fc1_terms(_vp(W1), self.d, self.m1, _vp(self.A), _vp(self.l1part),
+                                                C.c_void_p(stream) if stream else None), None, "fc1_terms")
+
+    def close_step(self, Mt, g, mu, lambda1, lin, nlin, scratch, n, h, st):
+        gate = h if self.gate is None else self.gate
+        w1, beta2, c2, eps, wd = self.coef
+        _lib.check(self.L.midagma_mlp_step(self.p, self.m, self.v, n, self.d, self.m1, _vp(Mt), _vp(g), mu, lambda1,
+                                           _vp(lin), nlin, _vp(scratch), _vp(self.table), _vp(self.counter), w1,
+                                           beta2, c2, eps, wd, _vp(gate), _vp(self.A), _vp(self.l1part), st), None,
+                   "mlp_step")
 
 
 class _SideLogdet:
@@ -502,7 +562,7 @@ class DagmaNonlinear:
         return 0.5 * d * torch.log(1 / n * torch.sum((output - target) ** 2))
 
     def _h_and_objective(self, mu: float, lambda1: float, s: float, overlap: bool = False, ld=None,
-                         exact: bool = True, counter=None):
+                         exact: bool = True, counter=None, step=None):
         """(h, mu * (score + lambda1 * |fc1|_1) + h) (nonlinear.py:198-204): for a [d, m1, 1] MLP
         on the GPU through the fused kernels (fc1 terms, log-det, tail, scalar objective),
         otherwise the reference's expressions."""
@@ -512,7 +572,7 @@ class DagmaNonlinear:
             m1 = m.dims[1]
             fc = m.fc2[0]
             return _MLPObjective.apply(self.X, m.fc1.weight, m.fc1.bias, fc.weight, fc.bias, d, m1, s, mu, lambda1,
-                                       overlap, ld, exact, counter)
+                                       overlap, ld, exact, counter, step)
         h_val = m.h_func(s)
         return h_val, mu * (self._score() + lambda1 * m.fc1_l1_reg()) + h_val
 
@@ -610,13 +670,23 @@ class DagmaNonlinear:
 
         seed = torch.ones((), dtype=torch.float64, device=dev)  # d obj / d obj: no fill node per step
         ld = self._ldfast(dev)
+        # the step closed by one launch (_MlpStep; MIDAGMA_NO_MLP_STEP=1: the separate launches)
+        step = None
+        if fused and not FUSED_TAIL and not os.environ.get("MIDAGMA_NO_MLP_STEP"):
+            with torch.no_grad():
+                step = _MlpStep(L, self.model, params, exp_avg, exp_avg_sq, table_d, counter, beta1, beta2, eps,
+                                wd)
 
         def body(gate, exact=True):
             for p in params:
                 p.grad = None
+            if step is not None:
+                step.gate = gate
             h_val, obj = self._h_and_objective(mu, lambda1, s, overlap=self.overlap, ld=ld, exact=exact,
-                                               counter=counter if fused else None)
+                                               counter=counter if fused else None, step=step)
             obj.backward(seed)
+            if step is not None:
+                return h_val, obj
             stream = torch.cuda.current_stream(dev).cuda_stream
             st = C.c_void_p(stream) if stream else None
             g_ptr = C.c_void_p((h_val if gate is None else gate).data_ptr())

@@ -25,7 +25,7 @@ def test_library_exports_every_symbol():
     L = _lib.load()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.midagma_abi_version() == 8
+    assert L.midagma_abi_version() == 9
 
 
 def test_missing_library_fails_loudly(tmp_path):
