@@ -195,6 +195,39 @@ def test_config5_logdet_side_stream_bit_identical(graph, monkeypatch):
         assert np.array_equal(out[True][k], out[False][k]), k
 
 
+@pytest.mark.parametrize("overlap", [True, False])
+def test_config5_one_launch_step_bit_identical(overlap, monkeypatch):
+    """The replayed step closed by one launch (midagma_mlp_step, ABI 9: the tail's dw sums, fc1's
+    weight gradient, Adam over the four parameters, the next step's fc1 terms) against the separate
+    launches (MIDAGMA_NO_MLP_STEP=1): after 200 Adam steps with checkpoints every 50 every
+    parameter is bit-identical, with the log-det on its side stream and on one stream."""
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    d, n = 200, 1000
+    X, _, _ = make_dataset(d, n, seed=2)
+    if overlap:
+        monkeypatch.delenv("MIDAGMA_NO_OVERLAP", raising=False)
+    else:
+        monkeypatch.setenv("MIDAGMA_NO_OVERLAP", "1")
+    out = {}
+    for one in (True, False):
+        if one:
+            monkeypatch.delenv("MIDAGMA_NO_MLP_STEP", raising=False)
+        else:
+            monkeypatch.setenv("MIDAGMA_NO_MLP_STEP", "1")
+        torch.manual_seed(11)
+        model = DagmaMLP(dims=[d, 10, 1], bias=True).to("cuda:0")
+        with torch.no_grad():
+            model.fc1.weight.normal_(0, 0.3 / np.sqrt(10 * d))
+        dn = DagmaNonlinear(model, device=0)
+        dn.X = torch.from_numpy(X).to("cuda:0")
+        dn.checkpoint = 50
+        assert dn.minimize(200, 2e-4, 0.02, 0.005, 0.1, 1.0)
+        assert all(p.grad is None for p in model.parameters())
+        out[one] = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    for k in out[True]:
+        assert np.array_equal(out[True][k], out[False][k]), k
+
+
 def test_config5_ldfast_path_matches_oracle(parity):
     """The h log-det's warm-started fast path (midagma_ldfast, nonlinear.LdFast): between the
     checkpoint steps (every 100 here; each runs the Gauss-Jordan chain) the product-form series
