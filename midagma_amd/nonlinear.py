@@ -369,10 +369,17 @@ class _SideLogdet:
     def finish(self) -> torch.cuda.Event:
         self.enqueue(self.parts)
         ev_tail, part, l1part, mu, lambda1, half_d, inv_n, out, ctr = self.objective
-        self.side.wait_event(ev_tail)
-        _lib.check(self.L.midagma_mlp_objective_part(_vp(part), part.numel(), _vp(l1part), l1part.numel(),
-                                                     _vp(self.h), mu, lambda1, half_d, inv_n, _vp(out), ctr,
-                                                     C.c_void_p(self.side.cuda_stream)), None, "mlp_objective_part")
+        if not self.exact and ctr is not None and not os.environ.get("MIDAGMA_FAST_OBJECTIVE"):
+            # a fast (LdFast, not exact) step's objective is never read (the loop reads the exact
+            # steps'): only its side effect, the Adam table's step counter, is kept
+            _lib.check(self.L.midagma_counter_advance(ctr, C.c_void_p(self.side.cuda_stream)), None,
+                       "counter_advance")
+        else:
+            self.side.wait_event(ev_tail)
+            _lib.check(self.L.midagma_mlp_objective_part(_vp(part), part.numel(), _vp(l1part), l1part.numel(),
+                                                         _vp(self.h), mu, lambda1, half_d, inv_n, _vp(out), ctr,
+                                                         C.c_void_p(self.side.cuda_stream)), None,
+                       "mlp_objective_part")
         ev = torch.cuda.Event()
         ev.record(self.side)
         return ev
