@@ -75,6 +75,24 @@ __global__ __launch_bounds__(64 * NW) void nm_resid_kernel(const double* __restr
   nm_resid_body<L, NW, false>(blockIdx.x, S, lds, SFromW{}, Pe, Po, Y0, Q0, part0, done, st, xmap, red);
 }
 
+// The DagmaMLP log-det's fast step opened by its residual (no launch before it): the Gauss-Jordan
+// gate reset to "skip", S = (sI - A)^T read from A by the tiles themselves, the warm start's
+// parity that of the step the end (ldfast_end_1wg, gj.hip) will count, st->slots + 1
+template <int L>
+__global__ __launch_bounds__(NTHREADS) void ldfast_resid_kernel(const double* __restrict__ A, int64_t lda, int64_t d,
+                                                                double s, const double* __restrict__ Pe,
+                                                                const double* __restrict__ Po,
+                                                                double* __restrict__ Y0, double* __restrict__ Q0,
+                                                                double* __restrict__ part0, int* __restrict__ done,
+                                                                State* __restrict__ st, State* __restrict__ gjst,
+                                                                int xmap) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) gjst->status = ST_DONE;
+  if (st->status != ST_RUNNING) return;
+  __shared__ double red[4 * 256];
+  SFromW sa{A, lda, d, nullptr, s};
+  nm_resid_body<L, 4, false, true>(blockIdx.x, nullptr, 0, sa, Pe, Po, Y0, Q0, part0, done, st, xmap, red, 1);
+}
+
 #ifdef MIDAGMA_EXPERIMENTS
 // build_at and outer block 0's residual in one launch (fast slots, B2 = 256): workgroups
 // [0, (D/32)^2) build the At tiles, the next 256 the residual tiles with S read from W (the two
@@ -844,6 +862,18 @@ void launch_series_pass(int B2, const SeriesWork& w, State* st, int p, hipStream
     hipLaunchKernelGGL(nm_pass_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, w.Y[(p - 1) & 1], w.Q[(p - 1) & 1],
                        w.Y[p & 1], w.Q[p & 1], w.P, w.part + (p - 1) * PART_STRIDE, w.part + p * PART_STRIDE, w.done,
                        p, st, none, nm_xmap());
+  });
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_ldfast_resid(const double* A, int64_t lda, int64_t d, double s, int B2, const SeriesWork& w, State* st,
+                         State* gjst, hipStream_t stream) {
+  if (d > B2) throw std::invalid_argument("launch_ldfast_resid: d exceeds the series block");
+  with_series_l(B2, [&](auto Lc) {
+    constexpr int L = decltype(Lc)::value;
+    const int nwg = (B2 / 16) * (B2 / 16);
+    hipLaunchKernelGGL(ldfast_resid_kernel<L>, dim3(nwg), dim3(NTHREADS), 0, stream, A, lda, d, s, w.Pe, w.Po, w.Y[0],
+                       w.Q[0], w.part, w.done, st, gjst, nm_xmap());
   });
   HIP_TRY(hipGetLastError());
 }

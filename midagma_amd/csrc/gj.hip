@@ -365,10 +365,48 @@ __device__ __forceinline__ void gj_1wg_phase_end() {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(NTHREADS) void gj_inverse_1wg_kernel(const double* __restrict__ X, int64_t ldx,
-                                                                  double* __restrict__ A, int64_t D, int64_t d,
-                                                                  double s, GJWork w, const State* __restrict__ st) {
-  if (st && st->status != ST_RUNNING) return;
+// ldfast_post's work (mlp.hip) for a fast step, in the workgroup that ran (or skipped) the
+// gated chain: the same values and the same piv sum order.  One workgroup: every thread reads
+// the step's slot before thread 0 counts it, after the reduction's barriers.
+static __device__ void ldfast_end_1wg(const LdfastEnd& e, bool ran, const double* __restrict__ Wgj, int64_t Dgj) {
+  const int64_t slot = e.st->slots + 1;
+  if (ran) {
+    double* dst = (slot & 1) ? e.ring1 : e.ring0;
+    for (int64_t x = threadIdx.x; x < (int64_t)e.B * e.B; x += NTHREADS) {
+      const int64_t i = x / e.B, j = x % e.B;
+      dst[x] = (i < Dgj && j < Dgj) ? Wgj[i * Dgj + j] : (i == j ? 1.0 : 0.0);
+    }
+    for (int64_t x = threadIdx.x; x < e.d * e.d; x += NTHREADS) {
+      const int64_t i = x / e.d, j = x % e.d;
+      e.Mt[i * e.ldm + j] = Wgj[i * Dgj + j];
+    }
+  }
+  __shared__ double red[NTHREADS];
+  double acc = 0.0;
+  if (ran)
+    for (int64_t k = threadIdx.x; k < e.d; k += NTHREADS) acc += e.piv[k];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s2 = NTHREADS / 2; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    State* st = e.st;
+    const double hv = ran ? -red[0] + e.dls : e.hlast[0];
+    e.h[0] = hv;
+    if (ran) e.hlast[0] = hv;
+    st->warm_run = st->warm_run < 2 ? st->warm_run + 1 : 2;
+    st->ckpt_pending = 0;
+    st->status = ST_RUNNING;
+    st->iter += 1;
+    if (ran) st->halvings += 1;
+    st->slots = slot;
+  }
+}
+
+static __device__ void gj_inverse_1wg_body(const double* __restrict__ X, int64_t ldx, double* __restrict__ A,
+                                           int64_t D, int64_t d, double s, const GJWork& w, const State* __restrict__ st) {
   __shared__ __attribute__((aligned(16))) double img[4][NB * ST];
   __shared__ double scratch[4 * NB];
   double(&tile)[32][33] = *reinterpret_cast<double(*)[32][33]>(&img[0][0]);  // build phase only
@@ -393,6 +431,15 @@ __global__ __launch_bounds__(NTHREADS) void gj_inverse_1wg_kernel(const double* 
       }
     gj_1wg_phase_end();
   }
+}
+
+__global__ __launch_bounds__(NTHREADS) void gj_inverse_1wg_kernel(const double* __restrict__ X, int64_t ldx,
+                                                                  double* __restrict__ A, int64_t D, int64_t d,
+                                                                  double s, GJWork w, const State* __restrict__ st,
+                                                                  LdfastEnd end) {
+  const bool ran = !st || st->status == ST_RUNNING;
+  if (ran) gj_inverse_1wg_body(X, ldx, A, D, d, s, w, st);
+  if (end.st) ldfast_end_1wg(end, ran, A, D);
 }
 
 void gj_setup_attributes() {}
@@ -430,9 +477,10 @@ void launch_gj_step(double* A, int64_t lda, int64_t D, const GJWork& w, const St
 }
 
 void launch_gj_inverse_1wg(const double* X, int64_t ldx, double* At, int64_t D, int64_t d, double s, const GJWork& w,
-                           const State* st, hipStream_t stream) {
+                           const State* st, hipStream_t stream, const LdfastEnd& end) {
   if (D % 32) throw std::invalid_argument("gj_inverse_1wg: D must be a multiple of 32");
-  hipLaunchKernelGGL(gj_inverse_1wg_kernel, dim3(1), dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, w, st);
+  if (end.st && (end.d > D || end.d > end.B)) throw std::invalid_argument("gj_inverse_1wg: bad end arguments");
+  hipLaunchKernelGGL(gj_inverse_1wg_kernel, dim3(1), dim3(NTHREADS), 0, stream, X, ldx, At, D, d, s, w, st, end);
   HIP_TRY(hipGetLastError());
 }
 

@@ -39,10 +39,28 @@ void launch_build_at(const double* X, int64_t ldx, bool square, double* At, int6
 void launch_gj_inverse(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
 // the same as its parts: the prologue, then block steps k = 0 .. D/32 - 1 in order
 void launch_gj_prologue(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, hipStream_t stream);
+// The end of a warm-started DagmaMLP log-det step (ldfast_post's work for a fast step, in the same
+// workgroup after the gated chain): if the chain ran, h from its pivots and Mt and the warm-start
+// ring slot from its inverse, else h = *hlast; then the ring state advances (st->slots counts the
+// step: ldfast_resid_kernel opened it without the increment).  st null: no end.
+struct LdfastEnd {
+  const double* piv;
+  int64_t d;
+  double dls;
+  double* h;
+  double* Mt;
+  int64_t ldm;
+  int B;
+  double* ring0;
+  double* ring1;
+  State* st;
+  double* hlast;
+};
 // build_at (A given, not squared) + the whole Gauss-Jordan inverse in one workgroup, gated on st
-// (bit-identical to launch_build_at + launch_gj_inverse; the rare fallback of a warm-started step)
+// (bit-identical to launch_build_at + launch_gj_inverse; the rare fallback of a warm-started step),
+// then `end` when end.st is set
 void launch_gj_inverse_1wg(const double* X, int64_t ldx, double* At, int64_t D, int64_t d, double s, const GJWork& w,
-                           const State* st, hipStream_t stream);
+                           const State* st, hipStream_t stream, const LdfastEnd& end = LdfastEnd{});
 void launch_gj_step(double* A, int64_t lda, int64_t D, const GJWork& w, const State* st, int k, hipStream_t stream);
 
 // A GEMM launch's arguments (launch_gemm's meaning), for launches that carry one beside other work.
@@ -133,6 +151,10 @@ struct SeriesWork {
 };
 void launch_series(const double* S, int64_t lds, int B2, const SeriesWork& w, State* st, int passes,
                    hipStream_t stream);
+// the DagmaMLP log-det's fast step: the gate gjst reset and the series' residual launch with
+// S = (sI - A)^T read from A (d <= B2) and the warm start's parity of st->slots + 1
+void launch_ldfast_resid(const double* A, int64_t lda, int64_t d, double s, int B2, const SeriesWork& w, State* st,
+                         State* gjst, hipStream_t stream);
 // pass p (1 .. NM_PASSES) of that series alone
 void launch_series_pass(int B2, const SeriesWork& w, State* st, int p, hipStream_t stream);
 
@@ -330,10 +352,9 @@ void launch_logdet_post(const double* piv, int64_t d, double dls, double* h, con
 // result's certificate (Mt from P, gate opened when P did not converge or has an entry < 0 or
 // non-finite) and the step's end (h and Mt from the Gauss-Jordan chain when it ran, else h =
 // *hlast; the inverse into the ring; the ring state advanced).
-void launch_ldfast_begin(const double* A, int64_t lda, int64_t d, double s, double* S, int B, State* st, State* gjst,
-                         bool build, hipStream_t stream);
+void launch_ldfast_begin(State* st, State* gjst, hipStream_t stream);
 void launch_ldfast_certify(const double* P, int B, int64_t d, double* Mt, int64_t ldm, const State* st,
-                           const int* done, State* gjst, hipStream_t stream);
+                           const int* done, State* gjst, double* ring0, double* ring1, hipStream_t stream);
 void launch_ldfast_post(const double* piv, int64_t d, double dls, double* h, const double* Wgj, int64_t Dgj, double* Mt,
                         int64_t ldm, const double* P, int B, double* ring0, double* ring1, State* st,
                         const State* gjst, double* hlast, bool exact, hipStream_t stream);

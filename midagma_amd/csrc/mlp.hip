@@ -678,43 +678,38 @@ void launch_mlp_objective_bwd(const double* g, const double* ssq, int64_t np, do
 namespace midagma {
 namespace {
 
-// (sI - A)^T into the B x B S (identity padding); one workgroup also opens the step: the
-// step index (the warm-start ring's parity) and the Gauss-Jordan gate reset to "skip".
-__global__ __launch_bounds__(NTHREADS) void ldfast_begin_kernel(const double* __restrict__ A, int64_t lda, int64_t d,
-                                                                double s, double* __restrict__ S, int B,
-                                                                State* __restrict__ st, State* __restrict__ gjst,
-                                                                int build) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+// An exact step's opening: the step index (the warm-start ring's parity) and the Gauss-Jordan
+// gate reset to "skip".  (A fast step opens in its residual launch, ldfast_resid_kernel, and
+// counts the step at its end.)
+__global__ __launch_bounds__(64) void ldfast_begin_kernel(State* __restrict__ st, State* __restrict__ gjst) {
+  if (threadIdx.x == 0) {
     st->slots += 1;
     gjst->status = ST_DONE;
   }
-  if (!build) return;
-  const int64_t e = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
-  if (e >= (int64_t)B * B) return;
-  const int64_t r = e / B, c = e % B;  // S[r][c] = (sI - A)^T[r][c] = s delta - A[c][r]
-  double v;
-  if (r < d && c < d)
-    v = (r == c ? s : 0.0) - A[c * lda + r];
-  else
-    v = (r == c) ? 1.0 : 0.0;
-  S[e] = v;
 }
 
-// The series' inverse P (B x B, converged: *done != 0) is (sI - A)^-T: Mt (d x d) from it, and
-// the Gauss-Jordan gate opened (gjst->status = ST_RUNNING) when it did not converge or is not
-// entrywise >= 0 and finite on the d x d block.
+// The series' inverse P (B x B, converged: *done != 0) is (sI - A)^-T: Mt (d x d) and the step's
+// warm-start ring slot (parity of st->slots + 1: the end launch counts the step) from it, and the
+// Gauss-Jordan gate opened (gjst->status = ST_RUNNING) when it did not converge or is not
+// entrywise >= 0 and finite on the d x d block (the gated chain's end then overwrites Mt and the
+// slot).  The slot's old contents, slot k-2's inverse, were last read by this step's residual.
 __global__ __launch_bounds__(NTHREADS) void ldfast_certify_kernel(const double* __restrict__ P, int B, int64_t d,
                                                                   double* __restrict__ Mt, int64_t ldm,
                                                                   const State* __restrict__ st,
                                                                   const int* __restrict__ done,
-                                                                  State* __restrict__ gjst) {
+                                                                  State* __restrict__ gjst, double* __restrict__ ring0,
+                                                                  double* __restrict__ ring1) {
   const int64_t e = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  double* dst = ((st->slots + 1) & 1) ? ring1 : ring0;
   int bad = 0;
-  if (e < d * d) {
-    const int64_t i = e / d, j = e % d;
-    const double v = P[i * B + j];
-    Mt[i * ldm + j] = v;
-    bad = !(v >= 0.0) || !isfinite(v);
+  if (e < (int64_t)B * B) {
+    const int64_t i = e / B, j = e % B;
+    const double v = P[e];
+    dst[e] = v;
+    if (i < d && j < d) {
+      Mt[i * ldm + j] = v;
+      bad = !(v >= 0.0) || !isfinite(v);
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && (st->status != ST_RUNNING || *done == 0)) bad = 1;
   if (__syncthreads_or(bad) && threadIdx.x == 0)
@@ -769,19 +764,17 @@ __global__ __launch_bounds__(NTHREADS) void ldfast_post_kernel(const double* __r
 
 }  // namespace
 
-void launch_ldfast_begin(const double* A, int64_t lda, int64_t d, double s, double* S, int B, State* st, State* gjst,
-                         bool build, hipStream_t stream) {
-  const unsigned blocks = build ? (unsigned)(((int64_t)B * B + NTHREADS - 1) / NTHREADS) : 1u;
-  hipLaunchKernelGGL(ldfast_begin_kernel, dim3(blocks), dim3(NTHREADS), 0, stream, A, lda, d, s, S, B, st, gjst,
-                     build ? 1 : 0);
+void launch_ldfast_begin(State* st, State* gjst, hipStream_t stream) {
+  hipLaunchKernelGGL(ldfast_begin_kernel, dim3(1), dim3(64), 0, stream, st, gjst);
   HIP_TRY(hipGetLastError());
 }
 
 void launch_ldfast_certify(const double* P, int B, int64_t d, double* Mt, int64_t ldm, const State* st,
-                           const int* done, State* gjst, hipStream_t stream) {
-  const int64_t blocks = std::max<int64_t>(1, (d * d + NTHREADS - 1) / NTHREADS);
+                           const int* done, State* gjst, double* ring0, double* ring1, hipStream_t stream) {
+  if (d > B) throw std::invalid_argument("ldfast_certify: d exceeds the series block");
+  const int64_t blocks = std::max<int64_t>(1, ((int64_t)B * B + NTHREADS - 1) / NTHREADS);
   hipLaunchKernelGGL(ldfast_certify_kernel, dim3((unsigned)blocks), dim3(NTHREADS), 0, stream, P, B, d, Mt, ldm, st,
-                     done, gjst);
+                     done, gjst, ring0, ring1);
   HIP_TRY(hipGetLastError());
 }
 

@@ -42,6 +42,24 @@ __device__ __forceinline__ void splitk_load_a_w(const double* __restrict__ W, in
   }
 }
 
+// splitk_load_a of S = (sI - A)^T (the DagmaMLP log-det's fast path, B2 x B2 with identity
+// padding) computed from A itself: S[i][k] = (k == i ? s : 0) - A[k][i], the values the former S
+// launch stored, bit for bit, so the fast step's residual needs no launch before it
+// (ldfast_resid_kernel)
+template <int L>
+__device__ __forceinline__ void splitk_load_a_at(const double* __restrict__ A, int64_t lda, int64_t d, double s,
+                                                 int m0, double (&a)[L]) {
+  const int64_t i = m0 + (threadIdx.x & 15), k0 = splitk_k0<L>();
+#pragma unroll
+  for (int q = 0; q < L; ++q) {
+    const int64_t k = k0 + q;
+    if (i < d && k < d)
+      a[q] = (k == i ? s : 0.0) - A[k * lda + i];
+    else
+      a[q] = (k == i) ? 1.0 : 0.0;
+  }
+}
+
 // Row partial of |Q| over this tile's 16 columns -> rowpart[(m0 + row) * NT + tile column]
 __device__ __forceinline__ void store_row_partial(double a, double* __restrict__ rowpart, int m0, int n0, int NT) {
   a = row_sum16(a);
@@ -94,18 +112,21 @@ __device__ __forceinline__ void nm_tile(int wg, int nt, int xmap, int& m0, int& 
 // NW waves split K (B2 = 4 NW L): NW = 4 for B2 <= 256; B2 = 512 runs NW = 8 with L = 16, so
 // the per-lane operand runs and registers stay those of the 256-wide kernel
 // Body of the residual launch for workgroup wg; FROM_W: S from W (outer block 0, SW = {W, ldw,
-// d, s}) instead of the At block S (lds)
+// d, s}) instead of the At block S (lds); FROM_A (sw.pr null): S = (sI - A)^T from A = sw.W with
+// s = sw.s.  slot_bias: added to st->slots for the warm start's parity (1: the step's opening
+// increment is still to come, ldfast_resid_kernel)
 struct SFromW {
   const double* W;
   int64_t ldw, d;
   const Params* pr;
+  double s = 0.0;
 };
-template <int L, int NW, bool FROM_W>
+template <int L, int NW, bool FROM_W, bool FROM_A = false>
 __device__ __forceinline__ void nm_resid_body(int wg, const double* __restrict__ S, int64_t lds, const SFromW& sw,
                                               const double* __restrict__ Pe, const double* __restrict__ Po,
                                               double* __restrict__ Y0, double* __restrict__ Q0,
                                               double* __restrict__ part0, int* __restrict__ done,
-                                              State* __restrict__ st, int xmap, double* red) {
+                                              State* __restrict__ st, int xmap, double* red, int slot_bias = 0) {
   if (st->ckpt_pending) {  // a log-det is due: pivots come from the slow path only
     if (wg == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
     return;
@@ -116,12 +137,14 @@ __device__ __forceinline__ void nm_resid_body(int wg, const double* __restrict__
   int m0, n0;
   nm_tile(wg, nt, xmap, m0, n0);
   if (wg == 0 && threadIdx.x == 0) *done = 0;
-  const bool odd = (st->slots & 1) != 0;
+  const bool odd = ((st->slots + slot_bias) & 1) != 0;
   const double* P1 = odd ? Pe : Po;  // slot k-1
   const double* P2 = odd ? Po : Pe;  // slot k-2
   const bool extrap = st->warm_run >= 2;
   double a[L], b[L];
-  if (FROM_W)
+  if (FROM_A)
+    splitk_load_a_at<L>(sw.W, sw.ldw, sw.d, sw.s, m0, a);
+  else if (FROM_W)
     splitk_load_a_w<L>(sw.W, sw.ldw, sw.d, sw.pr->s, m0, a, sw.pr->w32 != 0);
   else
     splitk_load_a<L>(S, lds, m0, a);

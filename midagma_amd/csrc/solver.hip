@@ -1935,13 +1935,13 @@ struct midagma_ldfast {
   int device = 0;
   int64_t d = 0, Dgj = 0;  // Gauss-Jordan workspace: 32-padded, as midagma_logdet_h_dev
   int B = 0;               // series block: 128 or 256 (0: d > 256, every step exact)
-  DevBuf S, ring0, ring1, Y0, Y1, Q0, Q1, P, part, done, hlast;
+  DevBuf ring0, ring1, Y0, Y1, Q0, Q1, P, part, done, hlast;
   DevBuf A, Pgj, Rgj, Cgj, piv;
   State* st = nullptr;    // the ring's state (slots: step index; warm_run; status of the series)
   State* gjst = nullptr;  // the Gauss-Jordan gate of a fast step (ST_RUNNING: run the chain)
   std::string err;
   ~midagma_ldfast() {
-    for (DevBuf* b : {&S, &ring0, &ring1, &Y0, &Y1, &Q0, &Q1, &P, &part, &done, &hlast, &A, &Pgj, &Rgj, &Cgj, &piv})
+    for (DevBuf* b : {&ring0, &ring1, &Y0, &Y1, &Q0, &Q1, &P, &part, &done, &hlast, &A, &Pgj, &Rgj, &Cgj, &piv})
       b->release();
     if (st) (void)hipFree(st);
     if (gjst) (void)hipFree(gjst);
@@ -1970,7 +1970,7 @@ extern "C" int midagma_ldfast_create(midagma_ldfast** out, int64_t d) {
     h->hlast.alloc(1);
     if (h->B) {
       const size_t BB = (size_t)h->B * h->B;
-      for (DevBuf* b : {&h->S, &h->ring0, &h->ring1, &h->Y0, &h->Y1, &h->Q0, &h->Q1, &h->P}) b->alloc(BB);
+      for (DevBuf* b : {&h->ring0, &h->ring1, &h->Y0, &h->Y1, &h->Q0, &h->Q1, &h->P}) b->alloc(BB);
       h->part.alloc((size_t)(NM_PASSES + 1) * PART_STRIDE);
       h->done.alloc(1);
     }
@@ -1999,7 +1999,7 @@ extern "C" int midagma_ldfast_reset(midagma_ldfast* h) {
     HIP_TRY(hipSetDevice(h->device));
     State st{};
     st.status = ST_RUNNING;
-    st.slots = -1;        // ldfast_begin opens step 0
+    st.slots = -1;        // step 0: opened by ldfast_begin (exact) or counted by the fast step's end
     st.ckpt_pending = 1;  // no warm start: the first step runs the Gauss-Jordan chain
     State gj{};
     gj.status = ST_DONE;
@@ -2011,12 +2011,13 @@ extern "C" int midagma_ldfast_reset(midagma_ldfast* h) {
   });
 }
 
-// fast: 0 begin + series residual, 1 .. 3 the passes, 4 certificate + the gated chain, 5 end;
-// exact: 0 begin + build + prologue, 1 .. Dgj/32 the block steps, last the end
+// fast: 0 the series residual (opening the step), 1 .. 3 the passes, 4 certificate + the gated
+// chain with the step's end; exact: 0 begin + build + prologue, 1 .. Dgj/32 the block steps, last
+// the end
 static constexpr int kLdfastPasses = 3;
 extern "C" int64_t midagma_ldfast_parts(const midagma_ldfast* h, int exact) {
   if (!h) return 0;
-  return (exact || !h->B) ? h->Dgj / 32 + 2 : kLdfastPasses + 3;
+  return (exact || !h->B) ? h->Dgj / 32 + 2 : kLdfastPasses + 2;
 }
 
 extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t d_in, int64_t lda, double s,
@@ -2034,7 +2035,7 @@ extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_
     auto want = [&](int64_t p) { return part < 0 || part == p; };
     if (ex) {  // the Gauss-Jordan chain, ungated
       if (want(0)) {
-        launch_ldfast_begin(A, lda, d, s, h->S.p, h->B, h->st, h->gjst, false, st);
+        launch_ldfast_begin(h->st, h->gjst, st);
         launch_build_at(A, lda, false, h->A.p, D, d, s, nullptr, nullptr, st);
         launch_gj_prologue(h->A.p, D, D, h->gjw(), nullptr, st);
       }
@@ -2046,29 +2047,20 @@ extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_
       return MIDAGMA_OK;
     }
     const SeriesWork w = h->sw();
-    if (want(0)) {
-      launch_ldfast_begin(A, lda, d, s, h->S.p, h->B, h->st, h->gjst, true, st);
-      launch_series(h->S.p, h->B, h->B, w, h->st, 0, st);  // the residual launch only
-    }
+    if (want(0)) launch_ldfast_resid(A, lda, d, s, h->B, w, h->st, h->gjst, st);
     // the passes one by one (each its own part: the caller interleaves them)
     for (int p = 1; p <= kLdfastPasses; ++p)
       if (want(p)) launch_series_pass(h->B, w, h->st, p, st);
     if (want(kLdfastPasses + 1)) {
-      launch_ldfast_certify(h->P.p, h->B, d, Mt_dev, ldm, h->st, reinterpret_cast<const int*>(h->done.p), h->gjst, st);
+      launch_ldfast_certify(h->P.p, h->B, d, Mt_dev, ldm, h->st, reinterpret_cast<const int*>(h->done.p), h->gjst,
+                            h->ring0.p, h->ring1.p, st);
       // gated: opened by the certificate.  One launch, the whole Gauss-Jordan chain in one
       // workgroup (bit-identical; slow when open, which the bench window never is): a closed gate
-      // costs one no-op launch instead of the chain's 2 + D/32 (MIDAGMA_EXP_LDFAST_CHAIN=1, the
-      // experiments build: the launch-per-step chain, gated)
-      if (knob_set("MIDAGMA_EXP_LDFAST_CHAIN")) {
-        launch_build_at(A, lda, false, h->A.p, D, d, s, nullptr, h->gjst, st);
-        launch_gj_inverse(h->A.p, D, D, h->gjw(), h->gjst, st);
-      } else {
-        launch_gj_inverse_1wg(A, lda, h->A.p, D, d, s, h->gjw(), h->gjst, st);
-      }
+      // costs one launch instead of the chain's 2 + D/32, and that launch also ends the step
+      // (ldfast_post's fast-step work in the same workgroup: one dependent launch fewer)
+      const LdfastEnd end{h->piv.p, d, dls, h_dev, Mt_dev, ldm, h->B, h->ring0.p, h->ring1.p, h->st, h->hlast.p};
+      launch_gj_inverse_1wg(A, lda, h->A.p, D, d, s, h->gjw(), h->gjst, st, end);
     }
-    if (want(kLdfastPasses + 2))
-      launch_ldfast_post(h->piv.p, d, dls, h_dev, h->A.p, D, Mt_dev, ldm, h->P.p, h->B, h->ring0.p, h->ring1.p, h->st,
-                         h->gjst, h->hlast.p, false, st);
     return MIDAGMA_OK;
   });
 }
