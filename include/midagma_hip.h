@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 9
+#define MIDAGMA_ABI_VERSION 10
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -282,6 +282,10 @@ int64_t midagma_ldfast_parts(const midagma_ldfast* h, int exact);
 /* ABI 7: d (A is d x d) must equal the handle's d, else MIDAGMA_E_ARG. */
 int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_t d, int64_t lda, double s, double* h_dev,
                            double* Mt_dev, int64_t ldm, void* stream, int exact, int64_t part);
+/* ABI 10: fast steps enqueued from now on also add 1 to *counter (device; null: off) at their
+ * end, midagma_counter_advance's work in the end's launch, for a caller that skips the scalar
+ * objective on those steps.  Exact steps never touch it. */
+int midagma_ldfast_set_counter(midagma_ldfast* h, int64_t* counter);
 /* gate-open (Gauss-Jordan) steps and fast steps since the last reset (diagnostics; syncs) */
 int midagma_ldfast_stats(midagma_ldfast* h, int64_t* steps, int64_t* exact_steps);
 /* ABI 6: the [d, m1, 1] objective with the scalar objective's backward folded into its consumers

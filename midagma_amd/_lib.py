@@ -116,6 +116,7 @@ EXPORTED = {
     "midagma_ldfast_parts": (_i64, [_vp, _int]),
     "midagma_ldfast_enqueue": (_int, [_vp, _vp, _i64, _i64, _d, _vp, _vp, _i64, _vp, _int, _i64]),
     "midagma_ldfast_stats": (_int, [_vp, C.POINTER(_i64), C.POINTER(_i64)]),
+    "midagma_ldfast_set_counter": (_int, [_vp, _vp]),
     "midagma_mlp_tail_fwd_part": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),
     "midagma_mlp_objective_part": (_int, [_vp, _i64, _vp, _i64, _vp, _d, _d, _d, _d, _vp, _vp, _vp]),
     "midagma_mlp_tail_bwd_obj": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _d, _d, _d, _i64, _i64, _i64, _vp, _vp, _vp,

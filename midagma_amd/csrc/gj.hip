@@ -402,6 +402,7 @@ static __device__ void ldfast_end_1wg(const LdfastEnd& e, bool ran, const double
     st->iter += 1;
     if (ran) st->halvings += 1;
     st->slots = slot;
+    if (e.counter) *e.counter += 1;  // (midagma_ldfast_set_counter: counter_advance's work)
   }
 }
 

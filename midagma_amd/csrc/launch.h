@@ -55,6 +55,7 @@ struct LdfastEnd {
   double* ring1;
   State* st;
   double* hlast;
+  int64_t* counter;  // nullable: the Adam table's step counter, advanced by the end (+= 1)
 };
 // build_at (A given, not squared) + the whole Gauss-Jordan inverse in one workgroup, gated on st
 // (bit-identical to launch_build_at + launch_gj_inverse; the rare fallback of a warm-started step),

@@ -1939,6 +1939,7 @@ struct midagma_ldfast {
   DevBuf A, Pgj, Rgj, Cgj, piv;
   State* st = nullptr;    // the ring's state (slots: step index; warm_run; status of the series)
   State* gjst = nullptr;  // the Gauss-Jordan gate of a fast step (ST_RUNNING: run the chain)
+  int64_t* counter = nullptr;  // advanced by a fast step's end (midagma_ldfast_set_counter)
   std::string err;
   ~midagma_ldfast() {
     for (DevBuf* b : {&ring0, &ring1, &Y0, &Y1, &Q0, &Q1, &P, &part, &done, &hlast, &A, &Pgj, &Rgj, &Cgj, &piv})
@@ -2058,11 +2059,18 @@ extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_
       // workgroup (bit-identical; slow when open, which the bench window never is): a closed gate
       // costs one launch instead of the chain's 2 + D/32, and that launch also ends the step
       // (ldfast_post's fast-step work in the same workgroup: one dependent launch fewer)
-      const LdfastEnd end{h->piv.p, d, dls, h_dev, Mt_dev, ldm, h->B, h->ring0.p, h->ring1.p, h->st, h->hlast.p};
+      const LdfastEnd end{h->piv.p, d, dls, h_dev, Mt_dev, ldm, h->B, h->ring0.p, h->ring1.p, h->st, h->hlast.p,
+                          h->counter};
       launch_gj_inverse_1wg(A, lda, h->A.p, D, d, s, h->gjw(), h->gjst, st, end);
     }
     return MIDAGMA_OK;
   });
+}
+
+extern "C" int midagma_ldfast_set_counter(midagma_ldfast* h, int64_t* counter) {
+  if (!h) return fail(nullptr, MIDAGMA_E_ARG, "ldfast_set_counter: null handle");
+  h->counter = counter;
+  return MIDAGMA_OK;
 }
 
 extern "C" int midagma_ldfast_stats(midagma_ldfast* h, int64_t* steps, int64_t* exact_steps) {

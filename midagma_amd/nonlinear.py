@@ -199,7 +199,7 @@ class _MLPObjective(torch.autograd.Function):
                 ev_fc1 = torch.cuda.Event()
                 ev_fc1.record(main)
                 side.wait_event(ev_fc1)
-                chain = _SideLogdet(L, side, A, d, float(s), h, Mt, ld=ld, exact=exact)
+                chain = _SideLogdet(L, side, A, d, float(s), h, Mt, ld=ld, exact=exact, ctr=ctr)
                 chain.enqueue(1)
                 _tail_fwd(L, fused, X, W1, b1, w2, b2, n, d, m1, Z, R, part, st)
                 ev_tail = torch.cuda.Event()
@@ -210,6 +210,7 @@ class _MLPObjective(torch.autograd.Function):
                 ctx.keep = (A, l1part)  # read on the side stream: alive until the join
             else:
                 if ld is not None:
+                    ld.set_counter(None)  # (the objective below advances the counter)
                     ld.enqueue(A, d, float(s), h, Mt, stream, exact, -1)
                 else:
                     _lib.check(L.midagma_logdet_h_dev(_vp(A), d, d, float(s), _vp(h), _vp(Mt), d, st), None,
@@ -345,14 +346,19 @@ class _MlpStep:
 class _SideLogdet:
     """The h log-det (midagma_logdet_h_dev_part, or a warm-started LdFast step) enqueued part by
     part on a side stream, then the scalar objective once the tail's row partials are ready (objective
-    = (event, part, l1part, mu, lambda1, half_d, inv_n, out, counter or None))."""
+    = (event, part, l1part, mu, lambda1, half_d, inv_n, out, counter or None)).  A fast (LdFast, not
+    exact) step's objective is never read (the loop reads the exact steps'): only its side effect,
+    the Adam table's step counter `ctr`, is kept, advanced by the LdFast step's own end launch."""
 
-    def __init__(self, L, side, A, d, s, h, Mt, ld=None, exact=True):
+    def __init__(self, L, side, A, d, s, h, Mt, ld=None, exact=True, ctr=None):
         self.L, self.side, self.A, self.d, self.s, self.h, self.Mt = L, side, A, d, s, h, Mt
         self.ld, self.exact = ld, exact
         self.parts = ld.parts(exact) if ld is not None else int(L.midagma_logdet_h_parts(d))
         self.next = 0
         self.objective = None
+        self.skip = not exact and ctr is not None and not os.environ.get("MIDAGMA_FAST_OBJECTIVE")
+        if ld is not None:  # (before any part: the handle reads it at the enqueue of its end)
+            ld.set_counter(ctr if self.skip else None)
 
     def enqueue(self, k):
         ss = C.c_void_p(self.side.cuda_stream)
@@ -369,11 +375,10 @@ class _SideLogdet:
     def finish(self) -> torch.cuda.Event:
         self.enqueue(self.parts)
         ev_tail, part, l1part, mu, lambda1, half_d, inv_n, out, ctr = self.objective
-        if not self.exact and ctr is not None and not os.environ.get("MIDAGMA_FAST_OBJECTIVE"):
-            # a fast (LdFast, not exact) step's objective is never read (the loop reads the exact
-            # steps'): only its side effect, the Adam table's step counter, is kept
-            _lib.check(self.L.midagma_counter_advance(ctr, C.c_void_p(self.side.cuda_stream)), None,
-                       "counter_advance")
+        if self.skip:  # the step counter only (see the class docstring)
+            if self.ld is None:
+                _lib.check(self.L.midagma_counter_advance(ctr, C.c_void_p(self.side.cuda_stream)), None,
+                           "counter_advance")
         else:
             self.side.wait_event(ev_tail)
             _lib.check(self.L.midagma_mlp_objective_part(_vp(part), part.numel(), _vp(l1part), l1part.numel(),
@@ -423,6 +428,11 @@ class LdFast:
         _lib.check(self.L.midagma_ldfast_enqueue(self.h, _vp(A), d, d, float(s), _vp(h), _vp(Mt), d,
                                                  C.c_void_p(stream) if stream else None, 1 if exact else 0, part),
                    None, "ldfast_enqueue")
+
+    def set_counter(self, counter):
+        """Fast steps enqueued from now on advance `counter` (a c_void_p to a device int64, or
+        None: off) in their end launch (midagma_ldfast_set_counter, ABI 10)."""
+        _lib.check(self.L.midagma_ldfast_set_counter(self.h, counter), None, "ldfast_set_counter")
 
     def stats(self):
         """(steps, steps that ran the Gauss-Jordan chain) since the last reset."""

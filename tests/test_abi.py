@@ -25,7 +25,7 @@ def test_library_exports_every_symbol():
     L = _lib.load()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.midagma_abi_version() == 9
+    assert L.midagma_abi_version() == 10
 
 
 def test_missing_library_fails_loudly(tmp_path):
@@ -74,3 +74,4 @@ def test_ldfast_entry_points_validate_without_a_device():
     out = C.c_void_p()
     assert L.midagma_ldfast_create(C.byref(out), 0) == -3
     assert L.midagma_ldfast_reset(None) == -3
+    assert L.midagma_ldfast_set_counter(None, None) == -3
