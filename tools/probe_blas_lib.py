@@ -34,6 +34,13 @@ for lib in ("hipblas", "ck", "hipblaslt"):
         r = n // ks
         g = t(lambda: torch.bmm(dZ.view(ks, r, -1).transpose(1, 2), X.view(ks, r, -1)))
         g1 = t(lambda: dZ.t() @ X)
-        print(f"{lib:10s} ({cur}): fwd {f:7.2f} us  bwd bmm4 {g:7.2f} us  bwd mm {g1:7.2f} us", flush=True)
+        # layouts the tail kernels would have to adopt: Z^T = W1 X^T with X^T stored once (X is
+        # fixed over a fit), and Z = X W1t with W1^T stored (one transposed copy per step)
+        XT = X.t().contiguous()
+        W1t = W1.t().contiguous()
+        ft = t(lambda: W1 @ XT)
+        fw = t(lambda: X @ W1t)
+        print(f"{lib:10s} ({cur}): fwd {f:7.2f} us  fwd Z^T=W1 X^T {ft:7.2f} us  fwd X W1t {fw:7.2f} us  "
+              f"bwd bmm4 {g:7.2f} us  bwd mm {g1:7.2f} us", flush=True)
     except Exception as e:  # noqa: BLE001
         print(lib, "failed:", repr(e)[:200], flush=True)
