@@ -198,3 +198,47 @@ def test_ldfast_gate_open_fallback_equals_chain():
     assert h_open == h_ex and np.array_equal(M_open, M_ex)
     assert h_fast == h0                          # a certified fast step keeps the last exact h
     assert np.abs(M_fast - M_ex1).max() <= 1e-12 * np.abs(M_ex1).max()
+
+
+@pytest.mark.gpu
+def test_ldfast_counter_advanced_by_fast_steps_only():
+    """midagma_ldfast_set_counter (ABI 10): every fast step enqueued while a counter is set adds 1
+    to it in its end launch, whether its gate stayed shut or opened; exact steps, and fast steps
+    after set_counter(NULL), leave it alone (DagmaNonlinear's skipped objective keeps only this
+    side effect, nonlinear.py:214-217)."""
+    import ctypes as C
+    import torch
+    from midagma_amd import _lib
+    L = _lib.load()
+    d = 200
+    rng = np.random.default_rng(5)
+    A1 = rng.uniform(0.0, 0.5 / d, size=(d, d))
+    A2 = rng.uniform(0.0, 1.2 / d, size=(d, d))  # far: the certificate fails, the gate opens
+    dev = "cuda:0"
+    f64 = dict(dtype=torch.float64, device=dev)
+    ctr = torch.full((1,), 7, dtype=torch.int64, device=dev)
+    h = C.c_void_p()
+    _lib.check(L.midagma_ldfast_create(C.byref(h), d), None, "ldfast_create")
+
+    def step(A, exact):
+        At = torch.from_numpy(A).to(dev)
+        hv, Mt = torch.zeros((), **f64), torch.zeros(d, d, **f64)
+        _lib.check(L.midagma_ldfast_enqueue(h, C.c_void_p(At.data_ptr()), d, d, 1.0, C.c_void_p(hv.data_ptr()),
+                                            C.c_void_p(Mt.data_ptr()), d, None, 1 if exact else 0, -1),
+                   None, "ldfast_enqueue")
+        torch.cuda.synchronize()
+        return int(ctr.item())
+
+    try:
+        _lib.check(L.midagma_ldfast_set_counter(h, C.c_void_p(ctr.data_ptr())), None, "ldfast_set_counter")
+        assert step(A1, True) == 7                    # exact: its objective advances the counter
+        assert step(A1 * (1 + 1e-6), False) == 8      # fast, gate shut
+        assert step(A1 * (1 + 2e-6), False) == 9
+        assert step(A2, False) == 10                  # fast, gate opened (the chain ran)
+        _lib.check(L.midagma_ldfast_set_counter(h, None), None, "ldfast_set_counter")
+        assert step(A2 * (1 + 1e-6), False) == 10
+        a, b = C.c_int64(), C.c_int64()
+        _lib.check(L.midagma_ldfast_stats(h, C.byref(a), C.byref(b)), None, "ldfast_stats")
+        assert a.value == 5
+    finally:
+        L.midagma_ldfast_destroy(h)
