@@ -228,6 +228,38 @@ def test_config5_one_launch_step_bit_identical(overlap, monkeypatch):
         assert np.array_equal(out[True][k], out[False][k]), k
 
 
+def test_config5_skipped_fast_objective_bit_identical(monkeypatch):
+    """A fast (LdFast) step's scalar objective, which the loop never reads (nonlinear.py:214-217),
+    is skipped and the Adam table's step counter it advanced is advanced by the LdFast step's end
+    instead (midagma_ldfast_set_counter, ABI 10): against the objective kept on every step
+    (MIDAGMA_FAST_OBJECTIVE=1), after 200 Adam steps with checkpoints every 50 every parameter is
+    bit-identical."""
+    from midagma_amd.nonlinear import DagmaMLP, DagmaNonlinear
+    d, n = 200, 1000
+    X, _, _ = make_dataset(d, n, seed=3)
+    monkeypatch.delenv("MIDAGMA_NO_OVERLAP", raising=False)
+    monkeypatch.delenv("MIDAGMA_NO_LDFAST", raising=False)
+    out = {}
+    for keep in (False, True):
+        if keep:
+            monkeypatch.setenv("MIDAGMA_FAST_OBJECTIVE", "1")
+        else:
+            monkeypatch.delenv("MIDAGMA_FAST_OBJECTIVE", raising=False)
+        torch.manual_seed(13)
+        model = DagmaMLP(dims=[d, 10, 1], bias=True).to("cuda:0")
+        with torch.no_grad():
+            model.fc1.weight.normal_(0, 0.3 / np.sqrt(10 * d))
+        dn = DagmaNonlinear(model, device=0)
+        dn.X = torch.from_numpy(X).to("cuda:0")
+        dn.checkpoint = 50
+        assert dn.minimize(200, 2e-4, 0.02, 0.005, 0.1, 1.0)
+        steps, gj = dn._ld.stats()
+        assert steps >= 200 and gj < steps  # the fast path ran (the skip applies to its steps)
+        out[keep] = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    for k in out[True]:
+        assert np.array_equal(out[True][k], out[False][k]), k
+
+
 def test_config5_ldfast_path_matches_oracle(parity):
     """The h log-det's warm-started fast path (midagma_ldfast, nonlinear.LdFast): between the
     checkpoint steps (every 100 here; each runs the Gauss-Jordan chain) the product-form series
