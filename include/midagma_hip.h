@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MIDAGMA_ABI_VERSION 10
+#define MIDAGMA_ABI_VERSION 11
 
 /* return codes */
 #define MIDAGMA_OK 0
@@ -140,6 +140,45 @@ int midagma_comm_allreduce_zbuf(midagma_solver* s);
  * Bind an external buffer (e.g. a torch tensor that torch.distributed all-reduces). */
 int64_t midagma_zbuf_len(const midagma_solver* s);
 int midagma_bind_zbuf(midagma_solver* s, void* dev_ptr, int64_t len);
+
+/* ABI 11: data mode on several devices from ONE process ("one host thread drives
+ * all its devices ... the Python side stays single-process"), behind the reference's single-process
+ * DagmaLinear.fit(X) (linear.py:335-351; the per-step score gradient 244-246 summed over row shards).
+ * A group holds one data-mode solver per entry of devices[] (member k holds row shard k of X); the
+ * score partial is summed over the members inside every captured slot, between the GEMMs and the
+ * update:
+ *   - devices all distinct: one RCCL communicator per member from ncclCommInitAll over devices[];
+ *     each member's slot graphs carry its all-reduce and are replayed by a library thread of its
+ *     own, with the (status, iters) agreement all-reduce at every poll (midagma_comm_init's
+ *     protocol).  All members finish their setup (begin, graph capture) before any collective is
+ *     issued; a member that fails before that point fails the call on every member.
+ *   - flags & MIDAGMA_GROUP_EMULATE (every entry of devices[] the same device; tests on one GPU): no
+ *     RCCL.  The members' slots are captured as ONE graph over their streams with a fixed-order
+ *     device sum of the partials (member 0 + member 1 + ...) in place of the all-reduce, and the
+ *     calling thread replays it (test strategy 4).
+ * Members are ordinary data-mode solvers (midagma_group_member, owned by the group): set_cov,
+ * set_masks, set_w_float32, set_trek*, h, score_partial / score_finish and checkpoints act on one
+ * member; apply the loop's settings (cov, masks, dtype, trek) to every member. */
+#define MIDAGMA_GROUP_EMULATE 1
+typedef struct midagma_group midagma_group;
+int midagma_group_create(midagma_group** out, int loss, int64_t d, const int* devices, int ndev, int flags);
+void midagma_group_destroy(midagma_group* g);
+const char* midagma_group_last_error(const midagma_group* g);
+int midagma_group_size(const midagma_group* g);
+int midagma_group_emulated(const midagma_group* g);
+midagma_solver* midagma_group_member(midagma_group* g, int k);
+/* host X (n x d row-major): member k gets rows [lo_k, hi_k) of the even split (the first n % ndev
+ * members take one row more), with n_global = n.  MIDAGMA_E_ARG when n < ndev. */
+int midagma_group_set_data(midagma_group* g, const double* X, int64_t n);
+/* every member's score buffer (score_partial's or data_gram's partial) <- the sum over the members;
+ * returns after it is written */
+int midagma_group_allreduce_zbuf(midagma_group* g);
+/* DagmaLinear.minimize over the group (arguments and result as midagma_minimize).  W: host d x d,
+ * in/out, from member 0 after the members were checked to end with the same W bits, status,
+ * iterations and halvings (else MIDAGMA_E_STATE: the replicas diverged). */
+int midagma_group_minimize(midagma_group* g, double* W, double mu, int64_t max_iter, double s_dom, double lr,
+                           double tol, double beta1, double beta2, double lambda1, int64_t checkpoint,
+                           midagma_result* res);
 
 /* Replaces DagmaLinear.minimize(W, mu, max_iter, s, lr, tol, beta_1, beta_2)
  * (linear.py:165-333) with trek_reg disabled.  W: host d x d, in/out. */

@@ -16,7 +16,7 @@ import numpy as np
 
 __all__ = ["lib", "load", "check", "MidagmaResult", "MidagmaCkpt", "LIB_PATH", "HipSolverError",
            "ST_RUNNING", "ST_DONE", "ST_FAILED", "ST_LR_UNDERFLOW", "ST_SINGULAR",
-           "LOSS_L2", "LOSS_LOGISTIC", "MODE_COV", "MODE_DATA", "EXPORTED"]
+           "LOSS_L2", "LOSS_LOGISTIC", "MODE_COV", "MODE_DATA", "EXPORTED", "GROUP_EMULATE"]
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmidagma_hip.so")
 
@@ -126,7 +126,19 @@ EXPORTED = {
                                 _vp, _i64, _vp, _vp, _vp, _d, _d, _d, _d, _d, _vp, _vp, _vp, _vp]),
     "midagma_mlp_tail_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "midagma_mlp_tail_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # ABI 11: data mode on several devices from one process (midagma_amd.solver.HipGroup)
+    "midagma_group_create": (_int, [C.POINTER(_vp), _int, _i64, C.POINTER(_int), _int, _int]),
+    "midagma_group_destroy": (None, [_vp]),
+    "midagma_group_last_error": (C.c_char_p, [_vp]),
+    "midagma_group_size": (_int, [_vp]),
+    "midagma_group_emulated": (_int, [_vp]),
+    "midagma_group_member": (_vp, [_vp, _int]),
+    "midagma_group_set_data": (_int, [_vp, _dp, _i64]),
+    "midagma_group_allreduce_zbuf": (_int, [_vp]),
+    "midagma_group_minimize": (_int, [_vp, _dp, _d, _i64, _d, _d, _d, _d, _d, _d, _i64, C.POINTER(MidagmaResult)]),
 }
+
+GROUP_EMULATE = 1
 
 _lock = threading.Lock()
 _lib = None
@@ -166,10 +178,16 @@ def last_error(handle=None) -> str:
     return msg.decode() if msg else ""
 
 
-def check(rc: int, handle=None, what: str = ""):
+def check(rc: int, handle=None, what: str = "", group: bool = False):
+    """Raise for a negative return code: LinAlgError (singular), ValueError (bad argument,
+    non-finite input) or HipSolverError; `group`: the handle is a midagma_group."""
     if rc >= 0:
         return rc
-    msg = last_error(handle)
+    if group:
+        m = lib().midagma_group_last_error(handle)
+        msg = m.decode() if m else ""
+    else:
+        msg = last_error(handle)
     if rc == E_SINGULAR:
         raise np.linalg.LinAlgError(msg or "singular matrix")
     if rc == E_ARG:

@@ -16,6 +16,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "launch.h"
 
@@ -27,6 +28,7 @@ struct RcclApi {
   void* lib = nullptr;
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclCommInitAll) init_all = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
@@ -55,10 +57,11 @@ RcclApi& api() {
     }
     a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(a.lib, "ncclGetUniqueId"));
     a.init_rank = reinterpret_cast<decltype(a.init_rank)>(dlsym(a.lib, "ncclCommInitRank"));
+    a.init_all = reinterpret_cast<decltype(a.init_all)>(dlsym(a.lib, "ncclCommInitAll"));
     a.all_reduce = reinterpret_cast<decltype(a.all_reduce)>(dlsym(a.lib, "ncclAllReduce"));
     a.destroy = reinterpret_cast<decltype(a.destroy)>(dlsym(a.lib, "ncclCommDestroy"));
     a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(a.lib, "ncclGetErrorString"));
-    if (!a.get_unique_id || !a.init_rank || !a.all_reduce || !a.destroy || !a.error_string)
+    if (!a.get_unique_id || !a.init_rank || !a.init_all || !a.all_reduce || !a.destroy || !a.error_string)
       a.why = "RCCL: a symbol is missing";
   });
   if (!a.why.empty()) throw std::runtime_error(a.why);
@@ -96,6 +99,14 @@ void* comm_create(const void* id, int nranks, int rank) {
   ncclComm_t c = nullptr;
   check_nccl(api().init_rank(&c, nranks, u, rank), "ncclCommInitRank");
   return c;
+}
+
+// ABI 11: the communicators of a single-process device group, one per device of devlist (RCCL's
+// own group initialisation: ncclCommInitAll); comms[k] is rank k
+void comm_create_all(int ndev, const int* devlist, void** comms) {
+  std::vector<ncclComm_t> c((size_t)ndev, nullptr);
+  check_nccl(api().init_all(c.data(), ndev, devlist), "ncclCommInitAll");
+  for (int k = 0; k < ndev; ++k) comms[k] = c[(size_t)k];
 }
 
 void comm_destroy(void* comm) {

@@ -520,6 +520,7 @@ GramPlan gram_plan(int64_t n, int64_t d, int64_t chunk_rows);
 // in-place all-reduce of n doubles (sum, or max) on stream (graph-capturable)
 int comm_unique_id(void* out);
 void* comm_create(const void* id, int nranks, int rank);
+void comm_create_all(int ndev, const int* devlist, void** comms);
 void comm_destroy(void* comm);
 void comm_allreduce(void* comm, double* buf, size_t n, bool max, hipStream_t stream);
 // out[0..4) = (status, iter, -status, -iter) of *st (one max all-reduce: max and min over ranks)

@@ -19,6 +19,12 @@ the C ABI.  Extra keyword-only constructor arguments:
   'nccl' process group), 'host' (a `dist.all_reduce` between `step_partial` and `step_finish`
   every step; the default otherwise, e.g. gloo) or None (the default for the backend).
 * ``solver_factory``  the backend class (default `HipSolver`; tests pass a CPU double).
+* ``devices``  data mode on several devices from this ONE process (ABI 11, `HipGroup`): X is
+  row-sharded over the listed devices and every step sums the shards' score partials, RCCL
+  between distinct devices (ncclCommInitAll, one library thread per device), a fixed-order
+  device sum when every entry names the same device (an emulated group: the sharded arithmetic
+  on one GPU).  No launcher and no process group: `DagmaLinear('l2', devices=[0, 1, 2, 3]).fit(X)`.
+  Implies score_mode='data'.  ``group_factory`` replaces `HipGroup` (tests).
 
 `fit(X, ..., n_global=N)` (keyword-only extra): X is this rank's row shard of an
 N-row data matrix.  Each rank then touches only its own rows: l2 centring uses
@@ -73,7 +79,7 @@ class DagmaLinear:
     def __init__(self, loss_type: str, verbose: bool = False, dtype: type = np.float64, *,
                  trek_reg=None, logger=None, log_cfg=None, score_mode: str | None = None,
                  device: int | None = None, process_group=None, force_allreduce: bool = False,
-                 comm: str | None = None, solver_factory=None) -> None:
+                 comm: str | None = None, solver_factory=None, devices=None, group_factory=None) -> None:
         losses = ["l2", "logistic"]
         assert loss_type in losses, f"loss_type should be one of {losses}"
         # dtype (linear.py:29, 55): the type of Id, the exclusion mask and W_est (408, 220, 429).  The
@@ -97,6 +103,19 @@ class DagmaLinear:
         self._logger = logger or build_default_logger(level=logging.INFO if verbose else logging.WARNING)
         self._log_cfg = log_cfg or LogConfig(enabled=verbose)
         self._slog = StructuredLogger(self._logger, self._log_cfg)
+        if devices is not None:
+            devices = [int(x) for x in devices]
+            if not devices:
+                raise ValueError("devices must name at least one device")
+            if score_mode not in (None, "data"):
+                raise ValueError("devices=[...] shards X over the devices: it needs score_mode='data'")
+            if process_group is not None or force_allreduce or comm is not None:
+                raise ValueError("devices=[...] drives the devices from this process: no process_group, "
+                                 "force_allreduce or comm")
+            score_mode = "data"
+            device = devices[0]
+        self.devices = devices
+        self._group_factory = group_factory
         self.score_mode = score_mode or ("cov" if loss_type == "l2" else "data")
         if self.loss_type == "logistic" and self.score_mode != "data":
             raise ValueError("logistic loss needs score_mode='data' (the gradient depends on X every step)")
@@ -116,8 +135,9 @@ class DagmaLinear:
 
     # ------------------------------------------------------------------ helpers
     def _world(self):
-        # cov mode talks to the other ranks only while a sharded fit() prepares cov
-        if self.score_mode != "data" and not getattr(self, "_sharded", False):
+        # cov mode talks to the other ranks only while a sharded fit() prepares cov; a device group
+        # is one process
+        if self.devices is not None or (self.score_mode != "data" and not getattr(self, "_sharded", False)):
             return 1, 0
         try:
             import torch.distributed as dist
@@ -182,6 +202,16 @@ class DagmaLinear:
                 lo, hi = _row_range(self.n, world, rank)
                 X_local = self.X[lo:hi]
             s.set_data(X_local if is_device_tensor(X_local) else np.ascontiguousarray(X_local), n_global=self.n)
+            if getattr(s, "is_group", False):
+                # a single-process device group: the members' sum inside the slots and in _score
+                self._inlib = True
+                if cov_on_device:
+                    self.cov = s.gram_cov(float(self.n))
+                else:
+                    s.set_cov(self.cov)
+                self._install_trek(s)
+                self._solver = s
+                return
             self._inlib = (world > 1 or self.force_allreduce) and self._comm_kind() == "library"
             if self._inlib:
                 # the solver's own communicator: the score all-reduce inside the replayed slots
@@ -222,6 +252,11 @@ class DagmaLinear:
             self.cov = s.get_cov()
         else:
             s.set_cov(self.cov)
+        self._install_trek(s)
+        self._solver = s
+
+    def _install_trek(self, s):
+        """The trek regularizer of linear.py:251-258 on the solver (every member of a group)."""
         tr = self.trek_reg
         if tr is not None and tr.enabled() and tr.cfg.get("I") is not None and len(tr.cfg["I"]) > 0:
             if str(tr.name).lower().strip() == "tcc":
@@ -233,7 +268,6 @@ class DagmaLinear:
                 kw = dict(tr.cfg.get("kwargs") or {})
                 s.set_trek(tr.cfg["I"], tr.cfg.get("seq", "exp"), agg=kw.get("agg", "mean"), mode=tr.mode,
                            weight=tr.weight, eps_inv=kw.get("eps_inv", 1e-8), K_log=kw.get("K_log"))
-        self._solver = s
 
     # ------------------------------------------------------- reference methods
     def _score(self, W: np.ndarray) -> typing.Tuple[float, np.ndarray]:
@@ -362,7 +396,13 @@ class DagmaLinear:
                                                          float(X.shape[0]) * self.d * self.d >= 1e11)))
             if sharded and self.score_mode == "cov" and not gram_device:
                 raise ValueError("fit(X_shard, n_global=...) in cov mode forms cov on the device (gram='device')")
-            solver = self._solver_factory(self.d, self.loss_type, self.score_mode, device=self.device)
+            if self.devices is not None and sharded:
+                raise ValueError("devices=[...] shards X itself: pass the whole X, not n_global")
+            if self.devices is not None:
+                from .solver import HipGroup
+                solver = (self._group_factory or HipGroup)(self.d, self.loss_type, devices=self.devices)
+            else:
+                solver = self._solver_factory(self.d, self.loss_type, self.score_mode, device=self.device)
             if self.loss_type == 'l2':
                 if on_dev:  # the centring on the device: column sums (all-reduced over shards), X -= mean
                     colsum = self._allreduce_tensor(solver.colsum(X)) if sharded else solver.colsum(X)
@@ -391,6 +431,12 @@ class DagmaLinear:
             # data mode over several ranks (or a shard, or a device X): cov from the device Gram
             # matrices, no rank multiplies another rank's rows; one host X keeps the reference's product
             cov_on_device = self.score_mode == "data" and (sharded or world > 1 or on_dev)
+            if self.devices is not None:
+                # a device group: the members' Gram matrices summed (RCCL / the emulated sum) for a
+                # device X, gram='device', or a large X (as cov mode's 'auto'); else the reference's
+                # host product (linear.py:428)
+                cov_on_device = on_dev or gram == "device" or (
+                    gram == "auto" and float(X.shape[0]) * self.d * self.d >= 1e11)
             X_local = X if sharded else None
             if not cov_on_device and not gram_device:
                 self.cov = X.T @ X / float(self.n)

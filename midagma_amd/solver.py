@@ -17,8 +17,8 @@ import numpy as np
 from . import _lib
 from ._lib import check, dptr
 
-__all__ = ["HipSolver", "MinimizeResult", "CheckpointRecord", "run_allreduce_minimize", "device_count",
-           "colsum_dev", "center_dev", "gram"]
+__all__ = ["HipSolver", "HipGroup", "MinimizeResult", "CheckpointRecord", "run_allreduce_minimize",
+           "device_count", "colsum_dev", "center_dev", "gram", "row_range"]
 
 
 CheckpointRecord = namedtuple("CheckpointRecord", [f for f, _ in _lib.MidagmaCkpt._fields_])
@@ -118,22 +118,29 @@ def gram(X, device: int | None = None):
 class HipSolver:
     """Owns device buffers for one d and one score mode on one GPU."""
 
-    def __init__(self, d: int, loss: str = "l2", mode: str = "cov", device: int = 0, stream: int | None = None):
+    def __init__(self, d: int, loss: str = "l2", mode: str = "cov", device: int = 0, stream: int | None = None,
+                 _handle=None):
         self.L = _lib.lib()
         self.d = int(d)
         self.loss = loss
         self.mode = mode
         lt = {"l2": _lib.LOSS_L2, "logistic": _lib.LOSS_LOGISTIC}[loss]
         md = {"cov": _lib.MODE_COV, "data": _lib.MODE_DATA}[mode]
-        h = C.c_void_p()
-        check(self.L.midagma_create(C.byref(h), lt, md, self.d, int(device), stream), None, "midagma_create")
+        # _handle: a solver owned by something else (a HipGroup's member); never destroyed here
+        self._owned = _handle is None
+        if _handle is None:
+            h = C.c_void_p()
+            check(self.L.midagma_create(C.byref(h), lt, md, self.d, int(device), stream), None, "midagma_create")
+        else:
+            h = C.c_void_p(_handle)
         self.h = h
         self.device = device
         self.D = int(self.L.midagma_padded_dim(self.h))
 
     def close(self):
         if getattr(self, "h", None):
-            self.L.midagma_destroy(self.h)
+            if self._owned:
+                self.L.midagma_destroy(self.h)
             self.h = None
 
     def __del__(self):  # pragma: no cover
@@ -388,6 +395,173 @@ class HipSolver:
         G = np.empty((self.d, self.d))
         check(self.L.midagma_score_finish(self.h, C.byref(loss), dptr(G)), self.h, "score_finish")
         return float(loss.value), G
+
+
+def row_range(n: int, parts: int, k: int):
+    """Rows [lo, hi) of part k of the even split of n rows (the first n % parts parts take one
+    row more): the data-mode shard of rank / group member k."""
+    base, extra = divmod(int(n), int(parts))
+    lo = k * base + min(k, extra)
+    return lo, lo + base + (1 if k < extra else 0)
+
+
+class HipGroup:
+    """Data mode on several devices from ONE process (ABI 11, `midagma_group_*`): member k is a
+    data-mode `HipSolver` on devices[k] holding row shard k of X, and every slot sums the members'
+    score partials (the Python side stays single-process; the reference's own
+    entry is the single-process `fit(X)`, linear.py:335-351).
+
+    Distinct devices: an RCCL communicator per member from ncclCommInitAll, the all-reduce inside
+    each member's replayed slot graphs, one library thread per device.  Repeated devices (every
+    entry the same, e.g. [0, 0, 0, 0]) or emulate=True: an emulated group on that one device, whose
+    slots are captured as one graph with a fixed-order device sum of the partials instead of RCCL
+    (the sharding's arithmetic on a one-GPU box).
+
+    It answers HipSolver's calls that `DagmaLinear` makes, broadcasting the loop's settings to
+    every member and reading results from member 0."""
+
+    is_group = True
+
+    def __init__(self, d: int, loss: str = "l2", devices=(0,), emulate: bool | None = None):
+        self.L = _lib.lib()
+        self.d, self.loss, self.mode = int(d), loss, "data"
+        devices = [int(x) for x in devices]
+        if not devices:
+            raise ValueError("devices must name at least one device")
+        if emulate is None:
+            emulate = len(set(devices)) < len(devices)
+        lt = {"l2": _lib.LOSS_L2, "logistic": _lib.LOSS_LOGISTIC}[loss]
+        arr = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        check(self.L.midagma_group_create(C.byref(h), lt, self.d, arr, len(devices),
+                                          _lib.GROUP_EMULATE if emulate else 0), None, "group_create", group=True)
+        self.h = h
+        self.devices = devices
+        self.device = devices[0]
+        self.emulated = bool(self.L.midagma_group_emulated(h))
+        self.members = [HipSolver(self.d, loss, "data", device=dv, _handle=self.L.midagma_group_member(h, k))
+                        for k, dv in enumerate(devices)]
+        self.D = self.members[0].D
+
+    def _check(self, rc, what):
+        return check(rc, self.h, what, group=True)
+
+    def close(self):
+        if getattr(self, "h", None):
+            for m in self.members:
+                m.close()
+            self.L.midagma_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def size(self) -> int:
+        return len(self.members)
+
+    @property
+    def comm_ranks(self) -> int:
+        return 0 if self.emulated else len(self.members)
+
+    # -- data -----------------------------------------------------------------------
+    def set_data(self, X, n_global: int | None = None):
+        """X: the whole host ndarray or torch tensor (n x d, n_global ignored), split by rows over
+        the members (`row_range`).  A tensor's shards are copied to each member's device."""
+        n = int(X.shape[0])
+        if n < self.size:
+            raise ValueError(f"set_data: {n} rows for {self.size} members")
+        if hasattr(X, "data_ptr"):
+            import torch
+            for k, m in enumerate(self.members):
+                lo, hi = row_range(n, self.size, k)
+                part = X[lo:hi].to(torch.device("cuda", m.device)).contiguous()
+                m.set_data(part, n_global=n)
+            return
+        X = _as_f64(X)
+        self._check(self.L.midagma_group_set_data(self.h, X.ctypes.data_as(_lib._dp), n), "group_set_data")
+
+    def set_cov(self, cov):
+        for m in self.members:
+            m.set_cov(cov)
+
+    # fit()'s device data preparation for a device X (on one device; the shards are copied out)
+    def colsum(self, X):
+        return colsum_dev(X)
+
+    def center(self, X, colsum, nrows: float):
+        center_dev(X, colsum, nrows)
+
+    def set_w_float32(self, on: bool):
+        for m in self.members:
+            m.set_w_float32(on)
+
+    def set_masks(self, mask_inc, mask_exc):
+        for m in self.members:
+            m.set_masks(mask_inc, mask_exc)
+
+    def set_trek(self, *a, **k):
+        for m in self.members:
+            m.set_trek(*a, **k)
+
+    def set_trek_tcc(self, *a, **k):
+        for m in self.members:
+            m.set_trek_tcc(*a, **k)
+
+    def allreduce_zbuf(self):
+        """Every member's score buffer <- the sum over the members (RCCL, or the emulated sum)."""
+        self._check(self.L.midagma_group_allreduce_zbuf(self.h), "group_allreduce_zbuf")
+
+    comm_allreduce_zbuf = allreduce_zbuf
+
+    def gram_cov(self, n: float) -> np.ndarray:
+        """cov = (sum_k X_k^T X_k) / n (linear.py:428) from the members' device Gram matrices."""
+        for m in self.members:
+            m.data_gram()
+        self.allreduce_zbuf()
+        for m in self.members:
+            m.cov_from_zbuf(float(n))
+        return self.members[0].get_cov()
+
+    def get_cov(self) -> np.ndarray:
+        return self.members[0].get_cov()
+
+    # -- the loop -------------------------------------------------------------------
+    def minimize(self, W: np.ndarray, mu: float, max_iter: int, s: float, lr: float, tol: float = 1e-6,
+                 beta_1: float = 0.99, beta_2: float = 0.999, lambda1: float = 0.03,
+                 checkpoint: int = 1000, want_checkpoints: bool = False):
+        """linear.py:165-333 over the group; W (d x d float64) updated in place."""
+        assert W.shape == (self.d, self.d) and W.dtype == np.float64 and W.flags.c_contiguous
+        res = _lib.MidagmaResult()
+        self._check(self.L.midagma_group_minimize(self.h, dptr(W), float(mu), int(max_iter), float(s), float(lr),
+                                                  float(tol), float(beta_1), float(beta_2), float(lambda1),
+                                                  int(checkpoint), C.byref(res)), "group_minimize")
+        return MinimizeResult.from_c(res, self.checkpoints() if want_checkpoints else ())
+
+    def checkpoints(self):
+        return self.members[0].checkpoints()
+
+    def h_value(self, W, s: float = 1.0, grad: bool = True):
+        return self.members[0].h_value(W, s, grad)
+
+    def trek_value(self, W, grad: bool = True):
+        return self.members[0].trek_value(W, grad)
+
+    def score_partial(self, W):
+        for m in self.members:
+            m.score_partial(W)
+
+    def score_finish(self):
+        return self.members[0].score_finish()
+
+    def score(self, W):
+        """_score in data mode (linear.py:70-94): every member's partial, summed, finished."""
+        self.score_partial(W)
+        self.allreduce_zbuf()
+        return self.score_finish()
 
 
 def run_allreduce_minimize(backend, W, mu, max_iter, s, lr, tol=1e-6, beta_1=0.99, beta_2=0.999,

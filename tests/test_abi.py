@@ -25,7 +25,7 @@ def test_library_exports_every_symbol():
     L = _lib.load()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.midagma_abi_version() == 10
+    assert L.midagma_abi_version() == 11
 
 
 def test_missing_library_fails_loudly(tmp_path):
@@ -75,3 +75,27 @@ def test_ldfast_entry_points_validate_without_a_device():
     assert L.midagma_ldfast_create(C.byref(out), 0) == -3
     assert L.midagma_ldfast_reset(None) == -3
     assert L.midagma_ldfast_set_counter(None, None) == -3
+
+
+def test_group_entry_points_validate_without_a_device():
+    """ABI 11: the device-group entries refuse bad arguments (and a missing device) before touching
+    a device, with their message from midagma_group_last_error."""
+    import ctypes as C
+    from midagma_amd import _lib
+    L = _lib.load()
+    out = C.c_void_p()
+    devs = (C.c_int * 2)(0, 0)
+    assert L.midagma_group_create(C.byref(out), 0, 10, devs, 0, 0) == -3          # ndev 0
+    assert L.midagma_group_create(C.byref(out), 0, 10, devs, 2, 4) == -3          # unknown flag
+    assert L.midagma_group_create(C.byref(out), 2, 10, devs, 2, 0) == -3          # unknown loss
+    assert b"bad arguments" in L.midagma_group_last_error(None)
+    assert L.midagma_group_size(None) == 0 and L.midagma_group_emulated(None) == 0
+    assert L.midagma_group_member(None, 0) is None
+    assert L.midagma_group_set_data(None, None, 10) == -3
+    assert L.midagma_group_allreduce_zbuf(None) == -3
+    assert L.midagma_group_minimize(None, None, 1.0, 1, 1.0, 3e-4, 1e-6, .99, .999, .03, 1000, None) == -3
+    import torch
+    if not torch.cuda.is_available():
+        # no device: creating a group fails loudly (no CPU path)
+        rc = L.midagma_group_create(C.byref(out), 0, 10, devs, 2, _lib.GROUP_EMULATE)
+        assert rc < 0
