@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--logistic-steps", type=int, default=10)
     p.add_argument("--no-check", action="store_true", help="skip the value checks against the CPU oracle "
                    "(profiling runs)")
+    p.add_argument("--no-group", action="store_true", help="skip the single-process device-group leg (ABI 11: "
+                   "one process drives all N GPUs, DagmaLinear(devices=[...]))")
+    p.add_argument("--group-leg", action="store_true", help=argparse.SUPPRESS)  # the leg's child process
     return p.parse_args()
 
 
@@ -240,12 +243,22 @@ def supervise_ranks(args):
                     "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
                     "verified": False, "error": "every multi-GPU attempt failed (see launch.attempts)"}
             rc = 1
-        line["launch"] = {"supervised": True, "comm_path": attempts[-1]["comm_path"] if line.get("value") else None,
-                          "attempts": attempts,
+        # the path the successful workers report they ran (bench_data's comm["path_kind"]); the
+        # attempts list keeps what each attempt asked for
+        ran = None
+        if line.get("value"):
+            ran = (line.get("comm") or {}).get("path_kind") or attempts[-1]["comm_path"]
+            attempts[-1]["ran"] = ran
+        line["launch"] = {"supervised": True, "comm_path": ran, "attempts": attempts,
                           "note": "each rank process ran its GPU work in a worker child; a failed or stalled "
-                                  "attempt was killed on every rank and the next path started fresh"}
+                                  "attempt was killed on every rank and the next path started fresh; comm_path is "
+                                  "the path the successful workers ran, attempts[].comm_path the one each asked for"}
         if isinstance(line.get("comm"), dict):
-            line["comm"]["path_taken"] = attempts[-1]["comm_path"]
+            line["comm"]["path_taken"] = ran
+        if line.get("value") and not args.no_group and os.environ.get("MIDAGMA_BENCH_SAME_DEVICE") != "1":
+            # the same workload from ONE process driving all the GPUs (ABI 11), now that the
+            # workers are gone; the other ranks wait at the barrier below
+            line["single_process"] = run_group_leg(args, world)
         if line.get("value") and not args.no_cpu and os.path.exists(cov_out):
             cpu = cpu_baseline(args, np.load(cov_out))
             attach_cpu(line, cpu, line["value"])
@@ -444,6 +457,7 @@ def bench_data(args, world, rank, local):
             comm["host_enqueue_ms_per_step"] = sum(host_enqueue) / K * 1e3
         # the rank count the in-library RCCL communicator itself reports (midagma_comm_ranks)
         comm["rccl_ranks"] = s.comm_ranks if lib_comm else None
+        comm["path_kind"] = "library" if lib_comm else "host"
         # W must be bit-identical on every rank: compare (sum, sum of squares) over ranks
         v = np.array([Wf.sum(), (Wf * Wf).sum()])
         t = torch.tensor(np.concatenate([v, -v]), dtype=torch.float64, device=dev)
@@ -474,6 +488,79 @@ def bench_data(args, world, rank, local):
                n_local=n_k, prof=prof, D=s.D, sem_gen_s=t_gen, replicas_identical=replicas, comm=comm,
                W=Wf, cov=cov, steps_total=Wm + K)
     s.close()
+    return out
+
+
+def bench_group(args, ndev):
+    """The headline workload (config 4: d=1000, n=1e6, l2, data mode) from ONE process driving
+    `ndev` GPUs (ABI 11, midagma_amd.solver.HipGroup): member k holds rank k's rows
+    (generated on device k), an RCCL communicator per device from ncclCommInitAll, the score
+    all-reduce captured in each member's slot graphs, one library thread per device.  Timed: one
+    group minimize of --steps Adam steps from W = 0 (mu=1, s=1, lr=3e-4, tol=-1), after a warm-up
+    call that sizes the tables and captures the graphs.  Runs in a child process of its own
+    (`--group-leg`), so its RCCL state is separate from the ranks'."""
+    import torch
+    from midagma_amd.solver import HipGroup
+    d, n, K = args.d, args.n, args.steps
+    shards, t_gen = [], 0.0
+    for k in range(ndev):
+        X, n_k, t = make_shard(d, n, ndev, k, args.seed, torch.device("cuda", k))
+        shards.append(X)
+        t_gen = max(t_gen, t)
+    colsum = sum(X.sum(0).to("cuda:0") for X in shards)     # the global column sums (linear.py:411)
+    for X in shards:
+        X -= (colsum / n).to(X.device)
+    for k in range(ndev):
+        torch.cuda.synchronize(k)
+    t0 = time.perf_counter()
+    g = HipGroup(d, "l2", devices=list(range(ndev)))
+    t_create = time.perf_counter() - t0
+    for k, X in enumerate(shards):
+        g.members[k].set_data(X, n_global=n)
+    del shards, X
+    torch.cuda.empty_cache()
+    W = np.zeros((d, d))
+    # warm-up: tables sized for K steps and the graphs captured (stops at its first checkpoint,
+    # iteration 1: |dobj / 1e16| <= 1e300)
+    g.minimize(W, 1.0, K, 1.0, 3e-4, tol=1e300, lambda1=0.03, checkpoint=1)
+    W = np.zeros((d, d))
+    t0 = time.perf_counter()
+    r = g.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=1000)
+    el = time.perf_counter() - t0
+    out = dict(value=K / el, unit="steps/s", ms_per_step=el / K * 1e3, steps=K, n_gpus=ndev, iters=int(r.iters),
+               verified=bool(r.iters == K and r.success and np.isfinite(W).all()), rccl_ranks=g.comm_ranks,
+               emulated=g.emulated, group_create_s=t_create, sem_gen_s=t_gen,
+               workload=f"config4: d={d}, n={n}, l2, data mode, rows sharded over {ndev} GPU(s) of ONE process",
+               path=("midagma_group (ABI 11): one process, ncclCommInitAll over the devices, the score all-reduce "
+                     "captured in every member's slot graphs, one library thread per device; the members' W bits "
+                     "and states checked equal at the end"),
+               timing="wall clock of one HipGroup.minimize call of `steps` Adam steps (begin, replayed slots, "
+                      "the final W download and replica check included)")
+    g.close()
+    return out
+
+
+def run_group_leg(args, ndev, timeout=None):
+    """bench_group in a child process (no launcher environment): its JSON, or the failure."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "MIDAGMA_BENCH_WORKER",
+                        "MIDAGMA_BENCH_HEARTBEAT")}
+    env.setdefault("NCCL_ALGO", "Ring")
+    cmd = [sys.executable, os.path.abspath(__file__), "--group-leg", "--gpus", str(ndev), "--steps", str(args.steps),
+           "--d", str(args.d), "--n", str(args.n), "--seed", str(args.seed)]
+    timeout = timeout or float(os.environ.get("MIDAGMA_BENCH_GROUP_S", "900"))
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired:
+        return {"verified": False, "error": f"group leg did not finish in {timeout:.0f} s"}
+    js = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not js:
+        return {"verified": False, "error": f"group leg exited {r.returncode}", "stderr_tail": r.stderr[-1500:]}
+    out = json.loads(js[-1])
+    out["child_wall_s"] = round(time.time() - t0, 1)
     return out
 
 
@@ -1359,6 +1446,10 @@ def main():
     if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and os.environ.get("MIDAGMA_BENCH_WORKER") != "1"
             and os.environ.get("MIDAGMA_BENCH_SUPERVISE", "1") == "1"):
         sys.exit(supervise_ranks(args))
+    if args.group_leg:  # run_group_leg's child: one process, every GPU
+        import torch  # noqa: F401
+        print(json.dumps(bench_group(args, args.gpus)), flush=True)
+        return
     import torch
     world, rank, local = setup_dist(args)
     beat("process group up")
@@ -1538,6 +1629,8 @@ def main():
                                         "(cov precomputed; the CPU's own X^T X at n=1e6 not included)")
                 f4["vs_cpu_projected"] = f4["cpu_projected_wall_s"] / f4["wall_s"]
             line["full_fit_config4"] = f4
+        if world == 1 and args.workload == "data" and not args.no_group:
+            line["single_process"] = run_group_leg(args, 1)
         if fit_res is not None:
             fr = dict(fit_res)
             fr["workload"] = f"config2: DagmaLinear('l2').fit(X) defaults, d={d}, n={args.cov_n}, 1 GPU (cov mode)"

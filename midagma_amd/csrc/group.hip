@@ -19,7 +19,13 @@
 //     The members decide identically (same W, same sum), so member 0's state stands for all.
 #include <hip/hip_runtime.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <mutex>
@@ -33,6 +39,30 @@
 namespace {
 
 constexpr int kMaxEmulated = 16;
+
+// diagnostics (MIDAGMA_GROUP_DEBUG=1): stage marks on stderr and a native backtrace on SIGSEGV
+bool gdebug() {
+  static const bool on = std::getenv("MIDAGMA_GROUP_DEBUG") != nullptr;
+  return on;
+}
+void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  fprintf(stderr, "midagma group: signal %d, native backtrace:\n", sig);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+void gmark(const char* what, int k = -1) {
+  if (!gdebug()) return;
+  static bool installed = false;
+  if (!installed) {
+    installed = true;
+    signal(SIGSEGV, segv_trace);
+  }
+  fprintf(stderr, "midagma group: %s %d\n", what, k);
+  fflush(stderr);
+}
 
 struct GroupParts {
   double* p[kMaxEmulated];
@@ -106,46 +136,40 @@ struct midagma_group {
   int loss = 0;
   int64_t d = 0;
   std::string err;
-  // emulated: fork / join events of the combined capture
-  hipEvent_t ev0 = nullptr;
-  std::vector<hipEvent_t> ev;
-
   ~midagma_group() {
-    for (hipEvent_t e : ev)
-      if (e) (void)hipEventDestroy(e);
-    if (ev0) (void)hipEventDestroy(ev0);
     for (midagma_solver* s : m) midagma_destroy(s);  // (each destroys its communicator)
   }
 
   hipStream_t s0() const { return m[0]->stream; }
   int64_t zlen() const { return m[0]->D * m[0]->D + 64; }
 
-  // every member's stream joins member 0's (capture: the other streams enter the capture)
-  void fork() {
-    HIP_TRY(hipEventRecord(ev0, s0()));
-    for (size_t k = 1; k < m.size(); ++k) HIP_TRY(hipStreamWaitEvent(m[k]->stream, ev0, 0));
-  }
-  void join() {
-    for (size_t k = 1; k < m.size(); ++k) {
-      HIP_TRY(hipEventRecord(ev[k], m[k]->stream));
-      HIP_TRY(hipStreamWaitEvent(s0(), ev[k], 0));
-    }
-  }
-  // emulated all-reduce of the members' score buffers, on the joined streams: the fixed-order sum
-  // into member 0's buffer, then copies to the others (each on its own stream)
+  // emulated all-reduce of the members' score buffers, on member 0's stream: the fixed-order sum
+  // into member 0's buffer, then copies to the others
   void enqueue_emulated_allreduce() {
-    join();
     GroupParts parts{};
     parts.n = (int)m.size();
     for (size_t k = 0; k < m.size(); ++k) parts.p[k] = m[k]->zbuf;
     hipLaunchKernelGGL(group_sum_kernel, dim3(1024), dim3(NTHREADS), 0, s0(), parts, zlen());
     HIP_TRY(hipGetLastError());
-    fork();
     for (size_t k = 1; k < m.size(); ++k)
-      HIP_TRY(hipMemcpyAsync(m[k]->zbuf, m[0]->zbuf, (size_t)zlen() * sizeof(double), hipMemcpyDeviceToDevice,
-                             m[k]->stream));
-    join();
+      HIP_TRY(hipMemcpyAsync(m[k]->zbuf, m[0]->zbuf, (size_t)zlen() * sizeof(double), hipMemcpyDeviceToDevice, s0()));
   }
+
+  // every member's work enqueued on member 0's stream (the emulated group's capture; each member's
+  // own side stream still forks from it and joins back, as in a one-solver slot)
+  struct OnStream0 {
+    midagma_group* g;
+    std::vector<hipStream_t> saved;
+    explicit OnStream0(midagma_group* g_) : g(g_) {
+      for (midagma_solver* s : g->m) {
+        saved.push_back(s->stream);
+        s->stream = g->s0();
+      }
+    }
+    ~OnStream0() {
+      for (size_t k = 0; k < g->m.size(); ++k) g->m[k]->stream = saved[k];
+    }
+  };
 
   // runs f(k) for every member on a thread of its own (device k current), joined; the first
   // failure's code (and message, prefixed with the member) is returned
@@ -185,16 +209,19 @@ hipGraphExec_t group_capture(midagma_group* g, const midagma_solver* caller, int
     throw std::logic_error("emulated device group: its slots are driven through the group (midagma_group_minimize)");
   const bool fast = (which & 4) != 0;
   hipGraph_t graph = nullptr;
+  gmark("capture begin", which);
+  // one capturing stream: the members' work in sequence on member 0's stream (a capture that
+  // forked member streams from it and joined them back crashed hipStreamEndCapture on the box,
+  // ROCm 7.2; the emulated group checks arithmetic, not overlap)
+  midagma_group::OnStream0 on(g);
   HIP_TRY(hipStreamBeginCapture(g->s0(), hipStreamCaptureModeThreadLocal));
   try {
     for (int r = 0; r < reps; ++r) {
-      g->fork();
       if (which & 1)
         for (midagma_solver* s : g->m) s->enqueue_part1(fast, passes);
       if ((which & 3) == 3) g->enqueue_emulated_allreduce();
       if (which & 2)
         for (midagma_solver* s : g->m) s->enqueue_part2(fast);
-      g->join();
     }
   } catch (...) {
     (void)hipStreamEndCapture(g->s0(), &graph);
@@ -202,9 +229,11 @@ hipGraphExec_t group_capture(midagma_group* g, const midagma_solver* caller, int
     throw;
   }
   HIP_TRY(hipStreamEndCapture(g->s0(), &graph));
+  gmark("capture ended", which);
   hipGraphExec_t exec = nullptr;
   HIP_TRY(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
   HIP_TRY(hipGraphDestroy(graph));
+  gmark("instantiated", which);
   return exec;
 }
 
@@ -282,9 +311,6 @@ int midagma_group_create(midagma_group** out, int loss, int64_t d, const int* de
   }
   const int rc = gguard(g, [&] {
     if (emulate) {
-      HIP_TRY(hipEventCreateWithFlags(&g->ev0, hipEventDisableTiming));
-      g->ev.assign((size_t)ndev, nullptr);
-      for (int k = 1; k < ndev; ++k) HIP_TRY(hipEventCreateWithFlags(&g->ev[(size_t)k], hipEventDisableTiming));
       for (midagma_solver* s : g->m) s->group = g;
     } else {
       std::vector<void*> comms((size_t)ndev, nullptr);
@@ -366,10 +392,13 @@ int midagma_group_minimize(midagma_group* g, double* W, double mu, int64_t max_i
   if (g->emulated) {
     rc = gguard(g, [&] {
       for (midagma_solver* s : g->m) s->begin(W, mu, max_iter, s_dom, lr, tol, beta1, beta2, lambda1, checkpoint);
+      gmark("begun");
       // the combined graphs bake every member's buffers and settings in: captured afresh per call
       g->m[0]->destroy_graphs();
       g->m[0]->run_loop(max_iter, checkpoint);
+      gmark("loop done");
       for (int64_t k = 0; k < N; ++k) g->m[(size_t)k]->finish(Wk[(size_t)k].data(), &rk[(size_t)k]);
+      gmark("finished");
       return MIDAGMA_OK;
     });
   } else {

@@ -534,7 +534,13 @@ void launch_reduce_check(const double* Mt, const double* W, const double* Z, con
 // trek_val (nullable): the trek regularizer value of this slot's W (PST, trek.hip)
 void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
                     const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
-                    const double* npart, int64_t d, const double* trek_val, hipStream_t stream);
+                    const double* npart, int64_t d, const double* trek_val, hipStream_t stream,
+                    const double* l1_32 = nullptr);
+// float32 W (DagmaLinear(dtype=np.float32)): numpy's float32 np.abs(W).sum() (np_sum.h) into *out on
+// checkpoint slots, for control's objective (linear.py:127); chunk_sums: np_l1_chunks(d) floats
+int64_t np_l1_chunks(int64_t d);
+void launch_np_l1(const double* W, int64_t d, int64_t D, const State* st, float* chunk_sums, double* out,
+                  hipStream_t stream);
 // Z: the score partial, or (zsplit > 1) split-K slices Z + z*zstride summed here in the order
 // of launch_sum_slices.  trek (nullable): weight * trek gradient, added last (linear.py:258).
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,

@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "launch.h"
+#include "np_sum.h"
 #include "mfma64.h"
 #include "tcc_blk.h"
 
@@ -122,7 +123,7 @@ struct SmallCtl {
 struct SmallCtlParams {
   double d_log_s, score_scale, mu, lambda1, trek_weight, tol, s;
   int64_t max_iter, checkpoint;
-  int32_t trek_mode, pad_;
+  int32_t trek_mode, w32;  // w32: float32 W, the objective's float32 terms (step.hip control_kernel)
 };
 
 // The controller: step.hip's control_kernel decisions (linear.py:230-241, 279-331) on the
@@ -161,9 +162,12 @@ __device__ __noinline__ void small_control(const SmallCtlParams& pr_, State& S, 
         nf[f] = x;
       }
       S.ckpt_pending = 0;
-      const double h = -ld + pr->d_log_s;
+      // float32 W: l1 arrives as numpy's float32 sum, lambda1 * l1 and log|det| in float32
+      // (step.hip control_kernel, linear.py:113-114, 127)
+      const double h = pr->w32 ? -f32r(ld) + pr->d_log_s : -ld + pr->d_log_s;
       const double score = pr->score_scale * sd;
-      double obj = pr->mu * (score + pr->lambda1 * l1) + h;
+      const double l1term = pr->w32 ? f32r(f32r(pr->lambda1) * l1) : pr->lambda1 * l1;
+      double obj = pr->mu * (score + l1term) + h;
       const double tv = trek_val ? trek_val[0] : 0.0;
       if (trek_val && pr->trek_mode == 2) obj = obj + pr->trek_weight * tv;  // linear.py:131-133
       if (S.n_ckpt < ckpt_cap) {
@@ -288,6 +292,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   __shared__ double red[3][NW];               // checkpoint objective: (I - W) o Z, |W|, log|pivot|
   __shared__ double nred[NORM_FIELDS][NW];    // the checkpoint step's norms, per wave
   __shared__ int flw[NW];
+  __shared__ float l1img[W32 ? DS * DS : 1];  // float32 W: |W| in numpy's flat order (np_sum.h)
   __shared__ State S;                         // the controller's (thread 0's) state
   __shared__ SmallCtl ctl;                    // its decision for the slot, read by every thread
   // TCC: the body's LDS and the regularizer's state words (scal, v, u), loaded at entry
@@ -314,8 +319,8 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
   __shared__ SmallCtlParams cp;  // (thread 0's)
   __shared__ int64_t next_ck;
   if (tid == 0) {
-    cp = SmallCtlParams{pr->d_log_s, pr->score_scale, pr->mu, pr->lambda1, pr->trek_weight, pr->tol,
-                        pr->s,       pr->max_iter,    pr->checkpoint, pr->trek_mode, 0};
+    cp = SmallCtlParams{pr->d_log_s, pr->score_scale, pr->mu,          pr->lambda1,   pr->trek_weight,
+                        pr->tol,     pr->s,           pr->max_iter,    pr->checkpoint, pr->trek_mode, W32 ? 1 : 0};
     S = *stg;
     next_ck = (S.iter / cp.checkpoint + 1) * cp.checkpoint;
     ctl.run = S.status == ST_RUNNING && n_slots > 0;
@@ -634,6 +639,11 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
           l1 += fabs(wv[e]);
         }
       const double ld = tid < di ? log(fabs(piv[tid])) : 0.0;
+      if constexpr (W32) {
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (real[e]) l1img[rows[e] * di + cols[e]] = fabsf((float)wv[e]);
+      }
       sd = wave_sum(sd);
       l1 = wave_sum(l1);
       const double lds = wave_sum(ld);
@@ -656,6 +666,12 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
     bool norms, more;
     double lr_a, lr_b, bc1, bc2;
     if (!RC || r_ckpt || fl_all) {
+      if constexpr (W32) {  // numpy's float32 np.abs(W).sum() (one chunk: d * d <= 1024)
+        if (tid == 0 && (RC ? r_ckpt : S.ckpt_pending)) {
+          red[1][0] = (double)np_pairwise([&](int64_t f) { return l1img[f]; }, 0, (int64_t)di * di);
+          for (int x = 1; x < NW; ++x) red[1][x] = 0.0;
+        }
+      }
       if (tid == 0)
         small_control<NW>(cp, S, ctl, red, nred, flw, ckpt, ckpt_cap, bc1n, bc2n, TCC ? tsc : nullptr, next_ck);
       __syncthreads();
@@ -940,7 +956,7 @@ void launch_small_minimize(const Params* pr, State* st, double* W, double* m, do
     else
       MIDAGMA_SMALL(32, 4, 0, false);
   } else if (w32) {
-    MIDAGMA_SMALL(64, 16, 0, true);
+    throw std::invalid_argument("small_minimize: a float32 W with 32 < d <= 64 runs on the graph path");
   } else {
     MIDAGMA_SMALL(64, 16, 0, false);
   }

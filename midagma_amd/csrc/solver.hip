@@ -586,6 +586,8 @@ int midagma_set_w_float32(midagma_solver* s, int float32) {
   if (!s) return fail(s, MIDAGMA_E_ARG, "null solver");
   return guarded(s, [&] {
     const bool on = float32 != 0;
+    if (on != s->w32) s->graphs_valid = false;  // the float32 slots carry numpy's L1 sum
+    if (on && !s->l1w.p) s->l1w.alloc((size_t)(1 + (np_l1_chunks(s->d) + 1) / 2));
     if (on && (s->mode == MIDAGMA_MODE_COV || s->loss == MIDAGMA_LOSS_L2) && !s->IW.p) {
       // the score GEMM's I - W (float32 diagonal) comes from build_at, not the GEMM's staging
       s->IW.alloc((size_t)s->D * s->D);

@@ -72,14 +72,16 @@ struct midagma_solver {
   bool cov_at = !knob_set("MIDAGMA_EXP_COV_AMODE0");
   bool cov_iw = knob_set("MIDAGMA_EXP_COV_IW");
   DevBuf npart;  // checkpoint-step norm partials (fused_update -> control)
+  DevBuf l1w;    // float32 W: [0] numpy's float32 L1 sum, then its chunk sums (np_l1_kernel)
   // cov mode, l2, d <= 64, no trek regularizer: the one-workgroup persistent loop (small.hip)
   DevBuf scarry, sprev;  // between two small-loop launches: pending norms + warm count, last inverses
   bool use_small = !knob_set("MIDAGMA_EXP_NO_SMALL");
   bool small_tcc = knob("MIDAGMA_EXP_SMALL_TCC", 1) != 0;  // experiments: 0 keeps TCC on the graph slots
   // (the TCC regularizer runs inside it up to d = 32, tcc_blk.h; PST keeps the graph-replayed slots)
   bool small_on() const {
+    // (float32 W: DS <= 32, whose LDS has room for the float32 |W| image of numpy's L1 sum)
     return use_small && mode == MIDAGMA_MODE_COV && loss == MIDAGMA_LOSS_L2 && small_block(d) > 0 &&
-           (!trek_on || (trek_tcc && small_block(d) <= 32 && small_tcc && !w32));
+           (!w32 || small_block(d) <= 32) && (!trek_on || (trek_tcc && small_block(d) <= 32 && small_tcc && !w32));
   }
   // PST trek regularizer (trek.hip)
   TrekCfg tcfg{};
@@ -176,7 +178,7 @@ struct midagma_solver {
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &nmSync, &npart, &XT, &IW, &scarry,
-                      &sprev, &cupart_ctr})
+                      &sprev, &cupart_ctr, &l1w})
       b->release();
 #ifdef MIDAGMA_EXPERIMENTS
     for (DevBuf* b : {&dfA, &dfY, &dfQ, &dfP, &dfCtl, &dfTasks[0], &dfTasks[1], &dfWoff[0], &dfWoff[1], &dfStamps})
@@ -487,8 +489,12 @@ struct midagma_solver {
   void enqueue_part2(bool fast = false) {
     const bool lean = fast && blocked();
     if (!lean) launch_reduce_check(Mt.p, W.p, zbuf, d_params, d_state, partials.p, d, D, stream);
+    // float32 W: numpy's float32 L1 sum for the checkpoint objective (np_sum.h; checkpoint slots
+    // are never lean)
+    const bool l1f = w32 && l1w.p && !lean;
+    if (l1f) launch_np_l1(W.p, d, D, d_state, reinterpret_cast<float*>(l1w.p + 1), l1w.p, stream);
     launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
-                   trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream);
+                   trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream, l1f ? l1w.p : nullptr);
     const bool slices = lean && mode == MIDAGMA_MODE_COV && cov_split > 1;
     launch_fused_update(d_params, d_state, W.p, m.p, v.p, Mt.p, slices ? cov_parts.p : zbuf,
                         slices ? cov_split : 1, D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr,

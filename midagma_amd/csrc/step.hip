@@ -10,6 +10,7 @@
 // Elementwise arithmetic keeps numpy's operation order; the library is built
 // with -ffp-contract=off so no multiply-add is fused behind our back.
 #include "launch.h"
+#include "np_sum.h"
 
 namespace midagma {
 
@@ -76,6 +77,41 @@ __global__ __launch_bounds__(NTHREADS) void reduce_check_kernel(const double* __
   }
 }
 
+// |W| flattened, numpy's order: 32-bit index arithmetic while d * d fits (the 64-bit division
+// was most of a serial chunk's time)
+struct AbsW32u {
+  const double* W;
+  uint32_t d;
+  int64_t D;
+  __device__ float operator()(int64_t f) const {
+    const uint32_t u = (uint32_t)f;
+    return fabsf((float)W[(int64_t)(u / d) * D + u % d]);
+  }
+};
+
+// np.abs(W).sum() of a float32 W as numpy computes it (np_sum.h), on checkpoint slots of a
+// float32 fit: a thread per 8192-element chunk (numpy's pairwise sum inside it), then the
+// chunks' running float32 total in order.  One workgroup: ~1 ms per checkpoint at d = 1000,
+// checkpoint slots only.
+__global__ __launch_bounds__(1024) void np_l1_kernel(const double* __restrict__ W, int64_t d, int64_t D,
+                                                     const State* __restrict__ st, float* __restrict__ chunk_sums,
+                                                     double* __restrict__ out) {
+  if (st->status != ST_RUNNING || !st->ckpt_pending) return;
+  const int64_t n = d * d, nc = (n + NP_SUM_CHUNK - 1) / NP_SUM_CHUNK;
+  for (int64_t c = threadIdx.x; c < nc; c += blockDim.x) {
+    const int64_t off = c * NP_SUM_CHUNK, len = n - off < NP_SUM_CHUNK ? n - off : NP_SUM_CHUNK;
+    chunk_sums[c] = n < (int64_t(1) << 32) ? np_pairwise(AbsW32u{W, (uint32_t)d, D}, off, len)
+                                           : np_pairwise(AbsW32{W, d, D}, off, len);
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float total = 0.f;
+    for (int64_t c = 0; c < nc; ++c) total += chunk_sums[c];
+    out[0] = (double)total;
+  }
+}
+
 __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restrict__ pr, State* __restrict__ st,
                                                            const double* __restrict__ partials,
                                                            const double* __restrict__ pivlog,
@@ -83,7 +119,8 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
                                                            const double* __restrict__ bc_table,
                                                            CkptRec* __restrict__ ckpt, int64_t ckpt_cap,
                                                            const double* __restrict__ npart, int64_t nnpart,
-                                                           const double* __restrict__ trek_val) {
+                                                           const double* __restrict__ trek_val,
+                                                           const double* __restrict__ l1_32) {
   if (st->status != ST_RUNNING) {
     if (threadIdx.x == 0) st->action = ACT_NOOP;
     return;
@@ -122,9 +159,20 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
   st->flags = 0;
   if (ck) {
     st->ckpt_pending = 0;
-    const double h = -ld + pr->d_log_s;
     const double score = pr->logistic ? loss_total[0] * pr->logit_scale : pr->score_scale * sd;
-    double obj = pr->mu * (score + pr->lambda1 * l1) + h;
+    double h, l1term;
+    if (l1_32) {
+      // float32 W (linear.py:113-114, 127): np.abs(W).sum() is numpy's float32 sum (np_l1_kernel),
+      // lambda1 * it a float32 product (a Python float times a float32 scalar), slogdet's log|det|
+      // a float32 (modelled as the float64 one rounded); score and h come out float64
+      l1 = l1_32[0];
+      l1term = f32r(f32r(pr->lambda1) * l1);
+      h = -f32r(ld) + pr->d_log_s;
+    } else {
+      l1term = pr->lambda1 * l1;
+      h = -ld + pr->d_log_s;
+    }
+    double obj = pr->mu * (score + l1term) + h;
     const double tv = trek_val ? trek_val[0] : 0.0;
     if (pr->trek_mode == 2) obj = obj + pr->trek_weight * tv;  // linear.py:131-133
     if (st->n_ckpt < ckpt_cap) {
@@ -422,10 +470,19 @@ void launch_reduce_check(const double* Mt, const double* W, const double* Z, con
 
 void launch_control(const Params* pr, State* st, const double* partials, const double* pivlog,
                     const double* loss_total, const double* bc_table, CkptRec* ckpt, int64_t ckpt_cap,
-                    const double* npart, int64_t d, const double* trek_val, hipStream_t stream) {
+                    const double* npart, int64_t d, const double* trek_val, hipStream_t stream,
+                    const double* l1_32) {
   const int64_t nnpart = ((d + NTHREADS - 1) / NTHREADS) * d;  // fused_update workgroups
   hipLaunchKernelGGL(control_kernel, dim3(1), dim3(NTHREADS), 0, stream, pr, st, partials, pivlog, loss_total,
-                     bc_table, ckpt, ckpt_cap, npart, nnpart, trek_val);
+                     bc_table, ckpt, ckpt_cap, npart, nnpart, trek_val, l1_32);
+  HIP_TRY(hipGetLastError());
+}
+
+int64_t np_l1_chunks(int64_t d) { return (d * d + NP_SUM_CHUNK - 1) / NP_SUM_CHUNK; }
+
+void launch_np_l1(const double* W, int64_t d, int64_t D, const State* st, float* chunk_sums, double* out,
+                  hipStream_t stream) {
+  hipLaunchKernelGGL(np_l1_kernel, dim3(1), dim3(1024), 0, stream, W, d, D, st, chunk_sums, out);
   HIP_TRY(hipGetLastError());
 }
 

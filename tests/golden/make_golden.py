@@ -270,12 +270,53 @@ def gen_fit_f32(X):
     differ by float32 rounding; the pair bounds the dtype=float32 drop-in."""
     out = {}
     for tag, dt in (("f32", np.float32), ("f64", np.float64)):
-        m = DagmaLinear(loss_type="l2", verbose=False, dtype=dt)
+        calls = []
+        m = _stage_spy(calls)(loss_type="l2", verbose=False, dtype=dt)
         W = m.fit(X.copy(), lambda1=0.03, T=3, s=[1.0, .9, .8], warm_iter=4000, max_iter=5000)
         out[f"W_{tag}"] = W
         out[f"h_final_{tag}"] = np.array(m.h_final)
         out[f"score_final_{tag}"] = np.array(m.score_final)
+        # per minimize call: (mu, s, lr, max_iter, success, iterations) -- the float32 checkpoint
+        # objective decides where each stage stops early (linear.py:113-114, 127, 328-331)
+        out[f"calls_{tag}"] = np.array(calls, dtype=np.float64)
     np.savez_compressed(os.path.join(HERE, "fit_f32_d20.npz"), **out)
+
+
+def _stage_spy(calls):
+    """DagmaLinear recording (mu, s, lr, max_iter, success, iterations) of every minimize call."""
+    class Spy(DagmaLinear):
+        def minimize(self, W, mu, max_iter, s, lr, tol=1e-6, beta_1=0.99, beta_2=0.999, pbar=None):
+            rec = Recorder()
+            Wr, ok = super().minimize(W, mu, max_iter, s, lr, tol, beta_1, beta_2, pbar=rec)
+            calls.append((mu, s, lr, max_iter, ok, rec.iters))
+            return Wr, ok
+    return Spy
+
+
+def gen_fit_f32_default(X, seeds=(7, 11, 13, 17, 19, 23, 29, 31)):
+    """The DEFAULT fit (T=5, warm 3e4, max 6e4) with dtype=np.float32, whose stages stop early on
+    the float32 checkpoint objective (linear.py:113-114, 127, 328-331), with its per-call
+    iteration counts; and the same fit under float32-scale noise in every inverse (NoisyInv32),
+    one run per seed: the range of stage counts the reference's own float32 rounding allows."""
+    calls = []
+    m = _stage_spy(calls)(loss_type="l2", verbose=False, dtype=np.float32)
+    W = m.fit(X.copy(), lambda1=0.03)
+    out = {"W": W, "h_final": np.array(m.h_final), "score_final": np.array(m.score_final),
+           "calls": np.array(calls, dtype=np.float64)}
+    env = []
+    orig = ref_linear.sla
+    for sd in seeds:
+        ref_linear.sla = NoisyInv32(np.random.default_rng(sd))
+        try:
+            c = []
+            _stage_spy(c)(loss_type="l2", verbose=False, dtype=np.float32).fit(X.copy(), lambda1=0.03)
+        finally:
+            ref_linear.sla = orig
+        env.append([x[5] for x in c])
+    n = max(len(e) for e in env)
+    out["env_seeds"] = np.array(seeds)
+    out["env_stage_iters"] = np.array([e + [-1] * (n - len(e)) for e in env], dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "fit_f32_d20_default.npz"), **out)
 
 
 class NoisyInv32(NoisyInv):
@@ -294,11 +335,13 @@ def gen_fit_f32_envelope(X, seeds=(7, 11, 13, 17, 19, 23, 29, 31)):
     (NoisyInv32), one run per seed: the reference's own float32 perturbation envelope, the bar of
     tests/test_gpu_parity.py::test_full_fit_float32_dtype (the GPU's float32 loop inverts in
     float64 and rounds, a different valid float32 inversion)."""
-    rows = {"W": [], "h_final": [], "score_final": []}
+    rows = {"W": [], "h_final": [], "score_final": [], "stage_iters": []}
 
     def one_fit():
-        m = DagmaLinear(loss_type="l2", verbose=False, dtype=np.float32)
+        calls = []
+        m = _stage_spy(calls)(loss_type="l2", verbose=False, dtype=np.float32)
         W = m.fit(X.copy(), lambda1=0.03, T=3, s=[1.0, .9, .8], warm_iter=4000, max_iter=5000)
+        m.stage_iters = [c[5] for c in calls]
         return m, W
 
     orig = ref_linear.sla
@@ -311,6 +354,7 @@ def gen_fit_f32_envelope(X, seeds=(7, 11, 13, 17, 19, 23, 29, 31)):
         rows["W"].append(W.astype(np.float64))
         rows["h_final"].append(float(m.h_final))
         rows["score_final"].append(float(m.score_final))
+        rows["stage_iters"].append(m.stage_iters)
     np.savez_compressed(os.path.join(HERE, "fit_f32_d20_envelope.npz"), seeds=np.array(seeds),
                         **{k: np.array(v, dtype=np.float64) for k, v in rows.items()})
 
@@ -452,6 +496,7 @@ def main():
         gen_fit_envelope(X20)
         gen_fit_f32(X20)
         gen_fit_f32_envelope(X20)
+        gen_fit_f32_default(X20)
         gen_trek()
         gen_tcc(X20)
         gen_mlp()
@@ -465,6 +510,7 @@ if __name__ == "__main__":
             X20 = np.load(os.path.join(HERE, "data_d20_n1000_seed0.npz"))["X"]
             for name in sys.argv[1:]:
                 fn = globals()[name]
-                fn(X20) if name in ("gen_tcc", "gen_mlp_traj", "gen_fit_f32", "gen_fit_f32_envelope") else fn()  # e.g. gen_traj_logistic_d100
+                fn(X20) if name in ("gen_tcc", "gen_mlp_traj", "gen_fit_f32", "gen_fit_f32_envelope",
+                                             "gen_fit_f32_default") else fn()  # e.g. gen_traj_logistic_d100
     else:
         main()

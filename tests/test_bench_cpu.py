@@ -133,7 +133,7 @@ def test_supervised_ranks_fall_back_to_host_path(tmp_path):
     env.pop("MIDAGMA_BENCH_COMM", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", "29581", os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--dim", "20", "--rows", "500"]
+           "--gpus", "2", "--dim", "20", "--rows", "500", "--no-group"]
     t0 = __import__("time").time()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
@@ -144,7 +144,7 @@ def test_supervised_ranks_fall_back_to_host_path(tmp_path):
     assert line["value"] == 2.0
     la = line["launch"]
     assert la["comm_path"] == "host" and line["comm"]["path_taken"] == "host"
-    assert [a["comm_path"] for a in la["attempts"]] == ["library", "host"]
+    assert [a["comm_path"] for a in la["attempts"]] == ["library", "host"] and la["attempts"][1]["ran"] == "host"
     first = la["attempts"][0]
     assert first["failed_ranks"] >= 1
     assert any(x["rank"] == 1 and "exited 3" in x["outcome"] for x in first["ranks"])

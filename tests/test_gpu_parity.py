@@ -197,6 +197,64 @@ def test_full_fit_float32_dtype(hip, golden):
     env_w = float(np.abs(env["W"] - f["W_f32"]).max())
     assert np.array_equal(W != 0, f["W_f32"] != 0)
     assert np.abs(W - f["W_f32"]).max() <= env_w
+    # every call's iteration count (here the stages run to max_iter: no early stop at this length)
+    assert [e["iters"] for e in m.minimize_log] == [int(c[5]) for c in f["calls_f32"]]
+
+
+def test_float32_default_fit_stage_counts_in_envelope(hip, golden):
+    """The default fit with dtype=np.float32 stops its stages early on the float32 checkpoint
+    objective (linear.py:113-114, 127, 328-331): numpy's float32 L1 sum (csrc/np_sum.h, bit for bit),
+    lambda1 times it in float32, log|det| rounded to float32.  Each stage's successful call must take
+    a number of iterations inside the range the reference's own float32 fit and its float32-noise
+    replicas span (fit_f32_d20_default.npz: stage 1 12k-16k, stage 2 7k-8k, stage 3 8k-18k)."""
+    from midagma_amd import DagmaLinear
+    f = golden("fit_f32_d20_default.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    m = DagmaLinear("l2", dtype=np.float32)
+    W = m.fit(X, lambda1=0.03)
+    assert W.dtype == np.float32
+    ok = [e["iters"] for e in m.minimize_log if e["success"]]
+    ref = [int(c[5]) for c in f["calls"] if c[4] == 1]
+    env = f["env_stage_iters"]
+    assert len(ok) == len(ref) == env.shape[1] == 5
+    # stages 1-3; at mu = 1e-3 the reference's unperturbed float32 fit leaves the domain through
+    # negative entries of its float32 getri inverse and retries up to s = 1, which none of its
+    # float32-noise replicas does (tests/test_dtype_cpu.py, DESIGN.md section 2)
+    for i, it in enumerate(ok[:3]):
+        lo, hi = min(ref[i], env[:, i].min()), max(ref[i], env[:, i].max())
+        assert lo <= it <= hi, (i, it, lo, hi, ok)
+
+
+@pytest.mark.parametrize("d,mode", [(20, "cov"), (48, "cov"), (100, "cov"), (300, "cov"), (64, "data")])
+def test_float32_checkpoint_objective(hip, d, mode):
+    """The checkpoint record of a float32 fit holds the reference's float32 objective terms: l1 is
+    numpy's float32 np.abs(W).sum() of that checkpoint's W bit for bit (the small loop's thread-0
+    sum at d <= 32, np_l1_kernel on the graph path), obj = mu (score + f32(f32(lambda1) l1)) + h,
+    and h = -f32(log|det|) + d log s within float32 rounding of the oracle's float32 slogdet."""
+    from midagma_amd.solver import HipSolver
+    n = 1000
+    X, _, _ = make_dataset(d, n, seed=d + 1)
+    Xc = X - X.mean(axis=0, keepdims=True)
+    if mode == "cov":
+        sol = _solver(d, Xc.T @ Xc / n)
+    else:
+        sol = HipSolver(d, "l2", "data", device=0)
+        sol.set_data(Xc, n_global=n)
+        sol.set_cov(Xc.T @ Xc / n)
+    sol.set_w_float32(True)
+    W = np.zeros((d, d))
+    mu, lam = 1.0, 0.03
+    res = sol.minimize(W, mu, 200, 1.0, 3e-4, tol=-1.0, lambda1=lam, checkpoint=100, want_checkpoints=True)
+    sol.close()
+    assert res.iters == 200
+    rec = res.checkpoints[-1]
+    assert rec.iter == 200
+    W32 = W.astype(np.float32)
+    assert rec.l1 == float(np.abs(W32).sum())
+    l1term = float(np.float32(lam) * np.float32(rec.l1))
+    assert rec.obj == mu * (rec.score + l1term) + rec.h
+    h_ref, _ = h_logdet(W32, 1.0)
+    assert abs(rec.h - float(h_ref)) <= 1e-6 * max(1.0, abs(float(h_ref))) + 1e-7
 
 
 @pytest.mark.parametrize("d,K,n", [(20, 1000, 1000), (100, 300, 2000), (300, 100, 1000), (1000, 40, 2000)])

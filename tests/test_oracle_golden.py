@@ -163,3 +163,18 @@ def test_float32_fit_bit_exact(golden):
     env = golden("fit_f32_d20_envelope.npz")
     for Wn in env["W"]:
         assert np.array_equal(Wn != 0, f["W_f32"] != 0)
+
+
+def test_float32_default_fit_bit_exact(golden):
+    """The DEFAULT fit with dtype=np.float32 (fit_f32_d20_default.npz): its stages stop early on the
+    float32 checkpoint objective -- numpy's float32 np.abs(W).sum(), lambda1 times it in float32 and
+    slogdet's float32 log|det| (linear.py:113-114, 127, 328-331) -- and go out of domain and retry
+    at s = 0.7 and 0.6.  The oracle reproduces every call (mu, lr, success, iterations) and W."""
+    f = golden("fit_f32_d20_default.npz")
+    X = golden("data_d20_n1000_seed0.npz")["X"].copy()
+    o = LinearOracle("l2", dtype=np.float32)
+    W = o.fit(X, lambda1=0.03)
+    calls = np.array([(mu, s, lr, 0, tr.success, tr.iters) for (_, mu, s, lr, tr) in o.stages])
+    assert np.array_equal(calls[:, [0, 2, 4, 5]], f["calls"][:, [0, 2, 4, 5]])
+    assert np.array_equal(W, f["W"])
+    assert float(o.h_final) == float(f["h_final"]) and float(o.score_final) == float(f["score_final"])
