@@ -154,319 +154,7 @@ __global__ __launch_bounds__(64 * NW) void nm_pass_kernel(const double* __restri
 }
 
 #ifdef MIDAGMA_EXPERIMENTS
-// ---- 512-wide diagonal blocks (B2 = 512) ------------------------------------------------------
-// The 16 x 16 split-K tiles of the narrower series would run 1024 workgroups at 512, each
-// re-reading the block's 512 x 32 row partials of |Q| for the norm (measured: 43 us a pass).
-// Here 256 workgroups (one per CU) each own a 32 x 32 tile of both products of a pass; wave w
-// takes k in [128 w, 128 w + 128) as 2 x 2 accumulators per product, lane (r, kq) streaming 32
-// contiguous k of its rows (k = 128 w + 32 kq + q; the MFMA's four k slots are the four kq
-// lane groups), in two chunks of 16; the 4 waves' partials are summed in a fixed order in LDS;
-// a tile's row partials cover its 32 columns (16 per block row), so the next pass's norm reads
-// 512 x 16 values per workgroup.
-constexpr int N5 = 512, NT5 = N5 / 32;
-
-// acc[i][j] += A[rows m0 + 16 i ..][k-chunk h] B[k-chunk h][cols n0 + 16 j ..]
-__device__ __forceinline__ void load5_a(const double* __restrict__ A, int64_t lda, int m0, int h, double (&a)[2][16]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t k0 = 128 * w + 32 * (lane >> 4) + 16 * h;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const double* ap = A + (int64_t)(m0 + 16 * i + (lane & 15)) * lda + k0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) a[i][q] = ap[q];
-  }
-}
-__device__ __forceinline__ void load5_b(const double* __restrict__ B, int64_t ldb, int n0, int h, double (&b)[2][16]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t k0 = 128 * w + 32 * (lane >> 4) + 16 * h;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const double* bp = B + k0 * ldb + n0 + 16 * j + (lane & 15);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) b[j][q] = bp[(int64_t)q * ldb];
-  }
-}
-__device__ __forceinline__ void mma5(const double (&a)[2][16], const double (&b)[2][16], dbl4 (&acc)[2][2]) {
-#pragma unroll
-  for (int q = 0; q < 16; ++q)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
-}
-
-// Fixed-order sum of the 4 waves' 32 x 32 partials: thread tid returns the 4 accumulator
-// values of tile (i, j) = ((tid >> 6) >> 1, (tid >> 6) & 1), lane tid & 63 (red: 4096 doubles).
-__device__ __forceinline__ dbl4 sum5(const dbl4 (&acc)[2][2], double* red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) red[((w * 4 + 2 * i + j) * 4 + t) * 64 + lane] = acc[i][j][t];
-  __syncthreads();
-  const int tile = threadIdx.x >> 6;
-  dbl4 out;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    double v = red[((0 * 4 + tile) * 4 + t) * 64 + lane];
-#pragma unroll
-    for (int ww = 1; ww < 4; ++ww) v += red[((ww * 4 + tile) * 4 + t) * 64 + lane];
-    out[t] = v;
-  }
-  __syncthreads();  // red reused
-  return out;
-}
-
-// element t of this thread's tile in the 512 x 512 block
-__device__ __forceinline__ void elem5(int m0, int n0, int t, int& row, int& col) {
-  const int lane = threadIdx.x & 63, tile = threadIdx.x >> 6;
-  row = m0 + 16 * (tile >> 1) + acc_row(lane, t);
-  col = n0 + 16 * (tile & 1) + acc_col(lane);
-}
-
-// row partials of |v| over the tile's 32 columns -> rowpart[row * NT5 + n0 / 32] (rs: 32 doubles)
-__device__ __forceinline__ void row_partials5(const dbl4& v, int m0, int n0, double* __restrict__ rowpart, double* rs) {
-  const int lane = threadIdx.x & 63, tile = threadIdx.x >> 6, i = tile >> 1, j = tile & 1;
-  double s[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) s[t] = row_sum16(abs_or_inf(v[t]));
-  if (j == 1 && acc_col(lane) == 0)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) rs[16 * i + acc_row(lane, t)] = s[t];
-  __syncthreads();
-  if (j == 0 && acc_col(lane) == 0)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int r = 16 * i + acc_row(lane, t);
-      st_wt(rowpart + (int64_t)(m0 + r) * NT5 + n0 / 32, s[t] + rs[r]);
-    }
-}
-
-// ||Q||_inf of the 512-block from its row partials (512 x NT5), widened as inf_norm_rows
-__device__ __forceinline__ double inf_norm5(const double* __restrict__ rowpart, float* red4) {
-  float f = 0.0f;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = (int)threadIdx.x + 256 * h;
-    double v[NT5];
-#pragma unroll
-    for (int t = 0; t < NT5; ++t) v[t] = rowpart[row * NT5 + t];
-    double r = 0.0;
-#pragma unroll
-    for (int t = 0; t < NT5; ++t) r += v[t];
-    f = fmaxf(f, isfinite(r) ? (float)(r * (1.0 + 1e-6)) : INFINITY);
-  }
-  return (double)block_max(f, red4);
-}
-
-// R = I - S X0 for the 512-block (nm_resid_kernel's contract)
-__global__ __launch_bounds__(NTHREADS, 1) void nm5_resid_kernel(const double* __restrict__ S, int64_t lds,
-                                                                const double* __restrict__ Pe,
-                                                                const double* __restrict__ Po,
-                                                                double* __restrict__ Y0, double* __restrict__ Q0,
-                                                                double* __restrict__ part0, int* __restrict__ done,
-                                                                State* __restrict__ st) {
-  if (st->status != ST_RUNNING) return;
-  if (st->ckpt_pending) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
-    return;
-  }
-  __shared__ double red[4096];
-  __shared__ double rs[32];
-  const int wg = blockIdx.x, m0 = (wg / NT5) * 32, n0 = (wg % NT5) * 32;
-  if (wg == 0 && threadIdx.x == 0) *done = 0;
-  const bool odd = (st->slots & 1) != 0;
-  const double* P1 = odd ? Pe : Po;  // slot k-1
-  const double* P2 = odd ? Po : Pe;  // slot k-2
-  const bool extrap = st->warm_run >= 2;
-  dbl4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
-  // every operand load in flight before the first MFMA (one wave per SIMD: the registers allow)
-  double a0[2][16], a1[2][16], b0[2][16], b1[2][16];
-  load5_a(S, lds, m0, 0, a0);
-  load5_b(P1, N5, n0, 0, b0);
-  load5_a(S, lds, m0, 1, a1);
-  load5_b(P1, N5, n0, 1, b1);
-  if (extrap) {
-    double c0[2][16], c1[2][16];
-    load5_b(P2, N5, n0, 0, c0);
-    load5_b(P2, N5, n0, 1, c1);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        b0[j][q] = 2.0 * b0[j][q] - c0[j][q];
-        b1[j][q] = 2.0 * b1[j][q] - c1[j][q];
-      }
-  }
-  mma5(a0, b0, acc);
-  mma5(a1, b1, acc);
-  const dbl4 sum = sum5(acc, red);
-  dbl4 r;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    int row, col;
-    elem5(m0, n0, t, row, col);
-    const int64_t e = (int64_t)row * N5 + col;
-    st_wt(Y0 + e, extrap ? 2.0 * P1[e] - P2[e] : P1[e]);
-    r[t] = (row == col ? 1.0 : 0.0) - sum[t];
-    st_wt(Q0 + e, r[t]);
-  }
-  row_partials5(r, m0, n0, part0, rs);
-}
-
-// Pass p for the 512-block (nm_pass_kernel's contract, no look-ahead tiles)
-__global__ __launch_bounds__(NTHREADS, 1) void nm5_pass_kernel(const double* __restrict__ Y,
-                                                               const double* __restrict__ Q, double* __restrict__ Yn,
-                                                               double* __restrict__ Qn, double* __restrict__ P,
-                                                               const double* __restrict__ part_prev,
-                                                               double* __restrict__ part_next, int* __restrict__ done,
-                                                               int pass, State* __restrict__ st) {
-  if (st->status != ST_RUNNING) return;
-  __shared__ double red[4096];
-  __shared__ double rs[32];
-  __shared__ float red4[4];
-  const int dn = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (dn != 0 && dn < pass) return;
-  const int wg = blockIdx.x, m0 = (wg / NT5) * 32, n0 = (wg % NT5) * 32;
-  // every operand load in flight before the norm reduction (their latency overlaps it)
-  double aY[2][16], aQ[2][16], bQ[2][16], aY1[2][16], aQ1[2][16], bQ1[2][16];
-  load5_a(Y, N5, m0, 0, aY);
-  load5_b(Q, N5, n0, 0, bQ);
-  load5_a(Q, N5, m0, 0, aQ);
-  load5_a(Y, N5, m0, 1, aY1);
-  load5_b(Q, N5, n0, 1, bQ1);
-  load5_a(Q, N5, m0, 1, aQ1);
-  double yold[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    int row, col;
-    elem5(m0, n0, t, row, col);
-    yold[t] = Y[(int64_t)row * N5 + col];
-  }
-  const double rho = inf_norm5(part_prev, red4);
-  if (!(rho <= 0.25)) {
-    if (wg == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
-    return;
-  }
-  const bool last = rho <= 1e-8;  // last factor: P = Y (I + Q)
-  dbl4 ay[2][2], aq[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) ay[i][j] = aq[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
-  mma5(aY, bQ, ay);
-  if (!last) mma5(aQ, bQ, aq);
-  mma5(aY1, bQ1, ay);
-  if (!last) mma5(aQ1, bQ1, aq);
-  const dbl4 yq = sum5(ay, red);
-  if (last) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      int row, col;
-      elem5(m0, n0, t, row, col);
-      st_wt(P + (int64_t)row * N5 + col, yold[t] + yq[t]);
-    }
-    if (wg == 0 && threadIdx.x == 0) __hip_atomic_store(done, pass, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const dbl4 qq = sum5(aq, red);
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    int row, col;
-    elem5(m0, n0, t, row, col);
-    st_wt(Yn + (int64_t)row * N5 + col, yold[t] + yq[t]);
-    st_wt(Qn + (int64_t)row * N5 + col, qq[t]);
-  }
-  row_partials5(qq, m0, n0, part_next, rs);
-}
-
-// Panels of outer step g for 512-wide blocks (binv_panel_kernel's contract): 32 x 32 tiles of
-// U = P Ain[G, j] (j outside G) and V = -Ain[i, G] P (i outside G) on the nm5 tile (K = 512
-// split over the 4 waves, every operand load in flight before the first MFMA); one job per
-// workgroup (the U tiles, then the V tiles; 118 VGPRs: several workgroups per CU), and
-// workgroups 0..15 also copy a 32-row strip of P into Aout's diagonal block and the warm-start
-// store.
-__global__ __launch_bounds__(NTHREADS, 1) void panel5_kernel(const double* __restrict__ Ain,
-                                                             double* __restrict__ Aout, int64_t D, int g,
-                                                             const double* __restrict__ P,
-                                                             double* __restrict__ Pe, double* __restrict__ Po,
-                                                             const int* __restrict__ done, int check,
-                                                             State* __restrict__ st) {
-  if (st->status != ST_RUNNING) return;
-  if (done && *done == 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_NEED_GJ;
-    return;
-  }
-  __shared__ double red[4096];
-  const int64_t G0 = (int64_t)g * N5;
-  const int g32 = g * NT5, mb = (int)(D / 32) - NT5, nu = NT5 * mb;
-  int flag = 0;
-  for (int job = blockIdx.x; job < 2 * nu; job += gridDim.x) {
-    const double* A;
-    const double* B;
-    int64_t lda, ldb, orow, ocol;
-    double sign;
-    if (job < nu) {  // U: rows a of G, 32-block column c outside G
-      const int a = job / mb, cq = job % mb, c = cq < g32 ? cq : cq + NT5;
-      A = P + (int64_t)a * 32 * N5;
-      lda = N5;
-      B = Ain + G0 * D + (int64_t)c * 32;
-      ldb = D;
-      orow = G0 + a * 32;
-      ocol = (int64_t)c * 32;
-      sign = 1.0;
-    } else {  // V: 32-block row i outside G, columns c of G
-      const int j2 = job - nu, iq = j2 / NT5, c = j2 % NT5, i = iq < g32 ? iq : iq + NT5;
-      A = Ain + (int64_t)i * 32 * D + G0;
-      lda = D;
-      B = P + c * 32;
-      ldb = N5;
-      orow = (int64_t)i * 32;
-      ocol = G0 + c * 32;
-      sign = -1.0;
-    }
-    double a0[2][16], a1[2][16], b0[2][16], b1[2][16];
-    load5_a(A, lda, 0, 0, a0);
-    load5_b(B, ldb, 0, 0, b0);
-    load5_a(A, lda, 0, 1, a1);
-    load5_b(B, ldb, 0, 1, b1);
-    dbl4 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
-    mma5(a0, b0, acc);
-    mma5(a1, b1, acc);
-    const dbl4 sum = sum5(acc, red);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      int row, col;
-      elem5(0, 0, t, row, col);
-      const double v = sign * sum[t];
-      st_wt(Aout + (orow + row) * D + ocol + col, v);
-      flag |= domain_flag(v);
-    }
-  }
-  if ((int)blockIdx.x < NT5) {  // P's rows [32 b, 32 b + 32) -> Aout[G, G] and this slot's store
-    double* Pst = (st->slots & 1) ? Po : Pe;
-    const int r0 = (int)blockIdx.x * 32;
-    for (int e = threadIdx.x; e < 32 * N5; e += NTHREADS) {
-      const int row = r0 + e / N5, col = e % N5;
-      const double v = P[(int64_t)row * N5 + col];
-      st_wt(Aout + (G0 + row) * D + G0 + col, v);
-      st_wt(Pst + (int64_t)row * N5 + col, v);
-      flag |= domain_flag(v);
-    }
-  }
-  if (check && flag) atomicOr(&st->flags, flag);
-}
-
+#include "../../experiments/blockinv_exp.inc"
 #endif  // MIDAGMA_EXPERIMENTS
 
 // the next block's series counters (launch_trail128_series), zeroed by the panel launch before

@@ -1460,265 +1460,7 @@ void launch_trail128_series(const double* Ain, double* Aout, int64_t D, int64_t 
 }
 
 #ifdef MIDAGMA_EXPERIMENTS
-// launch_trail128 with C0 read in the epilogue at every B2 (the micro-benchmark's baseline)
-void launch_trail128_band(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
-                          const State* st, hipStream_t stream) {
-  launch_trail128_epi(Ain, Aout, D, B2, g, check, st, stream, false);
-}
-
-// The B2 = 256 trailing update on persistent workgroups (experiments build; tools/micro/trail_micro):
-// each workgroup runs tile after tile of the EPI_SUB_MID body, so a tile's store burst drains under
-// the next tile's K loop instead of at a workgroup boundary.  Static: tile w + k nwg (nwg % 8 == 0
-// keeps each workgroup's tiles on its XCD under xcd_remap); dynamic: tiles claimed from *ctr.
-__global__ __launch_bounds__(NTHREADS, 2) void trail_persist_kernel(const double* __restrict__ Ain,
-                                                                   double* __restrict__ Aout, int64_t D, int g, int tm,
-                                                                   int check, const State* __restrict__ st,
-                                                                   int* __restrict__ ctr) {
-  if (st && st->status != ST_RUNNING) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int claim;
-  const int ntiles = tm * tm;
-  const int64_t G0 = (int64_t)g * 256;
-  for (int i = blockIdx.x;; i += gridDim.x) {
-    int t = i;
-    if (ctr) {
-      __syncthreads();
-      if (threadIdx.x == 0) claim = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      t = claim;
-    }
-    if (t >= ntiles) break;
-    __syncthreads();  // the LDS images of the previous tile
-    gemm_pipe_tile<0, B_PLAIN, EPI_SUB_MID>(xcd_remap(t, ntiles), 256, 256, tm, tm, Ain + G0, D, Aout + G0 * D, D,
-                                            Aout, D, (int64_t)check, const_cast<double*>(Ain), G0 / 128, 2, st, smem);
-  }
-}
-
-void launch_trail128_persist(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, const State* st,
-                             int nwg, int* ctr, hipStream_t stream) {
-  const int tm = (int)((D - 256) / 128);
-  if (D % 128 || tm <= 0 || nwg <= 0 || nwg % 8) throw std::invalid_argument("launch_trail128_persist: bad shape");
-  static bool attr = false;
-  if (!attr) {
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(trail_persist_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmPipeLds));
-    attr = true;
-  }
-  hipLaunchKernelGGL(trail_persist_kernel, dim3((unsigned)std::min(nwg, tm * tm)), dim3(NTHREADS), kGemmPipeLds,
-                     stream, Ain, Aout, D, (int)g, tm, check ? 1 : 0, st, ctr);
-  HIP_TRY(hipGetLastError());
-}
-
-// The pipelined GEMM on the CUs of the first `ses` shader engines of each XCD (experiments build;
-// launch_gemm_cupart).  HW_REG_HW_ID bits 13-15 hold the shader engine (4 per XCD on MI355X, 8 CUs
-// each: tools/micro/hwid_probe.hip).
-template <int AMODE, int BMODE>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_cupart_kernel(int64_t K, int64_t kslice, int tiles_m, int tiles_n,
-                                                                 int ntasks, const double* __restrict__ A, int64_t lda,
-                                                                 const double* __restrict__ B, int64_t ldb,
-                                                                 double* __restrict__ C, int64_t ldc,
-                                                                 int64_t slice_stride, const State* __restrict__ st,
-                                                                 int ses, int* __restrict__ ctr) {
-  if (st && st->status != ST_RUNNING) return;
-  const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
-  if ((int)((hw >> 13) & 7) >= ses) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int claim;
-  for (;;) {
-    __syncthreads();
-    if (threadIdx.x == 0) claim = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int t = claim;
-    if (t >= ntasks) break;
-    gemm_pipe_tile<AMODE, BMODE, EPI_STORE>(t, K, kslice, tiles_m, tiles_n, A, lda, B, ldb, C, ldc, slice_stride,
-                                            nullptr, 0, 0, st, smem);
-  }
-}
-
-void launch_gemm_cupart(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, bool a_trans, const double* B,
-                        int64_t ldb, GemmB bmode, double* C, int64_t ldc, int split, int64_t slice_stride,
-                        const State* st, int ses, int* ctr, hipStream_t stream) {
-  if (M % 128 || N % 128 || K % 16 || split < 1 || ses < 1) throw std::invalid_argument("launch_gemm_cupart: bad shape");
-  const int64_t ktiles16 = K / 16, per16 = (ktiles16 + split - 1) / split;
-  const int nsplit = (int)((ktiles16 + per16 - 1) / per16);
-  const int tm = (int)(M / 128), tn = (int)(N / 128);
-  static int cus = 0;
-  static bool attr = false;
-  if (!cus) {
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(gemm_cupart_kernel<1, B_PLAIN>),
-                          reinterpret_cast<const void*>(gemm_cupart_kernel<1, B_IMINUS>),
-                          reinterpret_cast<const void*>(gemm_cupart_kernel<0, B_PLAIN>),
-                          reinterpret_cast<const void*>(gemm_cupart_kernel<0, B_IMINUS>)})
-      HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmPipeLds));
-    attr = true;
-  }
-  HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(int), stream));
-  const int ntasks = tm * tn * nsplit;
-  const dim3 grid((unsigned)(2 * cus));
-#define MIDAGMA_CP(AM, BM)                                                                                    \
-  hipLaunchKernelGGL((gemm_cupart_kernel<AM, BM>), grid, dim3(NTHREADS), kGemmPipeLds, stream, K, per16 * 16, tm, \
-                     tn, ntasks, A, lda, B, ldb, C, ldc, slice_stride, st, ses, ctr)
-  if (a_trans && bmode == B_PLAIN)
-    MIDAGMA_CP(1, B_PLAIN);
-  else if (a_trans)
-    MIDAGMA_CP(1, B_IMINUS);
-  else if (bmode == B_PLAIN)
-    MIDAGMA_CP(0, B_PLAIN);
-  else
-    MIDAGMA_CP(0, B_IMINUS);
-#undef MIDAGMA_CP
-  HIP_TRY(hipGetLastError());
-}
-
-// Stream-K remainder of the B2 = 256 trailing update (experiments build; launch_trail128_sk).
-struct TrailSkArgs {
-  const double* Ain;
-  double* Aout;
-  int64_t D;
-  int g, tm, check, dp, nsk;
-  double* ws;  // [2 nsk][128 x 128]: slot k = workgroup k's non-final piece, nsk + k its final piece
-  int* flags;  // [nsk]
-  const State* st;
-};
-
-__global__ __launch_bounds__(NTHREADS, 2) void trail_sk_kernel(TrailSkArgs a) {
-  if (a.st && a.st->status != ST_RUNNING) return;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int go;
-  const int ntiles = a.tm * a.tm, b = blockIdx.x;
-  const int64_t G0 = (int64_t)a.g * 256, D = a.D;
-  if (b < a.dp) {  // data-parallel tiles (the product's tile body)
-    gemm_pipe_tile<0, B_PLAIN, EPI_SUB_MID>(xcd_remap(b, ntiles), 256, 256, a.tm, a.tm, a.Ain + G0, D, a.Aout + G0 * D, D,
-                                            a.Aout, D, (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, 2, a.st,
-                                            smem);
-    return;
-  }
-  const int k = b - a.dp;
-  const int64_t It = (int64_t)(ntiles - a.dp) * 16;
-  const int64_t lo = (int64_t)k * It / a.nsk, hi = (int64_t)(k + 1) * It / a.nsk;
-  if (lo >= hi) return;
-  // one piece of tile s (index in the remainder) over K-tiles [k0, k1) into ws slot `slot`
-  auto piece = [&](int s, int k0, int k1, int slot) {
-    const int t = xcd_remap(a.dp + s, ntiles);
-    int bm = t / a.tm, bn = t % a.tm;
-    const int b0 = (int)(G0 / 128);
-    bm += bm >= b0 ? 2 : 0;  // skip the pivot band (launch_trail128's grid)
-    bn += bn >= b0 ? 2 : 0;
-    const double* A = a.Ain + G0 + (int64_t)bm * 128 * D + 16 * k0;
-    const double* B = a.Aout + (G0 + 16 * k0) * D + (int64_t)bn * 128;
-    __syncthreads();  // LDS images of the previous piece
-    gemm_pipe_tile<0, B_PLAIN, EPI_STORE>(0, 16 * (k1 - k0), 16 * (k1 - k0), 1, 1, A, D, B, D,
-                                          a.ws + (int64_t)slot * 128 * 128, 128, 0, nullptr, 0, 0, nullptr, smem);
-  };
-  const int s_end = (int)((hi - 1) / 16);
-  // the piece that does not finish its tile first (so a finisher never waits on a chain)
-  if (hi % 16 != 0) {
-    const int k0 = (int)(lo > 16 * (int64_t)s_end ? lo - 16 * (int64_t)s_end : 0);
-    piece(s_end, k0, (int)(hi - 16 * (int64_t)s_end), k);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.flags + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  // the piece that finishes tile sf (its last K-tile is in [lo, hi)), then the tile's fix-up
-  const int64_t fend = (hi / 16) * 16;
-  if (fend <= lo) return;
-  const int sf = (int)(fend / 16) - 1;
-  const int64_t fst = lo > 16 * (int64_t)sf ? lo : 16 * (int64_t)sf;
-  piece(sf, (int)(fst - 16 * (int64_t)sf), 16, a.nsk + k);
-  // contributors: the workgroups before k whose ranges hold K-tiles 16 sf .. fst - 1
-  int j0 = k;  // (the first is the one whose range holds K-tile 16 sf)
-  while (j0 > 0 && (int64_t)j0 * It / a.nsk > 16 * (int64_t)sf) --j0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int ok = 1;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (int j = j0; j < k && ok; ++j) {
-      while (__hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000) {
-          ok = 0;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int j = j0; j < k; ++j) __hip_atomic_store(a.flags + j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    go = ok;
-  }
-  __syncthreads();
-  if (!go) {
-    if (threadIdx.x == 0 && a.st)
-      __hip_atomic_store(const_cast<int32_t*>(&a.st->status), (int32_t)ST_HANDOFF_TIMEOUT, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int t = xcd_remap(a.dp + sf, ntiles);
-  int bm = t / a.tm, bn = t % a.tm;
-  const int b0 = (int)(G0 / 128);
-  bm += bm >= b0 ? 2 : 0;
-  bn += bn >= b0 ? 2 : 0;
-  int flag = 0;
-  for (int e = threadIdx.x; e < 128 * 64; e += NTHREADS) {  // pairs of columns
-    const int r = e / 64, c = 2 * (e % 64);
-    double2 sum = {0.0, 0.0};
-    for (int j = j0; j < k; ++j) {
-      const double2 p = *reinterpret_cast<const double2*>(a.ws + (int64_t)j * 16384 + r * 128 + c);
-      sum.x += p.x;
-      sum.y += p.y;
-    }
-    const double2 p = *reinterpret_cast<const double2*>(a.ws + (int64_t)(a.nsk + k) * 16384 + r * 128 + c);
-    sum.x += p.x;
-    sum.y += p.y;
-    const int64_t off = ((int64_t)bm * 128 + r) * D + (int64_t)bn * 128 + c;
-    const double2 c0 = *reinterpret_cast<const double2*>(a.Ain + off);
-    const double2 v = double2{c0.x - sum.x, c0.y - sum.y};
-    *reinterpret_cast<double2*>(a.Aout + off) = v;
-    flag |= (v.x + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v.x) ? 0 : 2);
-    flag |= (v.y + 1e-16 < 0.0 ? 1 : 0) | (isfinite(v.y) ? 0 : 2);
-  }
-  if (a.check && flag) atomicOr(const_cast<int32_t*>(&a.st->flags), flag);
-}
-
-void launch_trail128_sk(const double* Ain, double* Aout, int64_t D, int64_t g, bool check, const State* st, int dp,
-                        int nsk, double* ws, int* flags, hipStream_t stream) {
-  const int tm = (int)((D - 256) / 128);
-  if (D % 128 || tm <= 0 || dp < 0 || dp > tm * tm || nsk <= 0 || (dp < tm * tm && (tm * tm - dp) * 16 < nsk))
-    throw std::invalid_argument("launch_trail128_sk: bad shape");
-  static bool attr = false;
-  if (!attr) {
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(trail_sk_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGemmPipeLds));
-    attr = true;
-  }
-  TrailSkArgs a{Ain, Aout, D, (int)g, tm, check ? 1 : 0, dp, dp < tm * tm ? nsk : 0, ws, flags, st};
-  hipLaunchKernelGGL(trail_sk_kernel, dim3((unsigned)(dp + a.nsk)), dim3(NTHREADS), kGemmPipeLds, stream, a);
-  HIP_TRY(hipGetLastError());
-}
-
-// launch_trail128 with the accumulators preloaded from C0 (EPI_SUB_PRE; experiments build only:
-// measured no faster, tools/micro/trail_micro.hip)
-void launch_trail128_pre(const double* Ain, double* Aout, int64_t D, int64_t B2, int64_t g, bool check,
-                         const State* st, hipStream_t stream) {
-  if (D % 128 || B2 % 128) throw std::invalid_argument("launch_trail128_pre: D, B2 must be multiples of 128");
-  const int tm = (int)((D - B2) / 128);
-  if (tm <= 0) return;
-  const int64_t G0 = g * B2;
-  hipLaunchKernelGGL((gemm_pipe_kernel<0, B_PLAIN, EPI_SUB_PRE>), dim3((unsigned)(tm * tm)), dim3(NTHREADS),
-                     kGemmPipeLds, stream, B2, B2, tm, tm, Ain + G0, D, Aout + G0 * D, D, Aout, D,
-                     (int64_t)(check ? 1 : 0), const_cast<double*>(Ain), (int64_t)(G0 / 128), (int64_t)(B2 / 128), st);
-  HIP_TRY(hipGetLastError());
-}
+#include "../../experiments/gemm_exp.inc"
 #endif
 
 // The trailing update of outer step g in two parts (the cov-mode look-ahead, blockinv.hip):

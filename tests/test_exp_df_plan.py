@@ -1,4 +1,4 @@
-"""The one-launch blocked inverse's host plan (csrc/dfinv.hip), checked on the CPU: every
+"""The one-launch blocked inverse's host plan (experiments/dfinv.hip), checked on the CPU: every
 counter a task waits for gets exactly its target number of signals, and the per-workgroup
 task lists finish under random task durations (each workgroup runs its list in order and a
 task starts only when its counters are full) -- the plan cannot deadlock whatever the timing,

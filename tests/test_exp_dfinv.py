@@ -1,4 +1,4 @@
-"""The one-launch (dataflow) blocked inverse of the cov-mode fast slot (csrc/dfinv.hip, an
+"""The one-launch (dataflow) blocked inverse of the cov-mode fast slot (experiments/dfinv.hip, an
 experiment enabled by MIDAGMA_EXP_DF=1: measured slower) against
 the launch-per-phase blocked inverse it replaces (csrc/blockinv.hip, MIDAGMA_EXP_DF=0) and the
 oracle: the same tile products in the same order, so W, the iteration counts and the

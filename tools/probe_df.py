@@ -1,4 +1,4 @@
-"""Per-task timing of the one-launch fast-slot inverse (csrc/dfinv.hip), development tool:
+"""Per-task timing of the one-launch fast-slot inverse (experiments/dfinv.hip), development tool:
 python tools/probe_df.py [d] [passes] -- runs a few cov-mode slots with MIDAGMA_DF_STAMPS set,
 then prints per task type the compute and wait times and the outer steps' timeline of the
 last launch (100 MHz device clock).  The one-launch inverse exists in the experiments build
