@@ -92,16 +92,36 @@ def relaunch_ranks(args):
     supervise their GPU workers themselves (supervise_ranks: the fallback to the host-driven
     all-reduce lives there, so it also covers an external launcher); this wait is only bounded
     (MIDAGMA_BENCH_TOTAL_S, default 2 h)."""
+    import signal
     import subprocess
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     log("launching:", " ".join(cmd))
+    # its own session, so a timeout ends torchrun and its rank supervisors together (the workers
+    # die with their supervisor: _run_worker's parent-death signal)
+    p = subprocess.Popen(cmd, start_new_session=True)
     try:
-        rc = subprocess.run(cmd, timeout=float(os.environ.get("MIDAGMA_BENCH_TOTAL_S", "7200"))).returncode
+        rc = p.wait(timeout=float(os.environ.get("MIDAGMA_BENCH_TOTAL_S", "7200")))
     except subprocess.TimeoutExpired:
         log("bench ranks exceeded MIDAGMA_BENCH_TOTAL_S")
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        p.wait()
         rc = 124
     sys.exit(rc)
+
+
+def _die_with_parent():
+    """preexec_fn of a worker: SIGKILL when its supervisor dies (Linux PR_SET_PDEATHSIG), so a
+    killed supervisor leaves no worker holding a GPU."""
+    try:
+        import ctypes
+        import signal
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGKILL), 0, 0, 0)
+    except Exception:  # noqa: BLE001
+        pass
 
 
 def beat(what):
@@ -122,7 +142,7 @@ def _run_worker(cmd, env, hb, stall, cap, store, key):
     import subprocess
     import threading
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                         start_new_session=True)
+                         start_new_session=True, preexec_fn=_die_with_parent)
     out, err = [], []
 
     def pump(src, keep):

@@ -1004,7 +1004,9 @@ void launch_gemm(int64_t M, int64_t N, int64_t K, const double* A, int64_t lda, 
   hipLaunchKernelGGL((gemm128_kernel<AT, BM, EP>), dim3((unsigned)nwg), dim3(NTHREADS), kGemm128Lds, stream, K, \
                      kslice, tm, tn, A, lda, B, ldb, C, ldc, slice_stride, loss_part, m_valid, n_valid, st)
     if (epi == EPI_SIGMOID) {
-      if (bmode != B_PLAIN || nsplit != 1 || (a_trans && N != K))
+      // (a_trans: the epilogue reads X[m][n] from X^T's row n < N; X^T has D >= N rows, zero past d,
+      // so the k loop may stop short of N as in the pipelined kernel)
+      if (bmode != B_PLAIN || nsplit != 1 || (a_trans && K > N))
         throw std::invalid_argument("launch_gemm: sigmoid form");
       if (a_trans)
         MIDAGMA_GEMM128(true, B_PLAIN, EPI_SIGMOID);

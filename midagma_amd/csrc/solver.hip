@@ -1046,6 +1046,9 @@ extern "C" int midagma_ldfast_enqueue(midagma_ldfast* h, const double* A, int64_
 
 extern "C" int midagma_ldfast_set_counter(midagma_ldfast* h, int64_t* counter) {
   if (!h) return fail(nullptr, MIDAGMA_E_ARG, "ldfast_set_counter: null handle");
+  // a handle without the fast path (d > 256: every step runs the Gauss-Jordan chain, which never
+  // advances the counter) cannot honour the contract: refuse instead of stalling the caller's table
+  if (counter && !h->B) return fail(nullptr, MIDAGMA_E_ARG, "ldfast_set_counter: the handle has no fast path (d > 256)");
   h->counter = counter;
   return MIDAGMA_OK;
 }

@@ -356,7 +356,10 @@ class _SideLogdet:
         self.parts = ld.parts(exact) if ld is not None else int(L.midagma_logdet_h_parts(d))
         self.next = 0
         self.objective = None
-        self.skip = not exact and ctr is not None and not os.environ.get("MIDAGMA_FAST_OBJECTIVE")
+        # (a handle without the fast path runs the chain on every step, whose end never advances
+        # the counter: its steps keep the objective launch, which does)
+        self.skip = (not exact and ctr is not None and (ld is None or ld.has_fast)
+                     and not os.environ.get("MIDAGMA_FAST_OBJECTIVE"))
         if ld is not None:  # (before any part: the handle reads it at the enqueue of its end)
             ld.set_counter(ctr if self.skip else None)
 
@@ -420,6 +423,12 @@ class LdFast:
     def reset(self):
         with torch.cuda.device(self.device):
             _lib.check(self.L.midagma_ldfast_reset(self.h), None, "ldfast_reset")
+
+    @property
+    def has_fast(self) -> bool:
+        """The warm-started fast path exists (d <= 256, include/midagma_hip.h ABI 6); larger d
+        always runs the Gauss-Jordan chain."""
+        return self.d <= 256
 
     def parts(self, exact: bool) -> int:
         return int(self.L.midagma_ldfast_parts(self.h, 1 if exact else 0))
@@ -690,9 +699,12 @@ class DagmaNonlinear:
         # the step closed by one launch (_MlpStep; MIDAGMA_NO_MLP_STEP=1: the separate launches)
         step = None
         if fused and not FUSED_TAIL and not os.environ.get("MIDAGMA_NO_MLP_STEP"):
-            with torch.no_grad():
-                step = _MlpStep(L, self.model, params, exp_avg, exp_avg_sq, table_d, counter, beta1, beta2, eps,
-                                wd)
+            try:
+                with torch.no_grad():
+                    step = _MlpStep(L, self.model, params, exp_avg, exp_avg_sq, table_d, counter, beta1, beta2, eps,
+                                    wd)
+            except ValueError:  # not the four [d, m1, 1] tensors (e.g. a frozen one): separate launches
+                step = None
 
         def body(gate, exact=True):
             for p in params:

@@ -47,14 +47,17 @@ def test_gpus_n_relaunches_as_torchrun_child(bench, monkeypatch):
     seen = {}
 
     class Done:
-        returncode = 3
+        pid = -1
 
-    def fake_run(cmd, **kw):
-        seen["cmd"] = cmd
-        seen["timeout"] = kw.get("timeout")
-        return Done()
+        def __init__(self, cmd, **kw):
+            seen["cmd"] = cmd
+            seen["new_session"] = kw.get("start_new_session")
 
-    monkeypatch.setattr(subprocess, "run", fake_run)
+        def wait(self, timeout=None):
+            seen["timeout"] = timeout
+            return 3
+
+    monkeypatch.setattr(subprocess, "Popen", Done)
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     args = bench.parse()
@@ -66,6 +69,7 @@ def test_gpus_n_relaunches_as_torchrun_child(bench, monkeypatch):
     assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
     assert seen["timeout"] and seen["timeout"] > 0  # the wait is bounded
+    assert seen["new_session"]  # a timeout kills torchrun's whole session
 
 
 def test_oracle_check_child_matches_in_process_oracle(bench):
