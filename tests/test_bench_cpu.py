@@ -156,3 +156,15 @@ def test_supervised_ranks_fall_back_to_host_path(tmp_path):
     cb = line["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and "sample" in cb
     assert line["vs_cpu"] > 0 and line["vs_cpu_reference_algorithm"] > 0
+
+
+def test_profile_roofline_reads_the_committed_summary(bench):
+    """The line's roofline names the newest committed rocprofv3 summary of the data leg (with the
+    bench line that profiled run printed) and the fraction its average GEMM launch implies, next to
+    the live hipEvent figures; another workload has none."""
+    p = bench._profile_roofline(1000, 1_000_000, 1, 1_000_000)
+    assert p is not None and os.path.exists(os.path.join(REPO, p["source"]))
+    assert os.path.exists(os.path.join(REPO, p["line"]))
+    assert abs(p["frac"] - 2e12 / (p["avg_ms"] * 1e-3) / 1e12 / bench.FP64_MFMA_PEAK_TF) < 1e-12
+    assert 0.5 < p["frac"] < 1.0 and p["profiled_ms_per_step"] > 0
+    assert bench._profile_roofline(1000, 1_000_000, 8, 125_000) is None
