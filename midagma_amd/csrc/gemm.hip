@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "binv_tile.h"
+#include "control.h"
 #include "launch.h"
 #include "mfma64.h"
 #include "nm_series.h"
@@ -827,13 +828,23 @@ struct GemmTrailArgs {
   int64_t D;
   int B2, g, check, pf;
   State* st;
+  const Params* pr;         // control folded into the launch (ticket non-null; control.h)
+  const double* bc_table;
+  int* ticket;
 };
 constexpr size_t kGemmTrailLds = (4 * NB * ST * sizeof(double) > kGemmPipeLds) ? 4 * NB * ST * sizeof(double)
                                                                                 : kGemmPipeLds;
 
+// a gated-off launch with the control folded in: the control kernel's NOOP for this slot
+__device__ __forceinline__ bool gemm_trail_gated(const GemmTrailArgs& a) {
+  if (a.st->status == ST_RUNNING) return false;
+  if (a.ticket && blockIdx.x == 0 && threadIdx.x == 0) a.st->action = ACT_NOOP;
+  return true;
+}
+
 template <int AMODE, int BMODE>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_trail_kernel(GemmTrailArgs a) {
-  if (a.st->status != ST_RUNNING) return;
+  if (gemm_trail_gated(a)) return;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   if (b < a.n_gemm) {
@@ -843,6 +854,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_trail_kernel(GemmTrailArgs a
     binv_trail_tile(xcd_spread(b - a.n_gemm, (int)gridDim.x - a.n_gemm), a.Ain, a.Aout, a.D, a.B2, a.g, a.check, a.st,
                     a.pf, smem, smem + NB * ST, smem + 2 * NB * ST, smem + 3 * NB * ST);
   }
+  if (a.ticket) control_fold_tail(a.pr, a.st, a.bc_table, a.ticket);
 }
 
 // experiment knob MIDAGMA_EXP_TRAIL_EPI=1: C0 read in the epilogue at every B2
@@ -863,7 +875,7 @@ struct Gemm2Args {
 template <int AMODE, int BMODE>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_trail128_kernel(Gemm2Args a2) {
   const GemmTrailArgs& a = a2.g;
-  if (a.st->status != ST_RUNNING) return;
+  if (gemm_trail_gated(a)) return;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int b = blockIdx.x;
   if (b < a.n_gemm) {
@@ -882,6 +894,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_trail128_kernel(Gemm2Args a2
                                                (int64_t)a.check, const_cast<double*>(a.Ain), G0 / 128, a.B2 / 128,
                                                a.st, smem);
   }
+  if (a.ticket) control_fold_tail(a.pr, a.st, a.bc_table, a.ticket);
 }
 
 constexpr size_t kGemmLds = (2 * 64 * SB) * sizeof(double);
@@ -1092,6 +1105,10 @@ void launch_gemm_trail(const GemmSpec& gs, const double* Ain, double* Aout, int6
   a.check = check ? 1 : 0;
   a.pf = pf;
   a.st = st;
+  a.pr = gs.ctl_pr;
+  a.bc_table = gs.ctl_table;
+  a.ticket = gs.ctl_ticket;
+  if (a.ticket && (!a.pr || !a.bc_table)) throw std::invalid_argument("launch_gemm_trail: folded control needs pr, table");
   if (n_trail < 0) {
     if (D % 128 || B2 % 128) throw std::invalid_argument("launch_gemm_trail: D, B2 must be multiples of 128");
     Gemm2Args a2{a, (int)((D - B2) / 128), (B2 == 256 && trail_mid()) ? 1 : 0};

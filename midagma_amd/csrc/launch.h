@@ -78,6 +78,11 @@ struct GemmSpec {
   int64_t ldc;
   int split;
   int64_t slice_stride;
+  // launch_gemm_trail only: the fast slot's control folded into the launch (control.h
+  // control_fold_tail; null ticket: a control launch follows instead)
+  const Params* ctl_pr = nullptr;
+  const double* ctl_table = nullptr;
+  int* ctl_ticket = nullptr;
 };
 
 // --- blockinv.hip -----------------------------------------------------------

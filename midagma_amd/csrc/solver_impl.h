@@ -178,7 +178,7 @@ struct midagma_solver {
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &nmSync, &npart, &XT, &IW, &scarry,
-                      &sprev, &cupart_ctr, &l1w})
+                      &sprev, &cupart_ctr, &l1w, &ctl_ticket})
       b->release();
 #ifdef MIDAGMA_EXPERIMENTS
     for (DevBuf* b : {&dfA, &dfY, &dfQ, &dfP, &dfCtl, &dfTasks[0], &dfTasks[1], &dfWoff[0], &dfWoff[1], &dfStamps})
@@ -266,6 +266,7 @@ struct midagma_solver {
   // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
   void enqueue_part1(bool fast = false, int passes = NM_PASSES_RUN) {
     bool gemm_done = false;
+    ctl_folded = false;
     if (cov_fork_on()) {
       // large D, cov mode: the score GEMM (W and cov only) on the main stream beside the inverse
       // on the high-priority side stream, so its tiles fill the CUs the inverse's serial
@@ -299,6 +300,7 @@ struct midagma_solver {
       const bool fuse = fast && mode == MIDAGMA_MODE_COV && cov_split > 1 && fuse_gemm;
       if (fuse) gs = score_cov_spec();
       gemm_done = enqueue_build_inverse(fast, passes, fuse ? &gs : nullptr);
+      ctl_folded = fuse && gemm_done && gs.ctl_ticket != nullptr;
     } else if (forked_inverse()) {
       // fork: the inverse (latency-bound, a few % of the chip) on the side stream, the n x d
       // GEMMs on the main one; joined before anything reads Mt.  With the blocked layout the
@@ -406,6 +408,11 @@ struct midagma_solver {
   }
 #endif
   bool fuse_gemm = knob("MIDAGMA_EXP_FUSE_GEMM", 1) != 0;
+  // the fast cov slot's control decided by the last workgroup of the trailing launch that carries
+  // the score GEMM (control.h; MIDAGMA_EXP_CTL_FOLD=0 launches control_kernel instead)
+  bool ctl_fold = knob("MIDAGMA_EXP_CTL_FOLD", 1) != 0;
+  bool ctl_folded = false;  // set by enqueue_part1 for the enqueue_part2 of the same slot
+  DevBuf ctl_ticket;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
   GemmSpec score_cov_spec() const {
@@ -423,6 +430,11 @@ struct midagma_solver {
     gs.ldc = D;
     gs.split = cov_split;
     gs.slice_stride = D * D;
+    if (ctl_fold && ctl_ticket.p) {
+      gs.ctl_pr = d_params;
+      gs.ctl_table = bc_table.p;
+      gs.ctl_ticket = reinterpret_cast<int*>(ctl_ticket.p);
+    }
     return gs;
   }
 
@@ -493,8 +505,9 @@ struct midagma_solver {
     // are never lean)
     const bool l1f = w32 && l1w.p && !lean;
     if (l1f) launch_np_l1(W.p, d, D, d_state, reinterpret_cast<float*>(l1w.p + 1), l1w.p, stream);
-    launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
-                   trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream, l1f ? l1w.p : nullptr);
+    if (!(lean && ctl_folded))  // (else decided at the end of the slot's last trailing launch)
+      launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
+                     trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream, l1f ? l1w.p : nullptr);
     const bool slices = lean && mode == MIDAGMA_MODE_COV && cov_split > 1;
     launch_fused_update(d_params, d_state, W.p, m.p, v.p, Mt.p, slices ? cov_parts.p : zbuf,
                         slices ? cov_split : 1, D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr,
@@ -714,6 +727,10 @@ struct midagma_solver {
       if (cov_split > 1) cov_parts.alloc((size_t)cov_split * DD);
     }
     if (mode == MIDAGMA_MODE_COV) B2 = binv_block(D);
+    if (mode == MIDAGMA_MODE_COV && B2 > 0) {  // the folded control's workgroup ticket (control.h)
+      ctl_ticket.alloc(1);
+      HIP_TRY(hipMemsetAsync(ctl_ticket.p, 0, sizeof(double), stream));
+    }
     // cov mode: build_at also writes I - W for the score GEMM's plain-B form
     if (mode == MIDAGMA_MODE_COV && ((D % 128 == 0 && cov_iw) || w32)) IW.alloc(DD);
     if (blocked() || data_binv_on()) {

@@ -10,6 +10,7 @@
 // Elementwise arithmetic keeps numpy's operation order; the library is built
 // with -ffp-contract=off so no multiply-add is fused behind our back.
 #include "launch.h"
+#include "control.h"
 #include "np_sum.h"
 
 namespace midagma {
@@ -151,10 +152,7 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
     nf[NF_WMIN] = block_sum_min(nf[NF_WMIN], red);
   }
   if (threadIdx.x != 0) return;
-  if (st->slots == 0) st->t0 = __builtin_amdgcn_s_memrealtime();
-  st->slots += 1;
-  st->warm_valid = 1;  // this slot's GJ pass stored every diagonal-block inverse
-  st->warm_run = st->warm_run < 2 ? st->warm_run + 1 : 2;
+  control_open(st);
   const int flags = st->flags;
   st->flags = 0;
   if (ck) {
@@ -214,38 +212,7 @@ __global__ __launch_bounds__(NTHREADS) void control_kernel(const Params* __restr
       return;
     }
   }
-  if (flags & 2) {
-    st->status = ST_SINGULAR;
-    st->action = ACT_NOOP;
-    return;
-  }
-  if (flags & 1) {  // sI - W∘W is not an M-matrix (linear.py:230-241)
-    if (st->iter == 0 || pr->s <= 0.9) {
-      st->status = ST_FAILED;
-      st->action = ACT_NOOP;
-      return;
-    }
-    st->warm_run = 1;  // W turns back: the last two inverses do not extrapolate the path
-    const double lr_old = st->lr;
-    st->lr = lr_old * .5;
-    st->halvings += 1;
-    st->lr_a = lr_old;
-    st->lr_b = st->lr;
-    if (st->lr <= 1e-16) {
-      st->status = ST_LR_UNDERFLOW;
-      st->action = ACT_REVERT;
-      return;
-    }
-    st->action = ACT_HALVE;
-    return;
-  }
-  const int64_t it = st->iter + 1;
-  st->bc1 = bc_table[2 * (it - 1)];
-  st->bc2 = bc_table[2 * (it - 1) + 1];
-  st->lr_a = st->lr;
-  st->action = ACT_STEP;
-  st->iter = it;
-  if (it % pr->checkpoint == 0 || it == pr->max_iter) st->ckpt_pending = 1;
+  control_decide(pr, st, flags, bc_table);
 }
 
 __device__ __forceinline__ double sign_of(double w) { return w > 0.0 ? 1.0 : (w < 0.0 ? -1.0 : w); }
