@@ -300,13 +300,17 @@ struct TccWork {
   double *x, *y, *u, *z, *vprev, *uprev;  // D2 vectors
   double* part;          // ceil(2d / 64) x D2 transposed-GEMV partials
   double* scal;          // [0] value [1] sigma [2] lower [3] rho [4] u.v+eps [5] u.u+eps [7] breakdown [8] warm
-                         // [9] converged
+                         // [9] converged (this slot) [10] converged (the last completed slot)
   State* gates;          // 1 + TCC_NODA_MAX gate words
 };
 // The TCC penalty of W (value in w.scal[0]) and, in 'opt' mode, weight * d value / d W into
 // Gtrek (D x D), gated like launch_trek_pst.
+// handback (nullable; the launch-chain form, 2d > 128): only `steps` Noda steps are enqueued, and
+// if Noda has not converged by then the slot hands back (handback->status = ST_NEED_GJ, the rest of
+// the TCC sequence gated off): the fast cov slot's short chain, the host re-running the slot with
+// all TCC_NODA_MAX steps (tcc.hip).
 void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, const TccWork& w, const State* st,
-                     double* Gtrek, hipStream_t stream);
+                     double* Gtrek, hipStream_t stream, State* handback = nullptr, int steps = TCC_NODA_MAX);
 
 // --- mlp.hip ----------------------------------------------------------------
 constexpr int64_t MLP_TAIL_MAX_DM = 7936;  // d * m1 the fused DagmaMLP tail stages per row in LDS

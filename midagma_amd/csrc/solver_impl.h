@@ -265,7 +265,7 @@ struct midagma_solver {
   // ---- the slot -----------------------------------------------------------
   // fast: the outer diagonal blocks by the warm-started product form (blocked() only)
   void enqueue_part1(bool fast = false, int passes = NM_PASSES_RUN) {
-    bool gemm_done = false;
+    bool gemm_done = false, trek_done = false;
     ctl_folded = false;
     if (cov_fork_on()) {
       // large D, cov mode: the score GEMM (W and cov only) on the main stream beside the inverse
@@ -294,6 +294,15 @@ struct midagma_solver {
       HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
       gemm_done = true;
     } else if (blocked()) {
+      // TCC ('opt', 2d > 128) on a fast cov slot: first, with a short Noda chain that hands the slot
+      // back when it does not converge in time (the inverse, GEMM and control of the slot are then
+      // no-ops and the host re-runs it with the whole chain); it reads W only, so its place in the
+      // slot does not change any result
+      if (fast && tcc_fast_steps > 0 && trek_on && trek_tcc && tcfg.mode == 2 && 2 * d > 128 &&
+          mode == MIDAGMA_MODE_COV) {
+        launch_trek_tcc(W.p, d, D, ccfg, cw, d_state, Gtrek.p, stream, d_state, tcc_fast_steps);
+        trek_done = true;
+      }
       // cov fast slot: the score GEMM rides in the last trailing update's launch (its split-K
       // slices are what fused_update sums anyway); MIDAGMA_EXP_FUSE_GEMM=0 keeps it apart
       GemmSpec gs{};
@@ -333,7 +342,7 @@ struct midagma_solver {
     }
     // trek regularizer of this slot's W (linear.py:251-258): every slot in 'opt' mode; in 'log'
     // mode only checkpoint slots, which are never fast slots
-    if (trek_on && (tcfg.mode == 2 || !(fast && blocked()))) {
+    if (trek_on && !trek_done && (tcfg.mode == 2 || !(fast && blocked()))) {
       if (trek_tcc)
         launch_trek_tcc(W.p, d, D, ccfg, cw, d_state, Gtrek.p, stream);
       else
@@ -412,6 +421,10 @@ struct midagma_solver {
   // the score GEMM (control.h; MIDAGMA_EXP_CTL_FOLD=0 launches control_kernel instead)
   bool ctl_fold = knob("MIDAGMA_EXP_CTL_FOLD", 1) != 0;
   bool ctl_folded = false;  // set by enqueue_part1 for the enqueue_part2 of the same slot
+  // TCC on fast cov slots (2d > 128): Noda steps enqueued before the slot hands back (the full
+  // TCC_NODA_MAX on pivoted slots); a warm-started slot converges in 2-3.
+  // MIDAGMA_EXP_TCC_FAST_STEPS=0: every slot runs the whole gated chain
+  int tcc_fast_steps = (int)knob("MIDAGMA_EXP_TCC_FAST_STEPS", 5);
   DevBuf ctl_ticket;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)

@@ -24,6 +24,7 @@
 // Every kernel obeys a gate word: gate 0 (this slot runs: every slot in 'opt' mode,
 // checkpoint slots in 'log' mode), gates 1..TCC_NODA_MAX (Noda step k runs; the update kernel
 // turns the later ones off on convergence), so the sequence is graph-capturable.
+#include <algorithm>
 #include <cmath>
 #include <type_traits>
 
@@ -108,7 +109,9 @@ __global__ void tcc_init_kernel(const double* __restrict__ vprev, double* __rest
   }
   mn = wg_reduce(mn, sh, Min());
   mx = wg_reduce(mx, sh, Max());
-  const bool warm = scal[8] != 0.0 && scal[9] != 0.0 && mn > 1e-8 * mx && isfinite(mx);
+  // (scal[10]: the last completed slot's converged flag; scal[9] is this slot's, cleared by
+  // tcc_sigma0_kernel, so a slot handed back part-way still warm-starts its re-run)
+  const bool warm = scal[8] != 0.0 && scal[10] != 0.0 && mn > 1e-8 * mx && isfinite(mx);
   for (int64_t i = threadIdx.x; i < n; i += EB) x[i] = warm ? vprev[i] : 1.0;
 }
 
@@ -271,6 +274,7 @@ __global__ void tcc_value_kernel(const double* __restrict__ u, const double* __r
       scal[4] = uv + eps;  // u^T v + eps
       scal[5] = uu + eps;  // u^T u + eps
       scal[8] = 1.0;       // warm start available
+      scal[10] = scal[9];  // ... from a converged iteration
     } else {
       // no Perron gap at all (W o W and S nilpotent, e.g. W = 0 at a fit's start): the shifted
       // inverses overflow.  Value 0 and, through infinite denominators, gradient 0 -- the
@@ -325,10 +329,20 @@ __global__ __launch_bounds__(NB * NB) void tcc_blk_kernel(const double* __restri
 
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + EB - 1) / EB, 2048); }
 
+
+// a truncated chain (launch_trek_tcc's handback form): Noda still running after `steps` steps
+// (its gate for step `steps` not turned off) hands the slot back and gates off the final part
+__global__ void tcc_handback_kernel(State* __restrict__ st, State* __restrict__ gates, int steps) {
+  if (threadIdx.x != 0) return;
+  if (gates[0].status != ST_RUNNING || gates[1 + steps].status != ST_RUNNING) return;
+  st->status = ST_NEED_GJ;
+  gates[0].status = ST_DONE;
+}
+
 }  // namespace
 
 void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, const TccWork& w, const State* st,
-                     double* Gtrek, hipStream_t stream) {
+                     double* Gtrek, hipStream_t stream, State* handback, int steps) {
   const int64_t n = 2 * d, D2 = w.D2;
   static const bool chain = knob_set("MIDAGMA_EXP_TCC_CHAIN");  // experiments: the launch sequence at every d
   if (n <= 128 && !chain) {
@@ -363,7 +377,8 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.vprev, w.x, n, w.scal, g0);
   hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 0, w.x, w.y, g0);
   hipLaunchKernelGGL(tcc_sigma0_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, g0);
-  for (int k = 0; k < TCC_NODA_MAX; ++k) {
+  const int nsteps = handback ? std::min(std::max(steps, 1), TCC_NODA_MAX - 1) : TCC_NODA_MAX;
+  for (int k = 0; k < nsteps; ++k) {
     const State* gk = &w.gates[1 + k];
     hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, w.Mi, n, D2, w.scal, 0.0,
                        gk);
@@ -372,6 +387,7 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
     hipLaunchKernelGGL(tcc_noda_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, w.gates, k, TCC_NODA_MAX,
                        gk);
   }
+  if (handback) hipLaunchKernelGGL(tcc_handback_kernel, dim3(1), dim3(64), 0, stream, handback, w.gates, nsteps);
   // final inverse just above the converged root: two sweeps for v, two (transposed) for u
   hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, w.Mi, n, D2, w.scal, 1e-14,
                      g0);

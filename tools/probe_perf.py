@@ -78,7 +78,8 @@ def trek_case(d, seq, K):
     s.run_slots(K)
     s.sync()
     dt = time.perf_counter() - t0
-    print(f"cov+{'TCC' if seq == 'tcc' else 'PST-' + seq} d={d}: {K / dt:.1f} steps/s ({dt / K * 1e3:.3f} ms/step)", flush=True)
+    print(f"cov+{'TCC' if seq == 'tcc' else 'PST-' + seq} d={d}: {K / dt:.1f} steps/s ({dt / K * 1e3:.3f} ms/step)"
+          f" hand-backs {s.debug_handbacks()}", flush=True)
     s.close()
 
 
@@ -118,6 +119,13 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_FUSE_GEMM={f}", end=" ")
                 cov_case(d, 2 * d, 10, K)
         os.environ.pop("MIDAGMA_EXP_FUSE_GEMM")
+    if which == "tccfast":  # TCC (2d > 128): the fast slots' short Noda chain with hand-back, or the whole gated chain
+        for d in [int(x) for x in sys.argv[2:]] or [100, 300, 1000]:
+            for f in ("5", "0", "4", "3"):
+                os.environ["MIDAGMA_EXP_TCC_FAST_STEPS"] = f
+                print(f"MIDAGMA_EXP_TCC_FAST_STEPS={f}", end=" ")
+                trek_case(d, "tcc", 300 if d <= 300 else 60)
+        os.environ.pop("MIDAGMA_EXP_TCC_FAST_STEPS")
     if which == "ctlfold":  # the fast cov slot's control in the last trailing launch, or its own launch
         for d, K in ((1000, 3000), (500, 3000), (1400, 1000), (2000, 300)):
             for f in ("1", "0", "1", "0"):
