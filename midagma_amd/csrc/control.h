@@ -57,14 +57,17 @@ __device__ inline void control_decide(const Params* pr, State* st, int flags, co
 // launch's workgroups ORed into st->flags and decides.  *ticket counts the launch's workgroups
 // (reset by the last).  A pending checkpoint never reaches a fast slot (the host runs those on
 // the pivoted path); if one did, the slot hands back (ST_NEED_GJ) instead of deciding.
+// No release fence: an agent-scope fence writes the XCD's L2 back (measured: 229 -> 246 us a slot
+// at d = 1000 with one per workgroup).  The only data the decision reads from this launch are the
+// domain flags, which arrive by device-scope atomics like the ticket itself; __syncthreads and the
+// wait below retire this workgroup's atomicOr before its ticket.
 __device__ inline void control_fold_tail(const Params* pr, State* st, const double* bc_table, int* ticket) {
   __syncthreads();
   if (threadIdx.x != 0) return;
-  __threadfence();
-  if (atomicAdd(ticket, 1) != (int)gridDim.x - 1) return;
-  __threadfence();
-  atomicExch(ticket, 0);
-  const int flags = atomicExch(&st->flags, 0);  // (from L2: the other workgroups' atomicOr)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (__hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (int)gridDim.x - 1) return;
+  __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int flags = __hip_atomic_exchange(&st->flags, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (st->ckpt_pending) {
     st->status = ST_NEED_GJ;
     st->action = ACT_NOOP;

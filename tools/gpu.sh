@@ -24,7 +24,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 
 leg_args() {
-  local skip="--no-cpu --no-check --no-fit --no-fit4 --no-cov --no-large --no-mlp --no-logistic --no-small --no-tcc"
+  local skip="--no-cpu --no-check --no-fit --no-fit4 --no-cov --no-large --no-mlp --no-logistic --no-small --no-tcc --no-group"
   case "$1" in
     data)     echo "--steps 5 --warmup 1 ${skip}" ;;
     cov)      echo "--workload cov --cov-steps 2000 --no-cpu --no-check --no-fit --no-fit4 --no-large" ;;
