@@ -623,6 +623,17 @@ extern "C" int midagma_debug_spoil_warm(midagma_solver* s) {
   });
 }
 extern "C" int64_t midagma_debug_handbacks(const midagma_solver* s) { return s ? s->handback_count : -1; }
+// Test hook (not in the public header): the Noda steps a fast cov slot's TCC chain enqueues before
+// it hands back (0: the whole gated chain on every slot; < 0: no change).  Returns the old value.
+extern "C" int midagma_debug_tcc_fast_steps(midagma_solver* s, int steps) {
+  if (!s) return -1;
+  const int old = s->tcc_fast_steps;
+  if (steps >= 0 && steps != old) {
+    s->tcc_fast_steps = steps;
+    s->graphs_valid = false;
+  }
+  return old;
+}
 
 // Diagnostics of the fast blocked inverse (not in the public header): per outer block g,
 // out[g*(NM_PASSES+2) + 0] = done word, out[... + 1 + p] = ||Q_p||_inf of pass p (stale for

@@ -237,6 +237,13 @@ class HipSolver:
         fn.restype, fn.argtypes = C.c_int, [C.c_void_p]
         check(fn(self.h), self.h, "debug_spoil_warm")
 
+    def debug_tcc_fast_steps(self, steps: int | None = None) -> int:
+        """Test hook: the Noda steps a fast cov slot's TCC chain runs before handing the slot back
+        (0: the whole gated chain on every slot; None: leave it).  Returns the previous value."""
+        fn = self.L.midagma_debug_tcc_fast_steps
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_int]
+        return int(fn(self.h, -1 if steps is None else int(steps)))
+
     def debug_handbacks(self) -> int:
         """Test hook: the hand-backs the slot scheduler has re-run on the pivoted path so far."""
         fn = self.L.midagma_debug_handbacks

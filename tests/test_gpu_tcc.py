@@ -138,3 +138,35 @@ def test_dagma_linear_tcc_fit_runs(golden):
     obj, sc, h, tv = m._func(Wd, 0.1, 1.0)
     v_ref, _ = tcc_value_grad(Wd, pairs)   # the loop ignores cycle_penalty / version (notreks.py:691)
     assert abs(tv - v_ref) <= 1e-10 * abs(v_ref)
+
+
+@pytest.mark.parametrize("d", [100, 300])
+def test_tcc_short_chain_hands_back(d):
+    """TCC with 2d > 128 on fast cov slots runs a short Noda chain first in the slot and hands the
+    slot back when it has not converged (tcc.hip tcc_handback_kernel): the re-run is a pivoted slot
+    with the whole chain, warm-started as before.  Forced to hand back nearly every slot (1 step), by
+    default (5 steps), and with the whole chain on every slot (0): W after 60 steps within 1e-9 of
+    the oracle each time."""
+    from midagma_amd.simulate import make_dataset
+    X, _, _ = make_dataset(d, 2 * d, seed=7)
+    rng = np.random.default_rng(7)
+    iu = np.array(np.triu_indices(d, 1)).T
+    pairs = iu[rng.uniform(size=len(iu)) < 0.3]
+    o = LinearOracle("l2")
+    o.prepare(X.copy(), 0.03, 1000)
+    o.trek = dict(kind="tcc", pairs=pairs, mode="opt", weight=0.2)
+    K = 60
+    Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
+    backs = {}
+    for steps in (1, None, 0):
+        s = _solver(d, o.cov)
+        if steps is not None:
+            s.debug_tcc_fast_steps(steps)
+        s.set_trek_tcc(pairs, mode="opt", weight=0.2)
+        W = np.zeros((d, d))
+        res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=1000)
+        backs[steps] = s.debug_handbacks()
+        s.close()
+        assert res.iters == K
+        assert np.abs(W - Wr).max() <= 1e-9, (steps, np.abs(W - Wr).max())
+    assert backs[1] >= K // 3  # forced: most fast slots handed back
