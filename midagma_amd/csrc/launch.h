@@ -302,6 +302,11 @@ struct TccWork {
   double* scal;          // [0] value [1] sigma [2] lower [3] rho [4] u.v+eps [5] u.u+eps [7] breakdown [8] warm
                          // [9] converged (this slot) [10] converged (the last completed slot)
   State* gates;          // 1 + TCC_NODA_MAX gate words
+  // the two-level blocked inverse's buffers for D2 (pivoted path: Aalt D2 x D2, Pst / Pst1 D2 x B2);
+  // null: the flat Gauss-Jordan
+  double* Aalt = nullptr;
+  double* Pst = nullptr;
+  double* Pst1 = nullptr;
 };
 // The TCC penalty of W (value in w.scal[0]) and, in 'opt' mode, weight * d value / d W into
 // Gtrek (D x D), gated like launch_trek_pst.

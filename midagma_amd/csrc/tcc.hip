@@ -330,6 +330,23 @@ __global__ __launch_bounds__(NB * NB) void tcc_blk_kernel(const double* __restri
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + EB - 1) / EB, 2048); }
 
 
+// the shifted inverse: the two-level blocked one (pivoted path: 256-blocks, panels, MFMA trailing
+// updates) where the solver allocated its buffers (2d >= 512), else the flat 32-block Gauss-Jordan
+BInvWork tcc_binv(const TccWork& w) {
+  BInvWork b{};
+  b.Aalt = w.Aalt;
+  b.Pst = w.Pst;
+  b.Pst1 = w.Pst1;
+  return b;
+}
+double* tcc_inv_input(const TccWork& w) { return w.Aalt ? binv_build_target(w.Mi, w.D2, tcc_binv(w)) : w.Mi; }
+void tcc_inverse(const TccWork& w, const GJWork& gj, const State* gate, hipStream_t stream) {
+  if (w.Aalt)
+    launch_blocked_inverse(w.Mi, w.D2, tcc_binv(w), /*fast=*/false, gj, const_cast<State*>(gate), stream);
+  else
+    launch_gj_inverse(w.Mi, w.D2, w.D2, gj, gate, stream);
+}
+
 // a truncated chain (launch_trek_tcc's handback form): Noda still running after `steps` steps
 // (its gate for step `steps` not turned off) hands the slot back and gates off the final part
 __global__ void tcc_handback_kernel(State* __restrict__ st, State* __restrict__ gates, int steps) {
@@ -380,18 +397,18 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   const int nsteps = handback ? std::min(std::max(steps, 1), TCC_NODA_MAX - 1) : TCC_NODA_MAX;
   for (int k = 0; k < nsteps; ++k) {
     const State* gk = &w.gates[1 + k];
-    hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, w.Mi, n, D2, w.scal, 0.0,
-                       gk);
-    launch_gj_inverse(w.Mi, D2, D2, gj, gk, stream);
+    hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
+                       w.scal, 0.0, gk);
+    tcc_inverse(w, gj, gk, stream);
     hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gk);
     hipLaunchKernelGGL(tcc_noda_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, w.gates, k, TCC_NODA_MAX,
                        gk);
   }
   if (handback) hipLaunchKernelGGL(tcc_handback_kernel, dim3(1), dim3(64), 0, stream, handback, w.gates, nsteps);
   // final inverse just above the converged root: two sweeps for v, two (transposed) for u
-  hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, w.Mi, n, D2, w.scal, 1e-14,
-                     g0);
-  launch_gj_inverse(w.Mi, D2, D2, gj, g0, stream);
+  hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
+                     w.scal, 1e-14, g0);
+  tcc_inverse(w, gj, g0, stream);
   for (int r = 0; r < 2; ++r) {
     hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, g0);
     hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.x, n, g0);

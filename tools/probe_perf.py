@@ -126,6 +126,13 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_TCC_FAST_STEPS={f}", end=" ")
                 trek_case(d, "tcc", 300 if d <= 300 else 60)
         os.environ.pop("MIDAGMA_EXP_TCC_FAST_STEPS")
+    if which == "tccbinv":  # TCC (2d >= 512): the shifted inverses on the blocked inverse, or the flat Gauss-Jordan
+        for d in [int(x) for x in sys.argv[2:]] or [300, 1000]:
+            for f in ("1", "0", "1", "0"):
+                os.environ["MIDAGMA_EXP_TCC_BINV"] = f
+                print(f"MIDAGMA_EXP_TCC_BINV={f}", end=" ")
+                trek_case(d, "tcc", 300 if d <= 300 else 60)
+        os.environ.pop("MIDAGMA_EXP_TCC_BINV")
     if which == "ctlfold":  # the fast cov slot's control in the last trailing launch, or its own launch
         for d, K in ((1000, 3000), (500, 3000), (1400, 1000), (2000, 300)):
             for f in ("1", "0", "1", "0"):
