@@ -607,7 +607,7 @@ static bool resid_lookahead() {
 // domain check) after rest(K2-2).  Every tile is computed by the same body as launch_trail128.
 static bool blocked_inverse_lookahead(double* Mt, int64_t D, int B2, const BInvWork& bw, State* st,
                                       hipStream_t stream, int passes, const GemmSpec* fuse,
-                                      const TrailLookAhead& la) {
+                                      const TrailLookAhead& la, double* ain0) {
   const int K2 = (int)(D / B2), gb = B2 / NB, mb = (int)(D / NB) - gb;
   double* bufs[2] = {binv_build_target(Mt, D, bw), nullptr};
   bufs[1] = bufs[0] == Mt ? bw.Aalt : Mt;
@@ -617,7 +617,7 @@ static bool blocked_inverse_lookahead(double* Mt, int64_t D, int B2, const BInvW
   HIP_TRY(hipEventRecord(ev[0], stream));
   HIP_TRY(hipStreamWaitEvent(side, ev[0], 0));
   for (int g = 0; g < K2; ++g) {
-    double* Ain = bufs[g & 1];
+    double* Ain = g == 0 && ain0 ? ain0 : bufs[g & 1];
     double* Aout = bufs[(g + 1) & 1];
     const int64_t G0 = (int64_t)g * B2;
     double* Pe = bw.Pst + (int64_t)g * B2 * B2;
@@ -665,13 +665,13 @@ void launch_build_resid0(const double* W, int64_t ldw, double* At, int64_t D, in
 
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes, const GemmSpec* fuse, const TrailLookAhead* tla,
-                            bool resid0_done) {
+                            bool resid0_done, double* ain0) {
   bool fused = false;
   const int B2 = binv_block(D);
   if (B2 == 0) throw std::invalid_argument("blocked inverse needs D >= 256, D % 128 == 0");
   const int K2 = (int)(D / B2), gb = B2 / NB, mb = (int)(D / NB) - gb;
   if (fast && tla && K2 >= 2 && D - B2 >= TRAIL128_MIN && (B2 == 256 || B2 == 128))
-    return blocked_inverse_lookahead(Mt, D, B2, bw, st, stream, passes, fuse, *tla);
+    return blocked_inverse_lookahead(Mt, D, B2, bw, st, stream, passes, fuse, *tla, ain0);
   double* bufs[2] = {binv_build_target(Mt, D, bw), nullptr};
   bufs[1] = bufs[0] == Mt ? bw.Aalt : Mt;
   // look-ahead residual (NmLA / TrailLA): fast path with 32 x 32 trailing updates
@@ -681,7 +681,7 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
   // ... and their panels too (the default 32 x 32 panel only)
   const int tpan = tser && D < panel64_min() ? trail_panel_workers(D) : 0;  // (< 0: band order only)
   for (int g = 0; g < K2; ++g) {
-    double* Ain = bufs[g & 1];
+    double* Ain = g == 0 && ain0 ? ain0 : bufs[g & 1];
     double* Aout = bufs[(g + 1) & 1];
     const int64_t G0 = (int64_t)g * B2;
     double* Pe = bw.Pst + (int64_t)g * B2 * B2;

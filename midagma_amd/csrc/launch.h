@@ -130,9 +130,12 @@ struct TrailLookAhead {
   hipEvent_t* ev;
 };
 // resid0_done (fast path, B2 = 256): outer block 0's residual already ran in launch_build_resid0.
+// ain0 (nullable; fast path): outer step 0 reads A from here instead of binv_build_target (the
+// A^T that the previous slot's fused_update_at wrote; only read)
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes = NM_PASSES_RUN, const GemmSpec* fuse = nullptr,
-                            const TrailLookAhead* tla = nullptr, bool resid0_done = false);
+                            const TrailLookAhead* tla = nullptr, bool resid0_done = false,
+                            double* ain0 = nullptr);
 #ifdef MIDAGMA_EXPERIMENTS
 // launch_build_at(W, ldw, square, binv_build_target(...), D, d, 0, pr, st, stream) and the fast
 // blocked inverse's outer block 0 residual (S read from W) in one launch; B2 = 256 only
@@ -560,6 +563,12 @@ void launch_np_l1(const double* W, int64_t d, int64_t D, const State* st, float*
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
                          const double* minc, const double* mexc, const double* trek, int64_t d, int64_t D,
                          double* npart, hipStream_t stream);
+// fused_update (never a checkpoint step) plus the next slot's build_at from the new W: A0 =
+// s I - (W o W)^T (outer step 0's input, launch_blocked_inverse ain0) and IW = I - W; D % 32 == 0
+void launch_fused_update_at(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt,
+                            const double* Z, int zsplit, int64_t zstride, const double* cov, const double* minc,
+                            const double* mexc, const double* trek, int64_t d, int64_t D, double* A0, double* IW,
+                            hipStream_t stream);
 // *flag (device int) <- 1 if any of x[0..n) is inf or nan, else 0
 void launch_any_nonfinite(const double* x, int64_t n, int* flag, hipStream_t stream);
 // y = a * x elementwise over n doubles

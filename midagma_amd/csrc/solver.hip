@@ -635,6 +635,22 @@ extern "C" int midagma_debug_tcc_fast_steps(midagma_solver* s, int steps) {
   return old;
 }
 
+// Test hook (not in the public header): build_at folded into the previous slot's update
+// (at_fold, MIDAGMA_EXP_AT_FOLD) on (1) or off (0); < 0 leaves it.  Returns the old setting, or -1
+// (no handle / the fold cannot apply: not a blocked cov solver with I - W).
+extern "C" int midagma_debug_at_fold(midagma_solver* s, int on) {
+  if (!s || s->begun) return -1;
+  const int old = s->at_fold ? 1 : 0;
+  if (on < 0 || (on != 0) == s->at_fold) return old;
+  if (on && !(s->mode == MIDAGMA_MODE_COV && s->blocked() && s->IW.p)) return -1;
+  return guarded(s, [&] {
+    if (on && !s->A0.p) s->A0.alloc(s->D * s->D);
+    s->at_fold = on != 0;
+    s->graphs_valid = false;
+    return old;
+  });
+}
+
 // Diagnostics of the fast blocked inverse (not in the public header): per outer block g,
 // out[g*(NM_PASSES+2) + 0] = done word, out[... + 1 + p] = ||Q_p||_inf of pass p (stale for
 // passes that did not run in the last slot).

@@ -385,6 +385,7 @@ struct midagma_solver {
       return false;
     }
 #endif
+    double* ain0 = fast && at_fold_on() ? A0.p : nullptr;  // (built by the previous slot's update)
     // experiments build, MIDAGMA_EXP_BUILD_RESID0=1: outer block 0's residual rides in build_at's
     // launch on fast slots at B2 = 256 (one dependent launch fewer, but measured slower: DESIGN 8)
 #ifdef MIDAGMA_EXPERIMENTS
@@ -395,6 +396,7 @@ struct midagma_solver {
 #else
     const bool resid0 = false;
 #endif
+    if (!ain0)
       launch_build_at(W.p, D, /*square=*/true, binv_build_target(Mt.p, D, binv()), D, d, 0.0, d_params, d_state,
                       stream, IW.p);
     if (fast && cov_la_on()) {
@@ -407,9 +409,9 @@ struct midagma_solver {
         }
       }
       const TrailLookAhead tla{side, la_ev.data()};
-      return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse, &tla);
+      return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse, &tla, false, ain0);
     }
-    return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse, nullptr, resid0);
+    return launch_blocked_inverse(Mt.p, D, binv(), fast, gj(), d_state, stream, passes, fuse, nullptr, resid0, ain0);
   }
 #ifdef MIDAGMA_EXPERIMENTS
   // experiment knob MIDAGMA_EXP_BUILD_RESID0=1: build_at and block 0's residual in one launch
@@ -419,6 +421,18 @@ struct midagma_solver {
   }
 #endif
   bool fuse_gemm = knob("MIDAGMA_EXP_FUSE_GEMM", 1) != 0;
+  // build_at folded into the previous slot's update (MIDAGMA_EXP_AT_FOLD): fast slots read outer
+  // step 0's A^T from A0, which fused_update_at (fast slots) or a build_at after the update (slow
+  // slots) wrote from the slot's new W; every call starts with a slow slot, so A0 is never stale
+  bool at_fold = knob("MIDAGMA_EXP_AT_FOLD", 0) != 0;
+  DevBuf A0;
+  bool at_fold_on() const {
+    if (!at_fold || !A0.p || cov_fork_on()) return false;
+#ifdef MIDAGMA_EXPERIMENTS
+    if (df_on || build_resid0_on()) return false;
+#endif
+    return true;
+  }
   // the fast cov slot's control decided by the last workgroup of the trailing launch that carries
   // the score GEMM (control.h; MIDAGMA_EXP_CTL_FOLD=0 launches control_kernel instead)
   bool ctl_fold = knob("MIDAGMA_EXP_CTL_FOLD", 1) != 0;
@@ -524,9 +538,18 @@ struct midagma_solver {
       launch_control(d_params, d_state, partials.p, pivlog.p, zbuf + D * D, bc_table.p, d_ckpt, ckpt_cap, npart.p, d,
                      trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream, l1f ? l1w.p : nullptr);
     const bool slices = lean && mode == MIDAGMA_MODE_COV && cov_split > 1;
+    const double* trek = trek_on && tcfg.mode == 2 ? Gtrek.p : nullptr;
+    if (lean && at_fold_on()) {  // the next slot's build_at in the update (fast slots: no checkpoint)
+      launch_fused_update_at(d_params, d_state, W.p, m.p, v.p, Mt.p, slices ? cov_parts.p : zbuf, slices ? cov_split : 1,
+                             D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr, trek, d, D, A0.p,
+                             IW.p, stream);
+      return;
+    }
     launch_fused_update(d_params, d_state, W.p, m.p, v.p, Mt.p, slices ? cov_parts.p : zbuf,
                         slices ? cov_split : 1, D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr,
-                        trek_on && tcfg.mode == 2 ? Gtrek.p : nullptr, d, D, npart.p, stream);
+                        trek, d, D, npart.p, stream);
+    if (blocked() && at_fold_on())  // slow slot: the next (fast) slot's A^T and I - W from the new W
+      launch_build_at(W.p, D, /*square=*/true, A0.p, D, d, 0.0, d_params, d_state, stream, IW.p);
   }
 
   hipGraphExec_t capture(int which, int reps = 1, int passes = NM_PASSES_RUN) {
@@ -759,6 +782,8 @@ struct midagma_solver {
     }
     // cov mode: build_at also writes I - W for the score GEMM's plain-B form
     if (mode == MIDAGMA_MODE_COV && ((D % 128 == 0 && cov_iw) || w32)) IW.alloc(DD);
+    // the next slot's A^T written by fused_update_at (at_fold_on)
+    if (at_fold && mode == MIDAGMA_MODE_COV && B2 > 0 && IW.p) A0.alloc(DD);
     if (blocked() || data_binv_on()) {
       const int64_t b2 = binv_block(D);
       Malt.alloc(DD);

@@ -316,22 +316,13 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
   }
 }
 
-__global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
-    const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
-    double* __restrict__ v, const double* __restrict__ Mt, const double* __restrict__ Z,
+// One entry's update (act STEP, HALVE or REVERT; no checkpoint norms): m, v stored on a STEP,
+// the new W entry returned (fused_update_kernel and the tiled fused_update_at_kernel)
+__device__ __forceinline__ double update_entry(
+    const Params* __restrict__ pr, const State* __restrict__ st, int act, const double* __restrict__ W,
+    double* __restrict__ m, double* __restrict__ v, const double* __restrict__ Mt, const double* __restrict__ Z,
     int zsplit, int64_t zstride, const double* __restrict__ cov, const double* __restrict__ minc,
-    const double* __restrict__ mexc, const double* __restrict__ trek, int64_t d, int64_t D,
-    double* __restrict__ npart) {
-  const int act = st->action;
-  if (act == ACT_NOOP) return;
-  const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
-  const int64_t i = blockIdx.y;
-  if (act == ACT_STEP && st->ckpt_pending) {  // checkpoint step: also the record's norms
-    fused_step_with_norms(pr, st, W, m, v, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, d, D, npart);
-    return;
-  }
-  if (j >= d) return;
-  const int64_t idx = i * D + j;
+    const double* __restrict__ mexc, const double* __restrict__ trek, int64_t idx) {
   if (act == ACT_STEP) {
     // every operand load first (the optional ones behind uniform selects), then the arithmetic:
     // with the loads among the branches the compiler waited for each before the next
@@ -361,22 +352,81 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
     if (has_exc) wn = wn * ce;
     m[idx] = mm;
     v[idx] = vv;
-    W[idx] = wn;
-  } else {
-    // the last STEP's Adam direction, recomputed from its m, v and bias terms (unchanged
-    // since: bit-identical to the value that step applied, so no d x d store per step)
-    const double gd = (m[idx] / st->bc1) / (sqrt(v[idx] / st->bc2) + 1e-8);
-    // (float32 W: each in-place update rounds, linear.py:235, 239)
-    const bool w32 = pr->w32 != 0;
-    if (act == ACT_HALVE) {
-      double wn = W[idx] + st->lr_a * gd;
-      if (w32) wn = f32r(wn);
-      wn = wn - st->lr_b * gd;
-      W[idx] = w32 ? f32r(wn) : wn;
-    } else {  // ACT_REVERT
-      const double wn = W[idx] + st->lr_a * gd;
-      W[idx] = w32 ? f32r(wn) : wn;
+    return wn;
+  }
+  // the last STEP's Adam direction, recomputed from its m, v and bias terms (unchanged
+  // since: bit-identical to the value that step applied, so no d x d store per step)
+  const double gd = (m[idx] / st->bc1) / (sqrt(v[idx] / st->bc2) + 1e-8);
+  // (float32 W: each in-place update rounds, linear.py:235, 239)
+  const bool w32 = pr->w32 != 0;
+  if (act == ACT_HALVE) {
+    double wn = W[idx] + st->lr_a * gd;
+    if (w32) wn = f32r(wn);
+    wn = wn - st->lr_b * gd;
+    return w32 ? f32r(wn) : wn;
+  }
+  const double wn = W[idx] + st->lr_a * gd;  // ACT_REVERT
+  return w32 ? f32r(wn) : wn;
+}
+
+__global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
+    const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
+    double* __restrict__ v, const double* __restrict__ Mt, const double* __restrict__ Z,
+    int zsplit, int64_t zstride, const double* __restrict__ cov, const double* __restrict__ minc,
+    const double* __restrict__ mexc, const double* __restrict__ trek, int64_t d, int64_t D,
+    double* __restrict__ npart) {
+  const int act = st->action;
+  if (act == ACT_NOOP) return;
+  const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (act == ACT_STEP && st->ckpt_pending) {  // checkpoint step: also the record's norms
+    fused_step_with_norms(pr, st, W, m, v, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, d, D, npart);
+    return;
+  }
+  if (j >= d) return;
+  const int64_t idx = i * D + j;
+  W[idx] = update_entry(pr, st, act, W, m, v, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, idx);
+}
+
+// fused_update on a fast slot with the next slot's build_at folded in (MIDAGMA_EXP_AT_FOLD):
+// 32 x 32 tiles of the whole padded D x D grid; each entry's update as fused_update_kernel
+// (update_entry), then I - W_new (IW, row-major) and A^T = s I - (W_new o W_new)^T through the
+// LDS tile into A0 (build_at_tile's values and padding, bit for bit).  Never a checkpoint step.
+__global__ __launch_bounds__(NTHREADS) void fused_update_at_kernel(
+    const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
+    double* __restrict__ v, const double* __restrict__ Mt, const double* __restrict__ Z, int zsplit,
+    int64_t zstride, const double* __restrict__ cov, const double* __restrict__ minc,
+    const double* __restrict__ mexc, const double* __restrict__ trek, int64_t d, int64_t D,
+    double* __restrict__ A0, double* __restrict__ IW) {
+  const int act = st->action;
+  if (act == ACT_NOOP) return;
+  __shared__ double tile[32][33];
+  const bool w32 = pr->w32 != 0;
+  const double s = pr->s;
+  const int bi = blockIdx.y, bj = blockIdx.x, tid = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 32 * 32 / NTHREADS; ++it) {
+    const int e = it * NTHREADS + tid;
+    const int r = e / 32, c = e % 32;
+    const int64_t I = (int64_t)bi * 32 + r, J = (int64_t)bj * 32 + c;
+    const int64_t idx = I * D + J;
+    double x = 0.0, a;
+    if (I < d && J < d) {
+      x = update_entry(pr, st, act, W, m, v, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, idx);
+      W[idx] = x;
+      a = sw_entry(I == J, s, x, w32);
+    } else {
+      a = (I == J) ? 1.0 : 0.0;
     }
+    IW[idx] = one_minus(I == J, x, w32);
+    tile[c][r] = a;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 32 * 32 / NTHREADS; ++it) {
+    const int e = it * NTHREADS + tid;
+    const int r = e / 32, c = e % 32;
+    A0[((int64_t)bj * 32 + r) * D + (int64_t)bi * 32 + c] = tile[r][c];
   }
 }
 
@@ -459,6 +509,17 @@ void launch_fused_update(const Params* pr, const State* st, double* W, double* m
   dim3 grid((unsigned)((d + NTHREADS - 1) / NTHREADS), (unsigned)d);
   hipLaunchKernelGGL(fused_update_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, Mt, Z, zsplit,
                      zstride, cov, minc, mexc, trek, d, D, npart);
+  HIP_TRY(hipGetLastError());
+}
+
+void launch_fused_update_at(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt,
+                            const double* Z, int zsplit, int64_t zstride, const double* cov, const double* minc,
+                            const double* mexc, const double* trek, int64_t d, int64_t D, double* A0, double* IW,
+                            hipStream_t stream) {
+  if (D % 32 || !A0 || !IW) throw std::invalid_argument("fused_update_at: needs D % 32 == 0, A0 and IW");
+  const dim3 grid((unsigned)(D / 32), (unsigned)(D / 32));
+  hipLaunchKernelGGL(fused_update_at_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, Mt, Z, zsplit, zstride,
+                     cov, minc, mexc, trek, d, D, A0, IW);
   HIP_TRY(hipGetLastError());
 }
 

@@ -140,6 +140,13 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_CTL_FOLD={f}", end=" ")
                 cov_case(d, 2 * d, 20, K)
         os.environ.pop("MIDAGMA_EXP_CTL_FOLD")
+    if which == "atfold":  # build_at folded into the previous slot's update, or its own launch
+        for d, K in ((1000, 3000), (500, 3000), (1400, 1000), (2000, 300)):
+            for f in ("1", "0", "1", "0"):
+                os.environ["MIDAGMA_EXP_AT_FOLD"] = f
+                print(f"MIDAGMA_EXP_AT_FOLD={f}", end=" ")
+                cov_case(d, 2 * d, 20, K)
+        os.environ.pop("MIDAGMA_EXP_AT_FOLD")
     if which == "splitcmp":  # split-K count of the cov score GEMM (fused into the last trail launch or apart)
         for d, K in ((1000, 2000), (1400, 1000)):
             for sp in ("4", "8", "2"):
