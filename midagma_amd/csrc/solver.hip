@@ -635,6 +635,19 @@ extern "C" int midagma_debug_tcc_fast_steps(midagma_solver* s, int steps) {
   return old;
 }
 
+// Test hook (not in the public header): the TCC fixed-shift stage on (1) or off (0); < 0 leaves
+// it.  Returns the old setting.
+extern "C" int midagma_debug_tcc_fix(midagma_solver* s, int on) {
+  if (!s) return -1;
+  const int old = s->tcc_fix != 0 ? 1 : 0;
+  if (on >= 0 && (on != 0 ? 1 : 0) != old) {
+    s->tcc_fix = on != 0 ? 1 : 0;
+    s->cw.fix = s->tcc_fix;
+    s->graphs_valid = false;
+  }
+  return old;
+}
+
 // Test hook (not in the public header): build_at folded into the previous slot's update
 // (at_fold, MIDAGMA_EXP_AT_FOLD) on (1) or off (0); < 0 leaves it.  Returns the old setting, or -1
 // (no handle / the fold cannot apply: not a blocked cov solver with I - W).

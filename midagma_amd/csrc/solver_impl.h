@@ -441,6 +441,8 @@ struct midagma_solver {
   // TCC_NODA_MAX on pivoted slots); a warm-started slot converges in 2-3.
   // MIDAGMA_EXP_TCC_FAST_STEPS=0: every slot runs the whole gated chain
   int tcc_fast_steps = (int)knob("MIDAGMA_EXP_TCC_FAST_STEPS", 5);
+  // TCC (2d > 128): the fixed-shift stage before Noda (tcc.hip; MIDAGMA_EXP_TCC_FIX=0 off)
+  int tcc_fix = (int)knob("MIDAGMA_EXP_TCC_FIX", 1);
   DevBuf ctl_ticket;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
@@ -695,8 +697,8 @@ struct midagma_solver {
     cC.alloc((size_t)2 * D2 * 32);
     HIP_TRY(hipMemcpy(cS.p, S.data(), S.size() * sizeof(double), hipMemcpyHostToDevice));
     HIP_TRY(hipMemset(cvec.p, 0, cvec.n * sizeof(double)));  // warm flag off, vectors 0
-    if (!cgates) HIP_TRY(hipMalloc(&cgates, (1 + TCC_NODA_MAX) * sizeof(State)));
-    HIP_TRY(hipMemset(cgates, 0, (1 + TCC_NODA_MAX) * sizeof(State)));
+    if (!cgates) HIP_TRY(hipMalloc(&cgates, TCC_GATES * sizeof(State)));
+    HIP_TRY(hipMemset(cgates, 0, TCC_GATES * sizeof(State)));
     TccWork w{};
     w.gj = GJWork{cP.p, cR.p, cC.p, nullptr, nullptr};
     w.D2 = D2;
@@ -711,6 +713,7 @@ struct midagma_solver {
     w.scal = v;
     w.part = cpart.p;
     w.gates = cgates;
+    w.fix = tcc_fix != 0 ? 1 : 0;
     // 2d >= 512: the shifted inverses on the two-level blocked inverse (pivoted path), ≈1.4x the
     // flat Gauss-Jordan's speed at D2 = 2048 (MIDAGMA_EXP_TCC_BINV=0: the flat one)
     if (D2 >= 512 && binv_block(D2) > 0 && knob("MIDAGMA_EXP_TCC_BINV", 1) != 0) {

@@ -167,6 +167,8 @@ __global__ void tcc_sigma0_kernel(const double* __restrict__ x, const double* __
     scal[2] = 0.0;  // lower bound (A >= 0)
     scal[7] = 0.0;  // breakdown flag
     scal[9] = 0.0;  // converged flag
+    scal[11] = scal[12] = scal[13] = 0.0;  // the fixed-shift stage's flags
+    scal[14] = mx;                         // ... and its upper bound
   }
 }
 
@@ -329,6 +331,189 @@ __global__ __launch_bounds__(NB * NB) void tcc_blk_kernel(const double* __restri
 
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + EB - 1) / EB, 2048); }
 
+// ---- the fixed-shift stage --------------------------------------------------------------------
+// With the previous slot's Perron vectors as the warm start, sigma_0 is already close to rho, so
+// inverse iteration at the FIXED shift sigma_s = sigma_0 (1 + kFixMargin) converges at the ratio
+// (sigma_s - rho) / (sigma_s - lambda_2) per sweep: v from M x and u from M^T u (one pass over
+// M = (sigma_s I - A)^-1 >= 0 for both), with ONE inverse per slot instead of Noda's two or three
+// plus the final one.  A vector is converged when its ratios x_i / (M x)_i agree to kFixTol
+// relative (its relative error); sigma_s - min_i x_i / (M x)_i >= rho is kept as the upper bound
+// a Noda continuation starts from when the stage does not converge in TCC_FIX_SWEEPS sweeps (a
+// cold start, a small Perron gap) or breaks down (no Perron gap: overflow) -- the Noda steps and
+// the final inverse then run as before (their gates stay on).
+constexpr double kFixMargin = 1e-14;
+constexpr double kFixTol = 1e-13;
+
+// the stage's outcome (thread 0): converged -> Noda and the final inverse gated off
+__device__ void tcc_fix_finish(double* __restrict__ scal, State* __restrict__ gates) {
+  if (scal[11] != 0.0 && scal[12] != 0.0 && scal[13] == 0.0) {
+    scal[9] = 1.0;
+    for (int t = 1; t <= TCC_GATE_FINAL; ++t) gates[t].status = ST_DONE;
+  } else if (scal[13] == 0.0) {
+    scal[1] = fmin(scal[1], scal[14]);
+  }
+}
+
+// 2d <= 256 (D2 <= 256): every sweep in one workgroup of 1024 threads (16 waves, row i on wave
+// i % 16; the u products' column partials per wave summed in wave order)
+__global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __restrict__ Mi, int64_t ld, int n,
+                                                             double* __restrict__ x, double* __restrict__ u,
+                                                             double* __restrict__ scal, State* __restrict__ gates,
+                                                             const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  __shared__ double xs[256], us[256], ys[256], zp[16][256], red[9][16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < 256) {
+    xs[tid] = tid < n ? x[tid] : 0.0;
+    us[tid] = tid < n ? u[tid] : 0.0;
+  }
+  __syncthreads();
+  const double sig = scal[1] * (1.0 + kFixMargin);
+  bool vok = false, uok = false, bad = false;
+  double ub = scal[1];
+  for (int k = 0; k < TCC_FIX_SWEEPS && !(vok && uok); ++k) {
+    double z[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < 16; ++t) {
+      const int i = wv + 16 * t;
+      if (i >= n) break;
+      const double ui = us[i];
+      const double* __restrict__ row = Mi + (int64_t)i * ld;
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        if (j < n) {
+          const double mij = row[j];
+          acc += mij * xs[j];
+          z[q] += mij * ui;
+        }
+      }
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+      if (lane == 0) ys[i] = acc;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zp[wv][lane + 64 * q] = z[q];
+    __syncthreads();
+    // fields: v ratio min / max, |y|^2, sum y; u ratio min / max, |z|^2, sum z; breakdown
+    double f[9] = {INFINITY, -INFINITY, 0.0, 0.0, INFINITY, -INFINITY, 0.0, 0.0, 0.0};
+    double yi = 0.0, zi = 0.0;
+    if (tid < n) {
+      yi = ys[tid];
+      for (int w2 = 0; w2 < 16; ++w2) zi += zp[w2][tid];
+      if (!(yi > 0.0) || !isfinite(yi) || !(zi > 0.0) || !isfinite(zi)) f[8] = 1.0;
+      const double rv = xs[tid] / yi, ru = us[tid] / zi;
+      f[0] = f[1] = rv;
+      f[2] = yi * yi;
+      f[3] = yi;
+      f[4] = f[5] = ru;
+      f[6] = zi * zi;
+      f[7] = zi;
+    }
+#pragma unroll
+    for (int c = 0; c < 9; ++c) {
+      double a = f[c];
+      for (int off = 32; off > 0; off >>= 1) {
+        const double b = __shfl_xor(a, off);
+        a = (c == 0 || c == 4) ? fmin(a, b) : ((c == 1 || c == 5 || c == 8) ? fmax(a, b) : a + b);
+      }
+      if (lane == 0) red[c][wv] = a;
+    }
+    __syncthreads();
+    double g[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) {
+      double a = red[c][0];
+      for (int w2 = 1; w2 < 16; ++w2) {
+        const double b = red[c][w2];
+        a = (c == 0 || c == 4) ? fmin(a, b) : ((c == 1 || c == 5 || c == 8) ? fmax(a, b) : a + b);
+      }
+      g[c] = a;
+    }
+    if (g[8] != 0.0 || !(g[2] > 0.0) || !(g[6] > 0.0) || !isfinite(g[2]) || !isfinite(g[6])) {
+      bad = true;  // (x, u keep the last good sweep's vectors)
+      break;
+    }
+    vok = !(g[1] - g[0] > kFixTol * g[0]);
+    uok = !(g[5] - g[4] > kFixTol * g[4]);
+    ub = fmin(ub, sig - g[0]);
+    if (tid < n) {
+      xs[tid] = yi * ((g[3] < 0.0 ? -1.0 : 1.0) / sqrt(g[2]));
+      us[tid] = zi * ((g[7] < 0.0 ? -1.0 : 1.0) / sqrt(g[6]));
+    }
+    __syncthreads();
+  }
+  if (tid < n) {
+    x[tid] = xs[tid];
+    u[tid] = us[tid];
+  }
+  if (tid == 0) {
+    scal[11] = vok ? 1.0 : 0.0;
+    scal[12] = uok ? 1.0 : 0.0;
+    scal[13] = bad ? 1.0 : 0.0;
+    scal[14] = ub;
+    tcc_fix_finish(scal, gates);
+  }
+}
+
+// 2d > 256: one sweep's update after y = M x and z = M^T u (the GEMV kernels): both vectors
+// renormalised, the convergence and breakdown flags, the later sweeps gated off when done
+__global__ void tcc_fix_update_kernel(double* __restrict__ x, const double* __restrict__ y, double* __restrict__ u,
+                                      const double* __restrict__ z, int64_t n, double* __restrict__ scal,
+                                      State* __restrict__ gates, int k, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  __shared__ double sh[EB];
+  double vmin = INFINITY, vmax = -INFINITY, vss = 0.0, vs = 0.0;
+  double umin = INFINITY, umax = -INFINITY, uss = 0.0, us = 0.0, bad = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += EB) {
+    const double yi = y[i], zi = z[i];
+    if (!(yi > 0.0) || !isfinite(yi) || !(zi > 0.0) || !isfinite(zi)) bad = 1.0;
+    const double rv = x[i] / yi, ru = u[i] / zi;
+    vmin = fmin(vmin, rv);
+    vmax = fmax(vmax, rv);
+    vss += yi * yi;
+    vs += yi;
+    umin = fmin(umin, ru);
+    umax = fmax(umax, ru);
+    uss += zi * zi;
+    us += zi;
+  }
+  vmin = wg_reduce(vmin, sh, Min());
+  vmax = wg_reduce(vmax, sh, Max());
+  vss = wg_reduce(vss, sh, Add());
+  vs = wg_reduce(vs, sh, Add());
+  umin = wg_reduce(umin, sh, Min());
+  umax = wg_reduce(umax, sh, Max());
+  uss = wg_reduce(uss, sh, Add());
+  us = wg_reduce(us, sh, Add());
+  bad = wg_reduce(bad, sh, Max());
+  const bool brk = bad != 0.0 || !(vss > 0.0) || !(uss > 0.0) || !isfinite(vss) || !isfinite(uss);
+  bool done = brk;
+  if (!brk) {
+    const double iv = (vs < 0.0 ? -1.0 : 1.0) / sqrt(vss), iu = (us < 0.0 ? -1.0 : 1.0) / sqrt(uss);
+    for (int64_t i = threadIdx.x; i < n; i += EB) {
+      x[i] = y[i] * iv;
+      u[i] = z[i] * iu;
+    }
+    const bool vok = !(vmax - vmin > kFixTol * vmin), uok = !(umax - umin > kFixTol * umin);
+    done = vok && uok;
+    if (threadIdx.x == 0) {
+      scal[11] = vok ? 1.0 : 0.0;
+      scal[12] = uok ? 1.0 : 0.0;
+      scal[14] = fmin(scal[14], scal[1] * (1.0 + kFixMargin) - vmin);
+    }
+  } else if (threadIdx.x == 0) {
+    scal[13] = 1.0;
+  }
+  if (done && threadIdx.x == 0)
+    for (int t = k + 1; t < TCC_FIX_SWEEPS; ++t) gates[TCC_GATE_FIX0 + t].status = ST_DONE;
+}
+
+__global__ void tcc_fix_done_kernel(double* __restrict__ scal, State* __restrict__ gates,
+                                    const State* __restrict__ gate) {
+  if (!gate_on(gate) || threadIdx.x != 0) return;
+  tcc_fix_finish(scal, gates);
+}
+
 
 // the shifted inverse: the two-level blocked one (pivoted path: 256-blocks, panels, MFMA trailing
 // updates) where the solver allocated its buffers (2d >= 512), else the flat 32-block Gauss-Jordan
@@ -354,6 +539,7 @@ __global__ void tcc_handback_kernel(State* __restrict__ st, State* __restrict__ 
   if (gates[0].status != ST_RUNNING || gates[1 + steps].status != ST_RUNNING) return;
   st->status = ST_NEED_GJ;
   gates[0].status = ST_DONE;
+  gates[TCC_GATE_FINAL].status = ST_DONE;
 }
 
 }  // namespace
@@ -380,7 +566,7 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   }
   State* g0 = w.gates;
   const double m = (double)cfg.m;
-  hipLaunchKernelGGL(tcc_gate_kernel, dim3(1), dim3(64), 0, stream, st, cfg.mode, w.gates, TCC_NODA_MAX);
+  hipLaunchKernelGGL(tcc_gate_kernel, dim3(1), dim3(64), 0, stream, st, cfg.mode, w.gates, TCC_GATES - 1);
   hipLaunchKernelGGL(tcc_build_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, W, w.S, cfg.w, d, D, D2, w.A,
                      g0);
   const dim3 gv((unsigned)((n + 3) / 4));
@@ -394,6 +580,27 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.vprev, w.x, n, w.scal, g0);
   hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 0, w.x, w.y, g0);
   hipLaunchKernelGGL(tcc_sigma0_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, g0);
+  // the fixed-shift stage (w.fix = 0, MIDAGMA_EXP_TCC_FIX=0: Noda from the warm start at once)
+  if (w.fix) {
+    hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
+                       w.scal, kFixMargin, g0);
+    tcc_inverse(w, gj, g0, stream);
+    hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.uprev, w.u, n, w.scal, g0);
+    if (D2 <= 256) {
+      hipLaunchKernelGGL(tcc_fix_small_kernel, dim3(1), dim3(1024), 0, stream, w.Mi, D2, (int)n, w.x, w.u, w.scal,
+                         w.gates, g0);
+    } else {
+      for (int k = 0; k < TCC_FIX_SWEEPS; ++k) {
+        const State* gk = &w.gates[TCC_GATE_FIX0 + k];
+        hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gk);
+        hipLaunchKernelGGL(tcc_gemv_t_partial_kernel, gt, dim3(EB), 0, stream, w.Mi, D2, n, w.u, w.part, gk);
+        hipLaunchKernelGGL(tcc_gemv_t_sum_kernel, gts, dim3(EB), 0, stream, w.part, D2, n, nchunks, w.z, gk);
+        hipLaunchKernelGGL(tcc_fix_update_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, w.u, w.z, n, w.scal, w.gates,
+                           k, gk);
+      }
+      hipLaunchKernelGGL(tcc_fix_done_kernel, dim3(1), dim3(64), 0, stream, w.scal, w.gates, g0);
+    }
+  }
   const int nsteps = handback ? std::min(std::max(steps, 1), TCC_NODA_MAX - 1) : TCC_NODA_MAX;
   for (int k = 0; k < nsteps; ++k) {
     const State* gk = &w.gates[1 + k];
@@ -405,19 +612,21 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
                        gk);
   }
   if (handback) hipLaunchKernelGGL(tcc_handback_kernel, dim3(1), dim3(64), 0, stream, handback, w.gates, nsteps);
-  // final inverse just above the converged root: two sweeps for v, two (transposed) for u
+  // final inverse just above the converged root: two sweeps for v, two (transposed) for u (the
+  // Noda path: gated off when the fixed-shift stage converged)
+  const State* gf = &w.gates[TCC_GATE_FINAL];
   hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
-                     w.scal, 1e-14, g0);
-  tcc_inverse(w, gj, g0, stream);
+                     w.scal, 1e-14, gf);
+  tcc_inverse(w, gj, gf, stream);
   for (int r = 0; r < 2; ++r) {
-    hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, g0);
-    hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.x, n, g0);
+    hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gf);
+    hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.x, n, gf);
   }
-  hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.uprev, w.u, n, w.scal, g0);
+  hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.uprev, w.u, n, w.scal, gf);
   for (int r = 0; r < 2; ++r) {
-    hipLaunchKernelGGL(tcc_gemv_t_partial_kernel, gt, dim3(EB), 0, stream, w.Mi, D2, n, w.u, w.part, g0);
-    hipLaunchKernelGGL(tcc_gemv_t_sum_kernel, gts, dim3(EB), 0, stream, w.part, D2, n, nchunks, w.y, g0);
-    hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.u, n, g0);
+    hipLaunchKernelGGL(tcc_gemv_t_partial_kernel, gt, dim3(EB), 0, stream, w.Mi, D2, n, w.u, w.part, gf);
+    hipLaunchKernelGGL(tcc_gemv_t_sum_kernel, gts, dim3(EB), 0, stream, w.part, D2, n, nchunks, w.y, gf);
+    hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.u, n, gf);
   }
   // rho (Rayleigh), the lower bound through B, value; then the gradient
   hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 0, w.x, w.y, g0);

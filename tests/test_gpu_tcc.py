@@ -142,11 +142,13 @@ def test_dagma_linear_tcc_fit_runs(golden):
 
 @pytest.mark.parametrize("d", [100, 300])
 def test_tcc_short_chain_hands_back(d):
-    """TCC with 2d > 128 on fast cov slots runs a short Noda chain first in the slot and hands the
-    slot back when it has not converged (tcc.hip tcc_handback_kernel): the re-run is a pivoted slot
-    with the whole chain, warm-started as before.  Forced to hand back nearly every slot (1 step), by
-    default (5 steps), and with the whole chain on every slot (0): W after 60 steps within 1e-9 of
-    the oracle each time."""
+    """TCC with 2d > 128 on fast cov slots: the fixed-shift stage (one inverse at the warm start's
+    Collatz-Wielandt bound, inverse iteration for v and u) and, when it does not converge, a short
+    Noda chain; the slot hands back when that has not converged either (tcc.hip
+    tcc_handback_kernel), the re-run is a pivoted slot with the whole chain.  Without the fixed
+    stage: forced to hand back nearly every slot (1 Noda step), by default (5 steps), and with the
+    whole chain on every slot (0); with it: by default and at 1 step.  W after 60 steps within 1e-9
+    of the oracle each time, and the fixed stage leaves fewer slots to hand back."""
     from midagma_amd.simulate import make_dataset
     X, _, _ = make_dataset(d, 2 * d, seed=7)
     rng = np.random.default_rng(7)
@@ -158,15 +160,17 @@ def test_tcc_short_chain_hands_back(d):
     K = 60
     Wr, tr = o.minimize(np.zeros((d, d)), 1.0, K, 1.0, 3e-4, tol=-1.0)
     backs = {}
-    for steps in (1, None, 0):
+    for fix, steps in ((False, 1), (False, None), (False, 0), (True, None), (True, 1)):
         s = _solver(d, o.cov)
+        s.debug_tcc_fix(fix)
         if steps is not None:
             s.debug_tcc_fast_steps(steps)
         s.set_trek_tcc(pairs, mode="opt", weight=0.2)
         W = np.zeros((d, d))
         res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=1000)
-        backs[steps] = s.debug_handbacks()
+        backs[fix, steps] = s.debug_handbacks()
         s.close()
         assert res.iters == K
-        assert np.abs(W - Wr).max() <= 1e-9, (steps, np.abs(W - Wr).max())
-    assert backs[1] >= K // 3  # forced: most fast slots handed back
+        assert np.abs(W - Wr).max() <= 1e-9, (fix, steps, np.abs(W - Wr).max())
+    assert backs[False, 1] >= K // 3  # forced: most fast slots handed back
+    assert backs[True, 1] < backs[False, 1], backs

@@ -126,6 +126,13 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_TCC_FAST_STEPS={f}", end=" ")
                 trek_case(d, "tcc", 300 if d <= 300 else 60)
         os.environ.pop("MIDAGMA_EXP_TCC_FAST_STEPS")
+    if which == "tccfix":  # TCC (2d > 128): the fixed-shift stage first (one inverse), or Noda from the warm start
+        for d in [int(x) for x in sys.argv[2:]] or [100, 300, 1000]:
+            for f in ("1", "0", "1"):
+                os.environ["MIDAGMA_EXP_TCC_FIX"] = f
+                print(f"MIDAGMA_EXP_TCC_FIX={f}", end=" ")
+                trek_case(d, "tcc", 300 if d <= 300 else 60)
+        os.environ.pop("MIDAGMA_EXP_TCC_FIX")
     if which == "tccbinv":  # TCC (2d >= 512): the shifted inverses on the blocked inverse, or the flat Gauss-Jordan
         for d in [int(x) for x in sys.argv[2:]] or [300, 1000]:
             for f in ("1", "0", "1", "0"):
@@ -276,6 +283,9 @@ if __name__ == "__main__":
             cov_case(d, d + 1000, 3, K)
     if which == "tcc20":  # one size, for a kernel trace
         trek_case(20, "tcc", 2000)
+    if which == "tccd":  # the given sizes (default 100), for a kernel trace
+        for d in [int(x) for x in sys.argv[2:]] or [100]:
+            trek_case(d, "tcc", 300 if d <= 300 else 60)
     if which == "tccnb":  # the one-workgroup TCC at each block count it fits
         for d, nbs in ((8, ("8", "16", "32")), (16, ("8", "16", "32")), (20, ("16", "32")), (32, ("16", "32")),
                        (64, ("32",))):
