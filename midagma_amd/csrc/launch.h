@@ -573,7 +573,8 @@ void launch_fused_update(const Params* pr, const State* st, double* W, double* m
                          const double* minc, const double* mexc, const double* trek, int64_t d, int64_t D,
                          double* npart, hipStream_t stream);
 // fused_update (never a checkpoint step) plus the next slot's build_at from the new W: A0 =
-// s I - (W o W)^T (outer step 0's input, launch_blocked_inverse ain0) and IW = I - W; D % 32 == 0
+// s I - (W o W)^T (outer step 0's input, launch_blocked_inverse ain0) and IW = I - W (nullable);
+// D % 32 == 0
 void launch_fused_update_at(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt,
                             const double* Z, int zsplit, int64_t zstride, const double* cov, const double* minc,
                             const double* mexc, const double* trek, int64_t d, int64_t D, double* A0, double* IW,

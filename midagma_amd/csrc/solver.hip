@@ -650,12 +650,12 @@ extern "C" int midagma_debug_tcc_fix(midagma_solver* s, int on) {
 
 // Test hook (not in the public header): build_at folded into the previous slot's update
 // (at_fold, MIDAGMA_EXP_AT_FOLD) on (1) or off (0); < 0 leaves it.  Returns the old setting, or -1
-// (no handle / the fold cannot apply: not a blocked cov solver with I - W).
+// (no handle / the fold cannot apply: not a blocked cov solver).
 extern "C" int midagma_debug_at_fold(midagma_solver* s, int on) {
   if (!s || s->begun) return -1;
   const int old = s->at_fold ? 1 : 0;
   if (on < 0 || (on != 0) == s->at_fold) return old;
-  if (on && !(s->mode == MIDAGMA_MODE_COV && s->blocked() && s->IW.p)) return -1;
+  if (on && !(s->mode == MIDAGMA_MODE_COV && s->blocked())) return -1;
   return guarded(s, [&] {
     if (on && !s->A0.p) s->A0.alloc(s->D * s->D);
     s->at_fold = on != 0;

@@ -786,7 +786,7 @@ struct midagma_solver {
     // cov mode: build_at also writes I - W for the score GEMM's plain-B form
     if (mode == MIDAGMA_MODE_COV && ((D % 128 == 0 && cov_iw) || w32)) IW.alloc(DD);
     // the next slot's A^T written by fused_update_at (at_fold_on)
-    if (at_fold && mode == MIDAGMA_MODE_COV && B2 > 0 && IW.p) A0.alloc(DD);
+    if (at_fold && mode == MIDAGMA_MODE_COV && B2 > 0) A0.alloc(DD);
     if (blocked() || data_binv_on()) {
       const int64_t b2 = binv_block(D);
       Malt.alloc(DD);

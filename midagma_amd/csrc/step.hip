@@ -390,7 +390,7 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
 
 // fused_update on a fast slot with the next slot's build_at folded in (MIDAGMA_EXP_AT_FOLD):
 // 32 x 32 tiles of the whole padded D x D grid; each entry's update as fused_update_kernel
-// (update_entry), then I - W_new (IW, row-major) and A^T = s I - (W_new o W_new)^T through the
+// (update_entry), then I - W_new (IW, row-major; nullable) and A^T = s I - (W_new o W_new)^T through the
 // LDS tile into A0 (build_at_tile's values and padding, bit for bit).  Never a checkpoint step.
 __global__ __launch_bounds__(NTHREADS) void fused_update_at_kernel(
     const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_at_kernel(
     } else {
       a = (I == J) ? 1.0 : 0.0;
     }
-    IW[idx] = one_minus(I == J, x, w32);
+    if (IW) IW[idx] = one_minus(I == J, x, w32);
     tile[c][r] = a;
   }
   __syncthreads();
@@ -516,7 +516,7 @@ void launch_fused_update_at(const Params* pr, const State* st, double* W, double
                             const double* Z, int zsplit, int64_t zstride, const double* cov, const double* minc,
                             const double* mexc, const double* trek, int64_t d, int64_t D, double* A0, double* IW,
                             hipStream_t stream) {
-  if (D % 32 || !A0 || !IW) throw std::invalid_argument("fused_update_at: needs D % 32 == 0, A0 and IW");
+  if (D % 32 || !A0) throw std::invalid_argument("fused_update_at: needs D % 32 == 0 and A0");
   const dim3 grid((unsigned)(D / 32), (unsigned)(D / 32));
   hipLaunchKernelGGL(fused_update_at_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, Mt, Z, zsplit, zstride,
                      cov, minc, mexc, trek, d, D, A0, IW);
