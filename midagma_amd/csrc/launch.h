@@ -572,13 +572,13 @@ void launch_np_l1(const double* W, int64_t d, int64_t D, const State* st, float*
 void launch_fused_update(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt, const double* Z, int zsplit, int64_t zstride, const double* cov,
                          const double* minc, const double* mexc, const double* trek, int64_t d, int64_t D,
                          double* npart, hipStream_t stream);
-// fused_update (never a checkpoint step) plus the next slot's build_at from the new W: A0 =
-// s I - (W o W)^T (outer step 0's input, launch_blocked_inverse ain0) and IW = I - W (nullable);
-// D % 32 == 0
+// fused_update (with the checkpoint iteration's norm partials, as launch_fused_update) plus the
+// next slot's build_at from the new W: A0 = s I - (W o W)^T (outer step 0's input,
+// launch_blocked_inverse ain0) and IW = I - W (nullable); D % 8 == 0
 void launch_fused_update_at(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt,
                             const double* Z, int zsplit, int64_t zstride, const double* cov, const double* minc,
                             const double* mexc, const double* trek, int64_t d, int64_t D, double* A0, double* IW,
-                            hipStream_t stream);
+                            double* npart, hipStream_t stream);
 // *flag (device int) <- 1 if any of x[0..n) is inf or nan, else 0
 void launch_any_nonfinite(const double* x, int64_t n, int* flag, hipStream_t stream);
 // y = a * x elementwise over n doubles

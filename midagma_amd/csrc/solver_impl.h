@@ -541,10 +541,10 @@ struct midagma_solver {
                      trek_on ? (trek_tcc ? cw.scal : tw.scal) : nullptr, stream, l1f ? l1w.p : nullptr);
     const bool slices = lean && mode == MIDAGMA_MODE_COV && cov_split > 1;
     const double* trek = trek_on && tcfg.mode == 2 ? Gtrek.p : nullptr;
-    if (lean && at_fold_on()) {  // the next slot's build_at in the update (fast slots: no checkpoint)
+    if (lean && at_fold_on()) {  // the next slot's build_at in the update
       launch_fused_update_at(d_params, d_state, W.p, m.p, v.p, Mt.p, slices ? cov_parts.p : zbuf, slices ? cov_split : 1,
                              D * D, cov.p, has_inc ? minc.p : nullptr, has_exc ? mexc.p : nullptr, trek, d, D, A0.p,
-                             IW.p, stream);
+                             IW.p, npart.p, stream);
       return;
     }
     launch_fused_update(d_params, d_state, W.p, m.p, v.p, Mt.p, slices ? cov_parts.p : zbuf,

@@ -237,66 +237,67 @@ __device__ __forceinline__ double z_at(const double* __restrict__ Z, int zsplit,
   return acc;
 }
 
-// The STEP of a checkpoint iteration: the same update as fused_update_kernel plus the
-// partials of the record's norms (linear.py:262-273, 307-311), one row of NORM_FIELDS per
-// workgroup.  Only every `checkpoint`-th slot takes this path.
-__device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr, const State* __restrict__ st,
-                                                   double* __restrict__ W, double* __restrict__ m,
-                                                   double* __restrict__ v,
-                                                   const double* __restrict__ Mt, const double* __restrict__ Z,
-                                                   int zsplit, int64_t zstride,
+// One entry of a checkpoint iteration's STEP: the update of update_entry (the same arithmetic)
+// and the entry's terms of the record's norms in q (linear.py:262-273, 307-311); m, v stored,
+// the new W entry returned
+__device__ __forceinline__ double step_entry_norms(const Params* __restrict__ pr, const State* __restrict__ st,
+                                                   const double* __restrict__ W, double* __restrict__ m,
+                                                   double* __restrict__ v, const double* __restrict__ Mt,
+                                                   const double* __restrict__ Z, int zsplit, int64_t zstride,
                                                    const double* __restrict__ cov, const double* __restrict__ minc,
                                                    const double* __restrict__ mexc, const double* __restrict__ trek,
-                                                   int64_t d, int64_t D, double* __restrict__ npart) {
-  __shared__ double red[NORM_FIELDS][4];
-  const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
-  const int64_t i = blockIdx.y;
-  double q[NORM_FIELDS];
-  for (int f = 0; f < NORM_FIELDS; ++f) q[f] = f == NF_WMIN ? INFINITY : 0.0;
-  if (j < d) {
-    const int64_t idx = i * D + j;
-    const double w = W[idx];
-    const bool w32 = pr->w32 != 0;
-    const double mt = m_entry(Mt[idx], w32);
-    double gs = pr->zscale * z_at(Z, zsplit, zstride, idx);
-    if (pr->logistic) gs = gs + pr->cscale * cov[idx];
-    const double sg = sign_of(w);
-    const double gl1 = pr->mu_l1 * sg;
-    const double gh = h_term(w, mt, w32);
-    double gobj = gs + gl1;
-    gobj = gobj + gh;
-    double ginc = 0.0;
-    if (pr->has_inc) {
-      ginc = minc[idx] * sg;
-      gobj = gobj + ginc;
-    }
-    double gtr = 0.0;
-    if (trek) {  // Gobj + weight * trek_grad (linear.py:257-258); trek holds weight * grad
-      gtr = trek[idx];
-      gobj = gobj + gtr;
-    }
-    const double mm = m[idx] * pr->beta1 + pr->c1 * gobj;
-    const double vv = v[idx] * pr->beta2 + pr->c2 * (gobj * gobj);
-    const double mh = mm / st->bc1;
-    const double vh = vv / st->bc2;
-    const double gd = mh / (sqrt(vh) + 1e-8);
-    double wn = w - st->lr_a * gd;
-    if (w32) wn = f32r(wn);  // W -= lr * grad into a float32 W (linear.py:275)
-    if (pr->has_exc) wn = wn * mexc[idx];
-    m[idx] = mm;
-    v[idx] = vv;
-    W[idx] = wn;
-    q[NF_GOBJ] = gobj * gobj;
-    q[NF_GSCORE] = gs * gs;
-    q[NF_GDAG] = gh * gh;
-    q[NF_GL1] = gl1 * gl1;
-    q[NF_GINC] = ginc * ginc;
-    q[NF_GTREK] = gtr * gtr;
-    q[NF_GSTEP] = gd * gd;
-    q[NF_W2] = wn * wn;
-    q[NF_WMAX] = fabs(wn);
-    if (wn != 0.0) q[NF_WMIN] = fabs(wn);
+                                                   int64_t idx, double (&q)[NORM_FIELDS]) {
+  const double w = W[idx];
+  const bool w32 = pr->w32 != 0;
+  const double mt = m_entry(Mt[idx], w32);
+  double gs = pr->zscale * z_at(Z, zsplit, zstride, idx);
+  if (pr->logistic) gs = gs + pr->cscale * cov[idx];
+  const double sg = sign_of(w);
+  const double gl1 = pr->mu_l1 * sg;
+  const double gh = h_term(w, mt, w32);
+  double gobj = gs + gl1;
+  gobj = gobj + gh;
+  double ginc = 0.0;
+  if (pr->has_inc) {
+    ginc = minc[idx] * sg;
+    gobj = gobj + ginc;
   }
+  double gtr = 0.0;
+  if (trek) {  // Gobj + weight * trek_grad (linear.py:257-258); trek holds weight * grad
+    gtr = trek[idx];
+    gobj = gobj + gtr;
+  }
+  const double mm = m[idx] * pr->beta1 + pr->c1 * gobj;
+  const double vv = v[idx] * pr->beta2 + pr->c2 * (gobj * gobj);
+  const double mh = mm / st->bc1;
+  const double vh = vv / st->bc2;
+  const double gd = mh / (sqrt(vh) + 1e-8);
+  double wn = w - st->lr_a * gd;
+  if (w32) wn = f32r(wn);  // W -= lr * grad into a float32 W (linear.py:275)
+  if (pr->has_exc) wn = wn * mexc[idx];
+  m[idx] = mm;
+  v[idx] = vv;
+  q[NF_GOBJ] = gobj * gobj;
+  q[NF_GSCORE] = gs * gs;
+  q[NF_GDAG] = gh * gh;
+  q[NF_GL1] = gl1 * gl1;
+  q[NF_GINC] = ginc * ginc;
+  q[NF_GTREK] = gtr * gtr;
+  q[NF_GSTEP] = gd * gd;
+  q[NF_W2] = wn * wn;
+  q[NF_WMAX] = fabs(wn);
+  if (wn != 0.0) q[NF_WMIN] = fabs(wn);
+  return wn;
+}
+
+__device__ __forceinline__ void norms_init(double (&q)[NORM_FIELDS]) {
+  for (int f = 0; f < NORM_FIELDS; ++f) q[f] = f == NF_WMIN ? INFINITY : 0.0;
+}
+
+// The workgroup's NORM_FIELDS partials of a 256-column row chunk into out (lane butterflies, then
+// the four waves in a fixed order); every thread of the workgroup calls it
+__device__ __forceinline__ void norms_store(const double (&q)[NORM_FIELDS], double (*red)[4],
+                                            double* __restrict__ out) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int f = 0; f < NORM_FIELDS; ++f) {
     double x = q[f];
@@ -312,8 +313,32 @@ __device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr
     const double a = red[f][0], b = red[f][1], c = red[f][2], e = red[f][3];
     const double r = f == NF_WMAX ? fmax(fmax(a, b), fmax(c, e))
                                   : (f == NF_WMIN ? fmin(fmin(a, b), fmin(c, e)) : (a + b) + (c + e));
-    npart[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * NORM_FIELDS + f] = r;
+    out[f] = r;
   }
+  __syncthreads();
+}
+
+// The STEP of a checkpoint iteration: the same update as fused_update_kernel plus the
+// partials of the record's norms, one row of NORM_FIELDS per (row, 256-column chunk).  Only
+// every `checkpoint`-th slot takes this path.
+__device__ __noinline__ void fused_step_with_norms(const Params* __restrict__ pr, const State* __restrict__ st,
+                                                   double* __restrict__ W, double* __restrict__ m,
+                                                   double* __restrict__ v,
+                                                   const double* __restrict__ Mt, const double* __restrict__ Z,
+                                                   int zsplit, int64_t zstride,
+                                                   const double* __restrict__ cov, const double* __restrict__ minc,
+                                                   const double* __restrict__ mexc, const double* __restrict__ trek,
+                                                   int64_t d, int64_t D, double* __restrict__ npart) {
+  __shared__ double red[NORM_FIELDS][4];
+  const int64_t j = (int64_t)blockIdx.x * NTHREADS + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  double q[NORM_FIELDS];
+  norms_init(q);
+  if (j < d) {
+    const int64_t idx = i * D + j;
+    W[idx] = step_entry_norms(pr, st, W, m, v, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, idx, q);
+  }
+  norms_store(q, red, npart + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * NORM_FIELDS);
 }
 
 // One entry's update (act STEP, HALVE or REVERT; no checkpoint norms): m, v stored on a STEP,
@@ -389,44 +414,52 @@ __global__ __launch_bounds__(NTHREADS) void fused_update_kernel(
 }
 
 // fused_update on a fast slot with the next slot's build_at folded in (MIDAGMA_EXP_AT_FOLD):
-// 32 x 32 tiles of the whole padded D x D grid; each entry's update as fused_update_kernel
-// (update_entry), then I - W_new (IW, row-major; nullable) and A^T = s I - (W_new o W_new)^T through the
-// LDS tile into A0 (build_at_tile's values and padding, bit for bit).  Never a checkpoint step.
+// 8-row x 256-column tiles of the whole padded D x D grid, thread t on column t of the tile.
+// Each entry's update is fused_update_kernel's (update_entry; on a checkpoint iteration's STEP
+// step_entry_norms and the norm partials of each (row, 256-column chunk), fused_step_with_norms'
+// partition and order); then I - W_new (IW, row-major; nullable) and A^T = s I - (W_new o W_new)^T
+// through the LDS tile into A0, one 64-byte row segment per 8 threads (build_at_tile's values and
+// padding, bit for bit).
 __global__ __launch_bounds__(NTHREADS) void fused_update_at_kernel(
     const Params* __restrict__ pr, const State* __restrict__ st, double* __restrict__ W, double* __restrict__ m,
     double* __restrict__ v, const double* __restrict__ Mt, const double* __restrict__ Z, int zsplit,
     int64_t zstride, const double* __restrict__ cov, const double* __restrict__ minc,
     const double* __restrict__ mexc, const double* __restrict__ trek, int64_t d, int64_t D,
-    double* __restrict__ A0, double* __restrict__ IW) {
+    double* __restrict__ A0, double* __restrict__ IW, double* __restrict__ npart) {
   const int act = st->action;
   if (act == ACT_NOOP) return;
-  __shared__ double tile[32][33];
+  __shared__ double tile[NTHREADS][9];
+  __shared__ double red[NORM_FIELDS][4];
   const bool w32 = pr->w32 != 0;
   const double s = pr->s;
-  const int bi = blockIdx.y, bj = blockIdx.x, tid = threadIdx.x;
-#pragma unroll
-  for (int it = 0; it < 32 * 32 / NTHREADS; ++it) {
-    const int e = it * NTHREADS + tid;
-    const int r = e / 32, c = e % 32;
-    const int64_t I = (int64_t)bi * 32 + r, J = (int64_t)bj * 32 + c;
-    const int64_t idx = I * D + J;
-    double x = 0.0, a;
-    if (I < d && J < d) {
+  const bool norms = act == ACT_STEP && st->ckpt_pending;
+  const int64_t J = (int64_t)blockIdx.x * NTHREADS + threadIdx.x, I0 = (int64_t)blockIdx.y * 8;
+  const int64_t gx = (d + NTHREADS - 1) / NTHREADS;  // fused_update_kernel's column chunks
+  for (int r = 0; r < 8; ++r) {
+    const int64_t I = I0 + r, idx = I * D + J;
+    const bool in = I < d && J < d;
+    double x = 0.0;
+    if (norms) {
+      double q[NORM_FIELDS];
+      norms_init(q);
+      if (in) {
+        x = step_entry_norms(pr, st, W, m, v, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, idx, q);
+        W[idx] = x;
+      }
+      if (I < d && (int64_t)blockIdx.x < gx) norms_store(q, red, npart + (I * gx + blockIdx.x) * NORM_FIELDS);
+    } else if (in) {
       x = update_entry(pr, st, act, W, m, v, Mt, Z, zsplit, zstride, cov, minc, mexc, trek, idx);
       W[idx] = x;
-      a = sw_entry(I == J, s, x, w32);
-    } else {
-      a = (I == J) ? 1.0 : 0.0;
     }
-    if (IW) IW[idx] = one_minus(I == J, x, w32);
-    tile[c][r] = a;
+    if (J < D && IW) IW[idx] = one_minus(I == J, x, w32);
+    tile[threadIdx.x][r] = in ? sw_entry(I == J, s, x, w32) : ((I == J) ? 1.0 : 0.0);
   }
   __syncthreads();
 #pragma unroll
-  for (int it = 0; it < 32 * 32 / NTHREADS; ++it) {
-    const int e = it * NTHREADS + tid;
-    const int r = e / 32, c = e % 32;
-    A0[((int64_t)bj * 32 + r) * D + (int64_t)bi * 32 + c] = tile[r][c];
+  for (int it = 0; it < 8; ++it) {
+    const int e = it * NTHREADS + threadIdx.x, jj = e >> 3, ii = e & 7;
+    const int64_t Jw = (int64_t)blockIdx.x * NTHREADS + jj;
+    if (Jw < D) A0[Jw * D + I0 + ii] = tile[jj][ii];
   }
 }
 
@@ -515,11 +548,11 @@ void launch_fused_update(const Params* pr, const State* st, double* W, double* m
 void launch_fused_update_at(const Params* pr, const State* st, double* W, double* m, double* v, const double* Mt,
                             const double* Z, int zsplit, int64_t zstride, const double* cov, const double* minc,
                             const double* mexc, const double* trek, int64_t d, int64_t D, double* A0, double* IW,
-                            hipStream_t stream) {
-  if (D % 32 || !A0) throw std::invalid_argument("fused_update_at: needs D % 32 == 0 and A0");
-  const dim3 grid((unsigned)(D / 32), (unsigned)(D / 32));
+                            double* npart, hipStream_t stream) {
+  if (D % 8 || !A0 || !npart) throw std::invalid_argument("fused_update_at: needs D % 8 == 0, A0 and npart");
+  const dim3 grid((unsigned)((D + NTHREADS - 1) / NTHREADS), (unsigned)(D / 8));
   hipLaunchKernelGGL(fused_update_at_kernel, grid, dim3(NTHREADS), 0, stream, pr, st, W, m, v, Mt, Z, zsplit, zstride,
-                     cov, minc, mexc, trek, d, D, A0, IW);
+                     cov, minc, mexc, trek, d, D, A0, IW, npart);
   HIP_TRY(hipGetLastError());
 }
 
