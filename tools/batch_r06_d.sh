@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash tools/gpu.sh tests tests/test_gpu_atfold.py tests/test_gpu_tcc.py tests/test_gpu_trek.py || exit $?
+bash tools/gpu.sh tests tests/test_gpu_atfold.py::test_at_fold_rejected_where_it_cannot_apply tests/test_gpu_tcc.py tests/test_gpu_trek.py || exit $?
 cp gpurun_out/gpu_tests.log gpurun_out/gpu_tests_r06_d.log
 MIDAGMA_LIB=$R/midagma_amd/libmidagma_hip_exp.so timeout -k 10 400 python tools/probe_perf.py atfold > gpurun_out/probe_atfold.log 2>&1 || exit $?
 MIDAGMA_LIB=$R/midagma_amd/libmidagma_hip_exp.so timeout -k 10 400 python tools/probe_perf.py tccfix > gpurun_out/probe_tccfix.log 2>&1 || exit $?
