@@ -251,6 +251,7 @@ struct SmallTcc {
   double* scal;           // TccWork::scal, vprev, uprev
   double* vprev;
   double* uprev;
+  int fix = 1;            // TccWork::fix
 };
 void launch_small_minimize(const Params* pr, State* st, double* W, double* m, double* v, const double* covs,
                            const double* minc, const double* mexc, const double* bc_table, CkptRec* ckpt,

@@ -414,7 +414,7 @@ __global__ __launch_bounds__(64 * NW) void small_minimize_kernel(
       if (tc.mode == 2 || (RC ? r_ckpt : S.ckpt_pending)) {
         tccb::tcc_blk_body<TNB, TBS>([&](int i, int j) { return Wimg[i * SW + j]; },
                                 [&](int i, int j) { return tc.S[(int64_t)i * D + j]; }, tc.ws, di, tc.mode, tc.eps,
-                                tc.m, tc.weight, tsc, tvp, tup, nullptr, D, TL);
+                                tc.m, tc.weight, tsc, tvp, tup, nullptr, D, TL, tc.fix != 0);
         tcc_ran = true;
       }
     }

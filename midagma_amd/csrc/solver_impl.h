@@ -1056,7 +1056,8 @@ struct midagma_solver {
       if (B <= 0) break;
       SmallTcc tc{};
       if (trek_on && trek_tcc)
-        tc = SmallTcc{cw.S, ccfg.w, ccfg.eps, (double)ccfg.m, ccfg.weight, ccfg.mode, cw.scal, cw.vprev, cw.uprev};
+        tc = SmallTcc{cw.S, ccfg.w, ccfg.eps, (double)ccfg.m, ccfg.weight, ccfg.mode, cw.scal, cw.vprev, cw.uprev,
+                      cw.fix};
       launch_small_minimize(d_params, d_state, W.p, m.p, v.p, covs.p, has_inc ? minc.p : nullptr,
                             has_exc ? mexc.p : nullptr, bc_table.p, d_ckpt, ckpt_cap, scarry.p, sprev.p, d, B,
                             stream, trek_on && trek_tcc ? &tc : nullptr, w32);

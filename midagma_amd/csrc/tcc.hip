@@ -321,12 +321,13 @@ __global__ __launch_bounds__(NB * NB) void tcc_blk_kernel(const double* __restri
                                                             double ws, int d, int64_t D, int mode, double eps,
                                                             double m, double weight, const State* __restrict__ st,
                                                             double* __restrict__ scal, double* __restrict__ vprev,
-                                                            double* __restrict__ uprev, double* __restrict__ G) {
+                                                            double* __restrict__ uprev, double* __restrict__ G,
+                                                            int fix) {
   if (!(st->status == ST_RUNNING && (mode == 2 || st->ckpt_pending))) return;  // tcc_gate_kernel's rule
   __shared__ TccLds<NB> L;
   tcc_blk_body<NB, 4>([&](int i, int j) { return W[(int64_t)i * D + j]; },
                    [&](int i, int j) { return S[(int64_t)i * D + j]; }, ws, d, mode, eps, m, weight, scal, vprev,
-                   uprev, G, D, L);
+                   uprev, G, D, L, fix != 0);
 }
 
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + EB - 1) / EB, 2048); }
@@ -553,7 +554,7 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
     const long nb = knob("MIDAGMA_EXP_TCC_NB", 0);  // experiments: force the block count
     auto go = [&](auto kern, int nt) {
       hipLaunchKernelGGL(kern, dim3(1), dim3(nt), 0, stream, W, w.S, cfg.w, (int)d, D, cfg.mode, cfg.eps,
-                         (double)cfg.m, cfg.weight, st, w.scal, w.vprev, w.uprev, Gtrek);
+                         (double)cfg.m, cfg.weight, st, w.scal, w.vprev, w.uprev, Gtrek, w.fix);
     };
     if ((nb == 8 || (nb == 0 && n <= 32)) && n <= 32)
       go(tcc_blk_kernel<8>, 64);

@@ -253,7 +253,7 @@ template <int NB, int BS, class WGet, class SGet>
 __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, int d, int mode, double eps, double m,
                                              double weight, double* __restrict__ scal, double* __restrict__ vprev,
                                              double* __restrict__ uprev, double* __restrict__ G, int64_t D,
-                                             TccLds<NB, BS>& L) {
+                                             TccLds<NB, BS>& L, bool fix = true) {
   constexpr int NM = TccBlk<NB, BS>::NM, VT = TccBlk<NB, BS>::VT, LA = TccLds<NB, BS>::LA;
   auto& rowb = L.rowb;
   auto& colb = L.colb;
@@ -304,7 +304,8 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
   double sc[10];
 #pragma unroll
   for (int t = 0; t < 10; ++t) sc[t] = scal[t];
-  if (w0) w0_init<NB, BS>(vprev, n, sc[9] != 0.0, sc[8] != 0.0, xs);
+  const bool conv_prev = sc[9] != 0.0;  // the last completed slot's solve converged
+  if (w0) w0_init<NB, BS>(vprev, n, conv_prev, sc[8] != 0.0, xs);
   __syncthreads();
   blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);
   if (w0) {  // tcc_sigma0_kernel
@@ -323,7 +324,80 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
   sc[7] = 0.0;
   sc[9] = 0.0;
   int ninv = 0;
-  for (int k = 0; k < TCC_NODA_MAX; ++k) {  // tcc_noda_kernel, until the stop rule
+  // the fixed-shift stage (tcc.hip tcc_fix_small_kernel: one inverse at sigma_0 (1 + 1e-14), then
+  // inverse iteration for v and u with the same convergence rule); Noda and the final inverse only
+  // when it does not converge in TCC_FIX_SWEEPS sweeps or breaks down
+  bool fixed = false;
+  if (fix) {
+    load_a(M);
+    blk_shift<BS>(M, n, a, b, sc[1] * (1.0 + 1e-14));
+    blk_gj_inverse<NB, BS>(M, n, a, b, act, rowb, colb, pivb);
+    ++ninv;
+    if (w0) w0_init<NB, BS>(uprev, n, conv_prev, sc[8] != 0.0, us);
+    __syncthreads();
+    const double sigs = sc[1] * (1.0 + 1e-14);
+    double ub = sc[1];
+    for (int k = 0; k < TCC_FIX_SWEEPS; ++k) {
+      blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);
+      blk_gemv_t<NB, BS>(M, a, b, act, us, part, zs);
+      if (w0) {
+        double vmin = INFINITY, vmax = -INFINITY, vss = 0.0, vs = 0.0;
+        double umin = INFINITY, umax = -INFINITY, uss = 0.0, usm = 0.0, bad = 0.0;
+#pragma unroll
+        for (int t = 0; t < VT; ++t) {
+          const int e = lane + 64 * t;
+          if (e < n) {
+            const double yi = ys[e], zi = zs[e];
+            if (!(yi > 0.0) || !isfinite(yi) || !(zi > 0.0) || !isfinite(zi)) bad = 1.0;
+            const double rv = xs[e] / yi, ru = us[e] / zi;
+            vmin = fmin(vmin, rv);
+            vmax = fmax(vmax, rv);
+            vss += yi * yi;
+            vs += yi;
+            umin = fmin(umin, ru);
+            umax = fmax(umax, ru);
+            uss += zi * zi;
+            usm += zi;
+          }
+        }
+        vmin = wave_reduce(vmin, Min());
+        vmax = wave_reduce(vmax, Max());
+        vss = wave_reduce(vss, Add());
+        vs = wave_reduce(vs, Add());
+        umin = wave_reduce(umin, Min());
+        umax = wave_reduce(umax, Max());
+        uss = wave_reduce(uss, Add());
+        usm = wave_reduce(usm, Add());
+        bad = wave_reduce(bad, Max());
+        double state = 2.0;  // 0 going on, 1 converged, 2 breakdown
+        if (!(bad != 0.0 || !(vss > 0.0) || !(uss > 0.0) || !isfinite(vss) || !isfinite(uss))) {
+          const double iv = (vs < 0.0 ? -1.0 : 1.0) / sqrt(vss), iu = (usm < 0.0 ? -1.0 : 1.0) / sqrt(uss);
+#pragma unroll
+          for (int t = 0; t < VT; ++t) {
+            const int e = lane + 64 * t;
+            if (e < n) {
+              xs[e] = ys[e] * iv;
+              us[e] = zs[e] * iu;
+            }
+          }
+          ub = fmin(ub, sigs - vmin);
+          state = (!(vmax - vmin > 1e-13 * vmin) && !(umax - umin > 1e-13 * umin)) ? 1.0 : 0.0;
+        }
+        if (lane == 0) {
+          scs[11] = state;
+          scs[12] = ub;
+        }
+      }
+      __syncthreads();
+      if (scs[11] != 0.0) break;
+    }
+    fixed = scs[11] == 1.0;
+    if (fixed)
+      sc[9] = 1.0;
+    else if (scs[11] == 0.0)
+      sc[1] = fmin(sc[1], scs[12]);  // Noda goes on from the stage's vector and bound
+  }
+  for (int k = 0; k < TCC_NODA_MAX && !fixed; ++k) {  // tcc_noda_kernel, until the stop rule
     ++ninv;
     load_a(M);
     blk_shift<BS>(M, n, a, b, sc[1]);
@@ -379,21 +453,23 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
     if (scs[10] != 0.0) break;
   }
   // the final inverse just above the root: two sweeps for v (x), two transposed for u
-  load_a(M);
-  blk_shift<BS>(M, n, a, b, sc[1] * (1.0 + 1e-14));
-  blk_gj_inverse<NB, BS>(M, n, a, b, act, rowb, colb, pivb);
-  ++ninv;
-  for (int t = 0; t < 2; ++t) {
-    blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);
-    if (w0) w0_normalize<NB, BS>(ys, n, xs);
+  if (!fixed) {
+    load_a(M);
+    blk_shift<BS>(M, n, a, b, sc[1] * (1.0 + 1e-14));
+    blk_gj_inverse<NB, BS>(M, n, a, b, act, rowb, colb, pivb);
+    ++ninv;
+    for (int t = 0; t < 2; ++t) {
+      blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);
+      if (w0) w0_normalize<NB, BS>(ys, n, xs);
+      __syncthreads();
+    }
+    if (w0) w0_init<NB, BS>(uprev, n, sc[9] != 0.0, sc[8] != 0.0, us);
     __syncthreads();
-  }
-  if (w0) w0_init<NB, BS>(uprev, n, sc[9] != 0.0, sc[8] != 0.0, us);
-  __syncthreads();
-  for (int t = 0; t < 2; ++t) {
-    blk_gemv_t<NB, BS>(M, a, b, act, us, part, ys);
-    if (w0) w0_normalize<NB, BS>(ys, n, us);
-    __syncthreads();
+    for (int t = 0; t < 2; ++t) {
+      blk_gemv_t<NB, BS>(M, a, b, act, us, part, ys);
+      if (w0) w0_normalize<NB, BS>(ys, n, us);
+      __syncthreads();
+    }
   }
   load_a(M);  // the inverse is no longer needed
   blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);  // A v

@@ -127,11 +127,11 @@ if __name__ == "__main__":
                 trek_case(d, "tcc", 300 if d <= 300 else 60)
         os.environ.pop("MIDAGMA_EXP_TCC_FAST_STEPS")
     if which == "tccfix":  # TCC (2d > 128): the fixed-shift stage first (one inverse), or Noda from the warm start
-        for d in [int(x) for x in sys.argv[2:]] or [100, 300, 1000]:
+        for d in [int(x) for x in sys.argv[2:]] or [20, 64, 100, 300, 1000]:
             for f in ("1", "0", "1"):
                 os.environ["MIDAGMA_EXP_TCC_FIX"] = f
                 print(f"MIDAGMA_EXP_TCC_FIX={f}", end=" ")
-                trek_case(d, "tcc", 300 if d <= 300 else 60)
+                trek_case(d, "tcc", 2000 if d <= 64 else (300 if d <= 300 else 60))
         os.environ.pop("MIDAGMA_EXP_TCC_FIX")
     if which == "tccbinv":  # TCC (2d >= 512): the shifted inverses on the blocked inverse, or the flat Gauss-Jordan
         for d in [int(x) for x in sys.argv[2:]] or [300, 1000]:
