@@ -424,7 +424,10 @@ struct midagma_solver {
   // build_at folded into the previous slot's update (MIDAGMA_EXP_AT_FOLD): fast slots read outer
   // step 0's A^T from A0, which fused_update_at (fast slots) or a build_at after the update (slow
   // slots) wrote from the slot's new W; every call starts with a slow slot, so A0 is never stale
-  bool at_fold = knob("MIDAGMA_EXP_AT_FOLD", 0) != 0;
+  // Measured (profiles/r06_probe_atfold.log): D = 1024 +1.7 %, 1408 +0.6 %, 512 -4 % (128 update
+  // workgroups of 8 rows x 256 columns), 2048 -1.2 %; on for 1024 <= D <= 1408 (-1: that rule)
+  long at_fold_knob = knob("MIDAGMA_EXP_AT_FOLD", -1);
+  bool at_fold = at_fold_knob > 0;
   DevBuf A0;
   bool at_fold_on() const {
     if (!at_fold || !A0.p || cov_fork_on()) return false;
@@ -786,6 +789,7 @@ struct midagma_solver {
     // cov mode: build_at also writes I - W for the score GEMM's plain-B form
     if (mode == MIDAGMA_MODE_COV && ((D % 128 == 0 && cov_iw) || w32)) IW.alloc(DD);
     // the next slot's A^T written by fused_update_at (at_fold_on)
+    if (at_fold_knob < 0) at_fold = D >= 1024 && D <= 1408;
     if (at_fold && mode == MIDAGMA_MODE_COV && B2 > 0) A0.alloc(DD);
     if (blocked() || data_binv_on()) {
       const int64_t b2 = binv_block(D);

@@ -362,7 +362,7 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
                                                              double* __restrict__ scal, State* __restrict__ gates,
                                                              const State* __restrict__ gate) {
   if (!gate_on(gate)) return;
-  __shared__ double xs[256], us[256], ys[256], zp[16][256], red[9][16];
+  __shared__ double xs[256], us[256], ys[256], zp[16][256], red[9][16], gsh[9];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < 256) {
     xs[tid] = tid < n ? x[tid] : 0.0;
@@ -372,25 +372,51 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
   const double sig = scal[1] * (1.0 + kFixMargin);
   bool vok = false, uok = false, bad = false;
   double ub = scal[1];
+  int sweeps = 0;
   for (int k = 0; k < TCC_FIX_SWEEPS && !(vok && uok); ++k) {
-    double z[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int t = 0; t < 16; ++t) {
-      const int i = wv + 16 * t;
-      if (i >= n) break;
-      const double ui = us[i];
-      const double* __restrict__ row = Mi + (int64_t)i * ld;
-      double acc = 0.0;
+    ++sweeps;
+    // this wave's 16 rows (wv + 16 t) in batches of 4, each batch's loads issued before its
+    // reduction
+    double z[4] = {0.0, 0.0, 0.0, 0.0}, xv[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        if (j < n) {
-          const double mij = row[j];
-          acc += mij * xs[j];
+    for (int q = 0; q < 4; ++q) xv[q] = xs[lane + 64 * q];  // (0 past n)
+#pragma unroll 1
+    for (int bt = 0; bt < 4; ++bt) {
+      double acc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int i = wv + 16 * (4 * bt + t);
+        const bool rin = i < n;
+        const double ui = rin ? us[i] : 0.0;
+        const double* __restrict__ row = Mi + (int64_t)(rin ? i : 0) * ld;
+        double a = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = lane + 64 * q;
+          const double mij = (rin && j < n) ? row[j] : 0.0;
+          a += mij * xv[q];
           z[q] += mij * ui;
         }
+        acc[t] = a;
       }
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-      if (lane == 0) ys[i] = acc;
+      // the 4 row sums over the wave's lanes, halving the values per lane at each exchange (fixed
+      // order): lane bits 5..4 end up selecting the row, bits 3..0 the last four sums
+#pragma unroll
+      for (int h = 2, off = 32; h >= 1; h >>= 1, off >>= 1) {
+        const bool hi = (lane & off) != 0;
+#pragma unroll
+        for (int t = 0; t < h; ++t) {
+          const double keep = hi ? acc[t + h] : acc[t], send = hi ? acc[t] : acc[t + h];
+          acc[t] = keep + __shfl_xor(send, off);
+        }
+      }
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) acc[0] += __shfl_xor(acc[0], off);
+      if ((lane & 15) == 0) {
+        const int r = ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1);
+        const int i = wv + 16 * (4 * bt + r);
+        if (i < n) ys[i] = acc[0];
+      }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) zp[wv][lane + 64 * q] = z[q];
@@ -420,16 +446,19 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
       if (lane == 0) red[c][wv] = a;
     }
     __syncthreads();
-    double g[9];
-#pragma unroll
-    for (int c = 0; c < 9; ++c) {
+    if (tid < 9) {  // field tid over the 16 waves, in wave order
+      const int c = tid;
       double a = red[c][0];
       for (int w2 = 1; w2 < 16; ++w2) {
         const double b = red[c][w2];
         a = (c == 0 || c == 4) ? fmin(a, b) : ((c == 1 || c == 5 || c == 8) ? fmax(a, b) : a + b);
       }
-      g[c] = a;
+      gsh[c] = a;
     }
+    __syncthreads();
+    double g[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) g[c] = gsh[c];
     if (g[8] != 0.0 || !(g[2] > 0.0) || !(g[6] > 0.0) || !isfinite(g[2]) || !isfinite(g[6])) {
       bad = true;  // (x, u keep the last good sweep's vectors)
       break;
@@ -452,6 +481,7 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
     scal[12] = uok ? 1.0 : 0.0;
     scal[13] = bad ? 1.0 : 0.0;
     scal[14] = ub;
+    scal[15] = (double)sweeps;  // (diagnostic)
     tcc_fix_finish(scal, gates);
   }
 }
@@ -602,7 +632,11 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
       hipLaunchKernelGGL(tcc_fix_done_kernel, dim3(1), dim3(64), 0, stream, w.scal, w.gates, g0);
     }
   }
-  const int nsteps = handback ? std::min(std::max(steps, 1), TCC_NODA_MAX - 1) : TCC_NODA_MAX;
+  // the fast slot's chain (handback): with the fixed-shift stage, a slot it does not settle hands
+  // back at once (no Noda step and no final inverse enqueued: their gated launches alone cost more
+  // than the stage); without it, `steps` Noda steps first
+  const bool lean = handback && w.fix;
+  const int nsteps = lean ? 0 : (handback ? std::min(std::max(steps, 1), TCC_NODA_MAX - 1) : TCC_NODA_MAX);
   for (int k = 0; k < nsteps; ++k) {
     const State* gk = &w.gates[1 + k];
     hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
@@ -616,18 +650,20 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   // final inverse just above the converged root: two sweeps for v, two (transposed) for u (the
   // Noda path: gated off when the fixed-shift stage converged)
   const State* gf = &w.gates[TCC_GATE_FINAL];
-  hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
-                     w.scal, 1e-14, gf);
-  tcc_inverse(w, gj, gf, stream);
-  for (int r = 0; r < 2; ++r) {
-    hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gf);
-    hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.x, n, gf);
-  }
-  hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.uprev, w.u, n, w.scal, gf);
-  for (int r = 0; r < 2; ++r) {
-    hipLaunchKernelGGL(tcc_gemv_t_partial_kernel, gt, dim3(EB), 0, stream, w.Mi, D2, n, w.u, w.part, gf);
-    hipLaunchKernelGGL(tcc_gemv_t_sum_kernel, gts, dim3(EB), 0, stream, w.part, D2, n, nchunks, w.y, gf);
-    hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.u, n, gf);
+  if (!lean) {
+    hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
+                       w.scal, 1e-14, gf);
+    tcc_inverse(w, gj, gf, stream);
+    for (int r = 0; r < 2; ++r) {
+      hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gf);
+      hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.x, n, gf);
+    }
+    hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.uprev, w.u, n, w.scal, gf);
+    for (int r = 0; r < 2; ++r) {
+      hipLaunchKernelGGL(tcc_gemv_t_partial_kernel, gt, dim3(EB), 0, stream, w.Mi, D2, n, w.u, w.part, gf);
+      hipLaunchKernelGGL(tcc_gemv_t_sum_kernel, gts, dim3(EB), 0, stream, w.part, D2, n, nchunks, w.y, gf);
+      hipLaunchKernelGGL(tcc_normalize_kernel, dim3(1), dim3(EB), 0, stream, w.y, w.u, n, gf);
+    }
   }
   // rho (Rayleigh), the lower bound through B, value; then the gradient
   hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 0, w.x, w.y, g0);
