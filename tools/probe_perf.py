@@ -133,9 +133,9 @@ if __name__ == "__main__":
                 print(f"MIDAGMA_EXP_TCC_FIX={f}", end=" ")
                 trek_case(d, "tcc", 2000 if d <= 64 else (300 if d <= 300 else 60))
         os.environ.pop("MIDAGMA_EXP_TCC_FIX")
-    if which == "tccbinv":  # TCC (2d >= 512): the shifted inverses on the blocked inverse, or the flat Gauss-Jordan
-        for d in [int(x) for x in sys.argv[2:]] or [300, 1000]:
-            for f in ("1", "0", "1", "0"):
+    if which == "tccbinv":  # TCC (D2 >= 512): the shifted inverses on the blocked inverse (2), or the flat Gauss-Jordan (0)
+        for d in [int(x) for x in sys.argv[2:]] or [300, 500, 1000]:
+            for f in ("2", "0", "2", "0"):
                 os.environ["MIDAGMA_EXP_TCC_BINV"] = f
                 print(f"MIDAGMA_EXP_TCC_BINV={f}", end=" ")
                 trek_case(d, "tcc", 300 if d <= 300 else 60)
