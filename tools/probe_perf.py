@@ -83,6 +83,31 @@ def trek_case(d, seq, K):
     s.close()
 
 
+def trek_phase(d, warm, K, fix):
+    """TCC on a fit's later W: `warm` untimed steps from W = 0, then K timed steps (hand-backs of
+    the timed part only)"""
+    os.environ["MIDAGMA_EXP_TCC_FIX"] = fix
+    X, _, _ = make_dataset(d, 2 * d, seed=0)
+    X -= X.mean(0)
+    s = HipSolver(d, "l2", "cov")
+    s.set_cov(X.T @ X / X.shape[0])
+    rng = np.random.default_rng(0)
+    iu = np.array(np.triu_indices(d, 1)).T
+    pairs = iu[rng.uniform(size=len(iu)) < 0.3]
+    s.set_trek_tcc(pairs, mode="opt", weight=0.1)
+    s.begin(np.zeros((d, d)), 1.0, warm + K + 1000, 1.0, 3e-4, tol=-1.0)
+    s.run_slots(warm)
+    s.sync()
+    b0 = s.debug_handbacks()
+    t0 = time.perf_counter()
+    s.run_slots(K)
+    s.sync()
+    dt = time.perf_counter() - t0
+    print(f"MIDAGMA_EXP_TCC_FIX={fix} cov+TCC d={d} after {warm} steps: {K / dt:.1f} steps/s "
+          f"({dt / K * 1e3:.3f} ms/step) hand-backs {s.debug_handbacks() - b0} of {K}", flush=True)
+    s.close()
+
+
 def fit_case(d, n):
     from midagma_amd import DagmaLinear
     X, _, _ = make_dataset(d, n, seed=0)
@@ -132,6 +157,11 @@ if __name__ == "__main__":
                 os.environ["MIDAGMA_EXP_TCC_FIX"] = f
                 print(f"MIDAGMA_EXP_TCC_FIX={f}", end=" ")
                 trek_case(d, "tcc", 2000 if d <= 64 else (300 if d <= 300 else 60))
+        os.environ.pop("MIDAGMA_EXP_TCC_FIX")
+    if which == "tccphase":  # TCC after a fit's first steps: the fixed-shift stage on / off
+        for d, warm, K in ((100, 2000, 300), (300, 1000, 200), (1000, 200, 40)):
+            for f in ("1", "0"):
+                trek_phase(d, warm, K, f)
         os.environ.pop("MIDAGMA_EXP_TCC_FIX")
     if which == "tccbinv":  # TCC (D2 >= 512): the shifted inverses on the blocked inverse (2), or the flat Gauss-Jordan (0)
         for d in [int(x) for x in sys.argv[2:]] or [300, 500, 1000]:
