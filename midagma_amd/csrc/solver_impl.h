@@ -717,11 +717,12 @@ struct midagma_solver {
     w.part = cpart.p;
     w.gates = cgates;
     w.fix = tcc_fix != 0 ? 1 : 0;
-    // D2 >= 1024: the shifted inverses on the two-level blocked inverse (pivoted path; measured,
-    // profiles/r06_probe_tccbinv.log: d = 1000 6.15 -> 5.53 ms a step, but d = 300 (D2 = 640) 0.97 ->
-    // 1.18 ms; MIDAGMA_EXP_TCC_BINV=0: always the flat Gauss-Jordan, 2: from D2 >= 512)
+    // D2 >= 2048: the shifted inverses on the two-level blocked inverse (pivoted path; measured,
+    // profiles/r06_probe_tccbinv2.log: d = 1000 (D2 = 2048) 6.01 -> 5.36 ms a step, but d = 500
+    // (D2 = 1024) 2.04 -> 2.41 and d = 300 (D2 = 640) 1.07 -> 1.34 ms; MIDAGMA_EXP_TCC_BINV=0: always
+    // the flat Gauss-Jordan, 2: from D2 >= 512)
     const long tbinv = knob("MIDAGMA_EXP_TCC_BINV", 1);
-    if (D2 >= (tbinv == 2 ? 512 : 1024) && binv_block(D2) > 0 && tbinv != 0) {
+    if (D2 >= (tbinv == 2 ? 512 : 2048) && binv_block(D2) > 0 && tbinv != 0) {
       const int64_t b2 = binv_block(D2);
       cAalt.alloc((size_t)D2 * D2);
       cPst.alloc((size_t)D2 * b2);

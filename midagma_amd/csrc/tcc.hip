@@ -547,7 +547,7 @@ __global__ void tcc_fix_done_kernel(double* __restrict__ scal, State* __restrict
 
 
 // the shifted inverse: the two-level blocked one (pivoted path: 256-blocks, panels, MFMA trailing
-// updates) where the solver allocated its buffers (D2 >= 1024), else the flat 32-block Gauss-Jordan
+// updates) where the solver allocated its buffers (D2 >= 2048), else the flat 32-block Gauss-Jordan
 BInvWork tcc_binv(const TccWork& w) {
   BInvWork b{};
   b.Aalt = w.Aalt;
