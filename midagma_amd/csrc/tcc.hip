@@ -611,6 +611,23 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.vprev, w.x, n, w.scal, g0);
   hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 0, w.x, w.y, g0);
   hipLaunchKernelGGL(tcc_sigma0_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, g0);
+  // one Noda step (tcc_noda_kernel's update; gate 1 + k)
+  auto noda_step = [&](int k) {
+    const State* gk = &w.gates[1 + k];
+    hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
+                       w.scal, 0.0, gk);
+    tcc_inverse(w, gj, gk, stream);
+    hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gk);
+    hipLaunchKernelGGL(tcc_noda_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, w.gates, k, TCC_NODA_MAX,
+                       gk);
+  };
+  // the fast slot's chain (handback): with the fixed-shift stage, `fix_pre` Noda steps (whose shift
+  // update brings sigma much closer to rho than the warm start's bound), then the stage, and a slot
+  // that is still not settled hands back at once (no further Noda step and no final inverse
+  // enqueued: their gated launches alone cost more than the stage); without it, `steps` Noda steps
+  const bool lean = handback && w.fix;
+  const int pre = lean ? std::max(0, std::min(w.fix_pre, TCC_NODA_MAX - 1)) : 0;
+  for (int k = 0; k < pre; ++k) noda_step(k);
   // the fixed-shift stage (w.fix = 0, MIDAGMA_EXP_TCC_FIX=0: Noda from the warm start at once)
   if (w.fix) {
     hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
@@ -632,20 +649,8 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
       hipLaunchKernelGGL(tcc_fix_done_kernel, dim3(1), dim3(64), 0, stream, w.scal, w.gates, g0);
     }
   }
-  // the fast slot's chain (handback): with the fixed-shift stage, a slot it does not settle hands
-  // back at once (no Noda step and no final inverse enqueued: their gated launches alone cost more
-  // than the stage); without it, `steps` Noda steps first
-  const bool lean = handback && w.fix;
   const int nsteps = lean ? 0 : (handback ? std::min(std::max(steps, 1), TCC_NODA_MAX - 1) : TCC_NODA_MAX);
-  for (int k = 0; k < nsteps; ++k) {
-    const State* gk = &w.gates[1 + k];
-    hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
-                       w.scal, 0.0, gk);
-    tcc_inverse(w, gj, gk, stream);
-    hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gk);
-    hipLaunchKernelGGL(tcc_noda_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, w.gates, k, TCC_NODA_MAX,
-                       gk);
-  }
+  for (int k = 0; k < nsteps; ++k) noda_step(k);
   if (handback) hipLaunchKernelGGL(tcc_handback_kernel, dim3(1), dim3(64), 0, stream, handback, w.gates, nsteps);
   // final inverse just above the converged root: two sweeps for v, two (transposed) for u (the
   // Noda path: gated off when the fixed-shift stage converged)
