@@ -293,11 +293,14 @@ void launch_trek_pst(const double* W, int64_t d, int64_t D, const TrekCfg& cfg, 
 constexpr int TCC_NODA_MAX = 24;     // Noda steps per slot (gated off once converged)
 // the fixed-shift stage (tcc.hip): inverse iteration for v and u at the warm start's
 // Collatz-Wielandt bound, at most TCC_FIX_SWEEPS sweeps; gate words after the Noda steps' ones:
-// [TCC_GATE_FINAL] the Noda path's final inverse, [TCC_GATE_FIX0 + k] sweep k (2d > 256)
+// [TCC_GATE_FINAL] the Noda path's final inverse, [TCC_GATE_FIX0 + k] sweep k (2d > 256),
+// [TCC_GATE_PRE] a fast slot's Noda steps before the stage (on when the last stage was hard)
 constexpr int TCC_FIX_SWEEPS = 8;
+constexpr int TCC_FIX_EASY = 4;  // a stage settled in at most this many sweeps needs no Noda step before it
 constexpr int TCC_GATE_FINAL = 1 + TCC_NODA_MAX;
 constexpr int TCC_GATE_FIX0 = TCC_GATE_FINAL + 1;
-constexpr int TCC_GATES = TCC_GATE_FIX0 + TCC_FIX_SWEEPS;
+constexpr int TCC_GATE_PRE = TCC_GATE_FIX0 + TCC_FIX_SWEEPS;
+constexpr int TCC_GATES = TCC_GATE_PRE + 1;
 struct TccCfg {
   int mode;              // 1 'log', 2 'opt' (as TrekCfg)
   double weight, w, eps; // regularizer weight, multiplier of S, the reference's eps
@@ -313,6 +316,7 @@ struct TccWork {
   double* scal;          // [0] value [1] sigma [2] lower [3] rho [4] u.v+eps [5] u.u+eps [7] breakdown [8] warm
                          // [9] converged (this slot) [10] converged (the last completed slot)
                          // fixed-shift stage: [11] v converged [12] u converged [13] breakdown [14] upper bound
+                         // [15] sweeps to converge (0: none did) [16] hard (kept across slots)
   State* gates;          // TCC_GATES gate words
   // the two-level blocked inverse's buffers for D2 (pivoted path: Aalt D2 x D2, Pst / Pst1 D2 x B2);
   // null: the flat Gauss-Jordan
@@ -320,7 +324,7 @@ struct TccWork {
   double* Pst = nullptr;
   double* Pst1 = nullptr;
   int fix = 1;  // the fixed-shift stage first (2d > 128; 0: Noda from the warm start at once)
-  int fix_pre = 1;  // fast slots: Noda steps before the fixed-shift stage
+  int fix_pre = 1;  // fast slots: Noda steps before the fixed-shift stage when the last stage was hard
 };
 // The TCC penalty of W (value in w.scal[0]) and, in 'opt' mode, weight * d value / d W into
 // Gtrek (D x D), gated like launch_trek_pst.

@@ -694,7 +694,7 @@ struct midagma_solver {
     cA.alloc((size_t)D2 * D2);
     cMi.alloc((size_t)D2 * D2);
     cS.alloc((size_t)D * D);
-    cvec.alloc((size_t)6 * D2 + 16);
+    cvec.alloc((size_t)6 * D2 + 32);
     cpart.alloc((size_t)nch * D2);
     cP.alloc(2 * 32 * 32);
     cR.alloc((size_t)2 * 32 * D2);

@@ -62,10 +62,12 @@ struct Max {
   __device__ double operator()(double a, double b) const { return fmax(a, b); }
 };
 
-__global__ void tcc_gate_kernel(const State* __restrict__ st, int mode, State* __restrict__ gates, int nmax) {
+__global__ void tcc_gate_kernel(const State* __restrict__ st, int mode, State* __restrict__ gates, int nmax,
+                                const double* __restrict__ scal) {
   if (threadIdx.x != 0) return;
   const bool on = st->status == ST_RUNNING && (mode == 2 || st->ckpt_pending);
   for (int t = 0; t <= nmax; ++t) gates[t].status = on ? ST_RUNNING : ST_DONE;
+  if (TCC_GATE_PRE <= nmax) gates[TCC_GATE_PRE].status = on && scal[16] != 0.0 ? ST_RUNNING : ST_DONE;
 }
 
 // A = [[W o W, w S], [I, (W o W)^T]] on the logical 2d x 2d block, zero padding (D2 x D2)
@@ -168,7 +170,8 @@ __global__ void tcc_sigma0_kernel(const double* __restrict__ x, const double* __
     scal[7] = 0.0;  // breakdown flag
     scal[9] = 0.0;  // converged flag
     scal[11] = scal[12] = scal[13] = 0.0;  // the fixed-shift stage's flags
-    scal[14] = mx;                         // ... and its upper bound
+    scal[14] = mx;                         // ... its upper bound
+    scal[15] = 0.0;                        // ... and its sweep count
   }
 }
 
@@ -347,7 +350,9 @@ constexpr double kFixTol = 1e-13;
 
 // the stage's outcome (thread 0): converged -> Noda and the final inverse gated off
 __device__ void tcc_fix_finish(double* __restrict__ scal, State* __restrict__ gates) {
-  if (scal[11] != 0.0 && scal[12] != 0.0 && scal[13] == 0.0) {
+  const bool ok = scal[11] != 0.0 && scal[12] != 0.0 && scal[13] == 0.0;
+  scal[16] = ok && scal[15] <= (double)TCC_FIX_EASY ? 0.0 : 1.0;  // the next fast slot's Noda step
+  if (ok) {
     scal[9] = 1.0;
     for (int t = 1; t <= TCC_GATE_FINAL; ++t) gates[t].status = ST_DONE;
   } else if (scal[13] == 0.0) {
@@ -481,7 +486,7 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
     scal[12] = uok ? 1.0 : 0.0;
     scal[13] = bad ? 1.0 : 0.0;
     scal[14] = ub;
-    scal[15] = (double)sweeps;  // (diagnostic)
+    scal[15] = vok && uok ? (double)sweeps : 0.0;
     tcc_fix_finish(scal, gates);
   }
 }
@@ -531,6 +536,7 @@ __global__ void tcc_fix_update_kernel(double* __restrict__ x, const double* __re
       scal[11] = vok ? 1.0 : 0.0;
       scal[12] = uok ? 1.0 : 0.0;
       scal[14] = fmin(scal[14], scal[1] * (1.0 + kFixMargin) - vmin);
+      if (done) scal[15] = (double)(k + 1);
     }
   } else if (threadIdx.x == 0) {
     scal[13] = 1.0;
@@ -597,7 +603,7 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   }
   State* g0 = w.gates;
   const double m = (double)cfg.m;
-  hipLaunchKernelGGL(tcc_gate_kernel, dim3(1), dim3(64), 0, stream, st, cfg.mode, w.gates, TCC_GATES - 1);
+  hipLaunchKernelGGL(tcc_gate_kernel, dim3(1), dim3(64), 0, stream, st, cfg.mode, w.gates, TCC_GATES - 1, w.scal);
   hipLaunchKernelGGL(tcc_build_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, W, w.S, cfg.w, d, D, D2, w.A,
                      g0);
   const dim3 gv((unsigned)((n + 3) / 4));
@@ -611,9 +617,8 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.vprev, w.x, n, w.scal, g0);
   hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.A, D2, n, d, 0, w.x, w.y, g0);
   hipLaunchKernelGGL(tcc_sigma0_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, g0);
-  // one Noda step (tcc_noda_kernel's update; gate 1 + k)
-  auto noda_step = [&](int k) {
-    const State* gk = &w.gates[1 + k];
+  // one Noda step (tcc_noda_kernel's update; gate 1 + k, or gk)
+  auto noda_step = [&](int k, const State* gk) {
     hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
                        w.scal, 0.0, gk);
     tcc_inverse(w, gj, gk, stream);
@@ -621,13 +626,14 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
     hipLaunchKernelGGL(tcc_noda_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, n, w.scal, w.gates, k, TCC_NODA_MAX,
                        gk);
   };
-  // the fast slot's chain (handback): with the fixed-shift stage, `fix_pre` Noda steps (whose shift
-  // update brings sigma much closer to rho than the warm start's bound), then the stage, and a slot
-  // that is still not settled hands back at once (no further Noda step and no final inverse
-  // enqueued: their gated launches alone cost more than the stage); without it, `steps` Noda steps
+  // the fast slot's chain (handback): with the fixed-shift stage, `fix_pre` Noda steps when the last
+  // stage was hard (took more than TCC_FIX_EASY sweeps or did not settle: their shift update brings
+  // sigma much closer to rho than the warm start's bound), then the stage, and a slot that is still
+  // not settled hands back at once (no further Noda step and no final inverse enqueued: their gated
+  // launches alone cost more than the stage); without it, `steps` Noda steps
   const bool lean = handback && w.fix;
   const int pre = lean ? std::max(0, std::min(w.fix_pre, TCC_NODA_MAX - 1)) : 0;
-  for (int k = 0; k < pre; ++k) noda_step(k);
+  for (int k = 0; k < pre; ++k) noda_step(k, &w.gates[TCC_GATE_PRE]);
   // the fixed-shift stage (w.fix = 0, MIDAGMA_EXP_TCC_FIX=0: Noda from the warm start at once)
   if (w.fix) {
     hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
@@ -650,7 +656,7 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
     }
   }
   const int nsteps = lean ? 0 : (handback ? std::min(std::max(steps, 1), TCC_NODA_MAX - 1) : TCC_NODA_MAX);
-  for (int k = 0; k < nsteps; ++k) noda_step(k);
+  for (int k = 0; k < nsteps; ++k) noda_step(k, &w.gates[1 + k]);
   if (handback) hipLaunchKernelGGL(tcc_handback_kernel, dim3(1), dim3(64), 0, stream, handback, w.gates, nsteps);
   // final inverse just above the converged root: two sweeps for v, two (transposed) for u (the
   // Noda path: gated off when the fixed-shift stage converged)
