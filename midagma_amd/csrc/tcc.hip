@@ -378,7 +378,7 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
   bool vok = false, uok = false, bad = false;
   double ub = scal[1];
   int sweeps = 0;
-  for (int k = 0; k < TCC_FIX_SWEEPS && !(vok && uok); ++k) {
+  for (int k = 0; k < TCC_FIX_SWEEPS_SMALL && !(vok && uok); ++k) {
     ++sweeps;
     // this wave's 16 rows (wv + 16 t) in batches of 4, each batch's loads issued before its
     // reduction

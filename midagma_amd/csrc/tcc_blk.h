@@ -326,7 +326,7 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
   int ninv = 0;
   // the fixed-shift stage (tcc.hip tcc_fix_small_kernel: one inverse at sigma_0 (1 + 1e-14), then
   // inverse iteration for v and u with the same convergence rule); Noda and the final inverse only
-  // when it does not converge in TCC_FIX_SWEEPS sweeps or breaks down
+  // when it does not converge in TCC_FIX_SWEEPS_SMALL sweeps or breaks down
   bool fixed = false;
   if (fix) {
     load_a(M);
@@ -337,7 +337,7 @@ __device__ __forceinline__ void tcc_blk_body(WGet wget, SGet sget, double ws, in
     __syncthreads();
     const double sigs = sc[1] * (1.0 + 1e-14);
     double ub = sc[1];
-    for (int k = 0; k < TCC_FIX_SWEEPS; ++k) {
+    for (int k = 0; k < TCC_FIX_SWEEPS_SMALL; ++k) {
       blk_gemv<NB, BS>(M, a, b, act, false, d, xs, ys);
       blk_gemv_t<NB, BS>(M, a, b, act, us, part, zs);
       if (w0) {
