@@ -297,7 +297,8 @@ constexpr int TCC_NODA_MAX = 24;     // Noda steps per slot (gated off once conv
 // [TCC_GATE_PRE] a fast slot's Noda steps before the stage (on when the last stage was hard)
 constexpr int TCC_FIX_SWEEPS = 8;        // (2d > 256: four launches a sweep)
 constexpr int TCC_FIX_SWEEPS_SMALL = 16; // (2d <= 256: one workgroup, a few microseconds a sweep)
-constexpr int TCC_FIX_EASY = 6;  // a stage settled in at most this many sweeps needs no Noda step before it
+// a stage settled in at most half its sweep budget needs no Noda step before the next one
+constexpr int TCC_FIX_EASY = TCC_FIX_SWEEPS / 2, TCC_FIX_EASY_SMALL = TCC_FIX_SWEEPS_SMALL / 2;
 constexpr int TCC_GATE_FINAL = 1 + TCC_NODA_MAX;
 constexpr int TCC_GATE_FIX0 = TCC_GATE_FINAL + 1;
 constexpr int TCC_GATE_PRE = TCC_GATE_FIX0 + TCC_FIX_SWEEPS;

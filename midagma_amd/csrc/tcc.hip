@@ -349,9 +349,9 @@ constexpr double kFixMargin = 1e-14;
 constexpr double kFixTol = 1e-13;
 
 // the stage's outcome (thread 0): converged -> Noda and the final inverse gated off
-__device__ void tcc_fix_finish(double* __restrict__ scal, State* __restrict__ gates) {
+__device__ void tcc_fix_finish(double* __restrict__ scal, State* __restrict__ gates, int easy) {
   const bool ok = scal[11] != 0.0 && scal[12] != 0.0 && scal[13] == 0.0;
-  scal[16] = ok && scal[15] <= (double)TCC_FIX_EASY ? 0.0 : 1.0;  // the next fast slot's Noda step
+  scal[16] = ok && scal[15] <= (double)easy ? 0.0 : 1.0;  // the next fast slot's Noda step
   if (ok) {
     scal[9] = 1.0;
     for (int t = 1; t <= TCC_GATE_FINAL; ++t) gates[t].status = ST_DONE;
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
     scal[13] = bad ? 1.0 : 0.0;
     scal[14] = ub;
     scal[15] = vok && uok ? (double)sweeps : 0.0;
-    tcc_fix_finish(scal, gates);
+    tcc_fix_finish(scal, gates, TCC_FIX_EASY_SMALL);
   }
 }
 
@@ -548,7 +548,7 @@ __global__ void tcc_fix_update_kernel(double* __restrict__ x, const double* __re
 __global__ void tcc_fix_done_kernel(double* __restrict__ scal, State* __restrict__ gates,
                                     const State* __restrict__ gate) {
   if (!gate_on(gate) || threadIdx.x != 0) return;
-  tcc_fix_finish(scal, gates);
+  tcc_fix_finish(scal, gates, TCC_FIX_EASY);
 }
 
 
