@@ -202,7 +202,9 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
       s->Y.alloc(2 * nx + (size_t)(sig_tiles + 1) / 2);
       HIP_TRY(hipMemsetAsync(s->Y.p + 2 * nx, 0, (size_t)(sig_tiles + 1) / 2 * sizeof(double), s->stream));
     } else {
-      s->Y.alloc(nx);
+      // experiments build: Y placed MIDAGMA_EXP_Y_OFFSET bytes into its allocation (L2 set
+      // aliasing between X and Y in the X^T Y GEMM)
+      s->Y.alloc_shifted(nx, (size_t)knob("MIDAGMA_EXP_Y_OFFSET", 0) / sizeof(double));
     }
     HIP_TRY(hipMemsetAsync(s->X.p, 0, nx * sizeof(double), s->stream));
     HIP_TRY(hipMemcpy2DAsync(s->X.p, D * sizeof(double), X, s->d * sizeof(double), s->d * sizeof(double), n_local,

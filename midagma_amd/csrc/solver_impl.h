@@ -31,15 +31,25 @@ namespace midagma {
 struct DevBuf {
   double* p = nullptr;
   size_t n = 0;
+  double* base = nullptr;  // the allocation (p = base + an offset, alloc_shifted)
   void alloc(size_t count) {
-    if (count <= n && p) return;
+    if (count <= n && p && p == base) return;
     release();
-    HIP_TRY(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(double)));
+    HIP_TRY(hipMalloc(&base, std::max<size_t>(count, 1) * sizeof(double)));
+    p = base;
+    n = count;
+  }
+  // count entries starting `off` entries into a fresh allocation (placement experiments)
+  void alloc_shifted(size_t count, size_t off) {
+    if (off == 0) return alloc(count);
+    release();
+    HIP_TRY(hipMalloc(&base, (count + off) * sizeof(double)));
+    p = base + off;
     n = count;
   }
   void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
+    if (base) (void)hipFree(base);
+    base = p = nullptr;
     n = 0;
   }
 };
