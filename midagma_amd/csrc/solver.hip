@@ -189,6 +189,10 @@ int midagma_set_data(midagma_solver* s, const double* X, int64_t n_local, int64_
     s->n_global = n_global;
     s->n_pad = (n_local + 127) / 128 * 128;
     const size_t nx = (size_t)s->n_pad * D;
+    // experiments build: MIDAGMA_EXP_PREPAD_MB of device memory allocated (and kept) before X, to
+    // move X, X^T and Y elsewhere (the X^T Y GEMM's fetched bytes against placement)
+    if (const long pad = knob("MIDAGMA_EXP_PREPAD_MB", 0); pad > 0 && !s->prepad.p)
+      s->prepad.alloc((size_t)pad << 17);
     s->X.alloc(nx);
     // logistic with few 128-tiles: the sigmoid GEMM in two serial K halves when its last round of
     // tiles would be at most half full (n = 1e4, d = 1000: 632 tiles for 512 resident slots)

@@ -127,6 +127,7 @@ struct midagma_solver {
   // X^T (D x n_pad), the xw GEMM's A operand in the m-contiguous layout (the X^T Y GEMM reads
   // X itself that way); kept when the device has the room (MIDAGMA_NO_XT disables it)
   DevBuf XT;
+  DevBuf prepad;  // (experiments: MIDAGMA_EXP_PREPAD_MB)
   DevBuf IW;  // I - W of the slot, written by build_at for the data-mode X (I - W) GEMM
   bool use_xt = false;
   const double* xw_a() const { return use_xt ? XT.p : X.p; }
