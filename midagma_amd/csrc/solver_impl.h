@@ -526,7 +526,10 @@ struct midagma_solver {
   // iw (nullable): I - W already formed (build_at), the plain-B form of the GEMM
   void enqueue_data_partial(const double* Wp, const State* st, const double* iw = nullptr) {
     if (loss == MIDAGMA_LOSS_L2) {
-      launch_gemm(n_pad, D, Kd(), xw_a(), xw_lda(), use_xt, iw ? iw : Wp, D, iw ? B_PLAIN : B_IMINUS, Y.p, D, EPI_STORE, 1,
+      // (experiments build, MIDAGMA_EXP_XW_FULLK=1: the k loop over all of D, as round 4 ran it)
+      static const int64_t kfull = knob("MIDAGMA_EXP_XW_FULLK", 0);
+      launch_gemm(n_pad, D, kfull ? D : Kd(), xw_a(), xw_lda(), use_xt, iw ? iw : Wp, D, iw ? B_PLAIN : B_IMINUS, Y.p, D,
+                  EPI_STORE, 1,
                   0, nullptr, 0, 0, st, stream);
     } else {
       launch_gemm(n_pad, D, Kd(), xw_a(), xw_lda(), use_xt, Wp, D, B_PLAIN, Y.p, D, EPI_SIGMOID, sig_split,
