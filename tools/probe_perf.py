@@ -168,6 +168,10 @@ if __name__ == "__main__":
                 trek_phase(d, warm, K, f)
         os.environ.pop("MIDAGMA_EXP_TCC_FIX")
         os.environ.pop("MIDAGMA_EXP_TCC_FIX_PRE")
+    if which == "tccphase1":  # one later-phase case (a kernel trace): d [warm K]
+        a = [int(x) for x in sys.argv[2:]]
+        d = a[0] if a else 100
+        trek_phase(d, a[1] if len(a) > 1 else 2000, a[2] if len(a) > 2 else 300, "1")
     if which == "tccbinv":  # TCC (D2 >= 512): the shifted inverses on the blocked inverse (2), or the flat Gauss-Jordan (0)
         for d in [int(x) for x in sys.argv[2:]] or [300, 500, 1000]:
             for f in ("2", "0", "2", "0"):
