@@ -119,11 +119,12 @@ __global__ void tcc_init_kernel(const double* __restrict__ vprev, double* __rest
 
 // y = M x on rows < n (one wave per row, fixed-order lane tree); skip_tr: B instead of A
 // (the top-right d x d block treated as zero)
-__global__ void tcc_gemv_kernel(const double* __restrict__ M, int64_t ld, int64_t n, int64_t d, int skip_tr,
-                                const double* __restrict__ x, double* __restrict__ y, const State* __restrict__ gate) {
-  if (!gate_on(gate)) return;
+// (the row block b of tcc_gemv_kernel's grid)
+__device__ __forceinline__ void tcc_gemv_body(int64_t b, const double* __restrict__ M, int64_t ld, int64_t n,
+                                              int64_t d, int skip_tr, const double* __restrict__ x,
+                                              double* __restrict__ y) {
   const int lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t i = b * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
   const int64_t jend = (skip_tr && i < d) ? d : n;
   double acc = 0.0;
@@ -132,18 +133,43 @@ __global__ void tcc_gemv_kernel(const double* __restrict__ M, int64_t ld, int64_
   if (lane == 0) y[i] = acc;
 }
 
-// y = M^T x on columns < n: stage 1, partial sums over 64-row chunks
-__global__ void tcc_gemv_t_partial_kernel(const double* __restrict__ M, int64_t ld, int64_t n,
-                                          const double* __restrict__ x, double* __restrict__ part,
-                                          const State* __restrict__ gate) {
+__global__ void tcc_gemv_kernel(const double* __restrict__ M, int64_t ld, int64_t n, int64_t d, int skip_tr,
+                                const double* __restrict__ x, double* __restrict__ y, const State* __restrict__ gate) {
   if (!gate_on(gate)) return;
-  const int64_t j = (int64_t)blockIdx.x * EB + threadIdx.x;
-  const int64_t c = blockIdx.y;
+  tcc_gemv_body(blockIdx.x, M, ld, n, d, skip_tr, x, y);
+}
+
+// y = M^T x on columns < n: stage 1, partial sums over 64-row chunks (column block bx, chunk c)
+__device__ __forceinline__ void tcc_gemv_t_partial_body(int64_t bx, int64_t c, const double* __restrict__ M,
+                                                        int64_t ld, int64_t n, const double* __restrict__ x,
+                                                        double* __restrict__ part) {
+  const int64_t j = bx * EB + threadIdx.x;
   if (j >= n) return;
   const int64_t i1 = min(n, (c + 1) * 64);
   double acc = 0.0;
   for (int64_t i = c * 64; i < i1; ++i) acc += M[i * ld + j] * x[i];
   part[c * ld + j] = acc;
+}
+
+__global__ void tcc_gemv_t_partial_kernel(const double* __restrict__ M, int64_t ld, int64_t n,
+                                          const double* __restrict__ x, double* __restrict__ part,
+                                          const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  tcc_gemv_t_partial_body(blockIdx.x, blockIdx.y, M, ld, n, x, part);
+}
+
+// one sweep's two products in one launch: blocks [0, nrow) y = M x (tcc_gemv_kernel's rows), the
+// rest the M^T u partials (tcc_gemv_t_partial_kernel's (column block, chunk) grid, ncb wide)
+__global__ void tcc_fix_pass_kernel(const double* __restrict__ M, int64_t ld, int64_t n, int64_t d,
+                                    const double* __restrict__ x, double* __restrict__ y,
+                                    const double* __restrict__ u, double* __restrict__ part, int64_t nrow,
+                                    int64_t ncb, const State* __restrict__ gate) {
+  if (!gate_on(gate)) return;
+  const int64_t b = blockIdx.x;
+  if (b < nrow)
+    tcc_gemv_body(b, M, ld, n, d, 0, x, y);
+  else
+    tcc_gemv_t_partial_body((b - nrow) % ncb, (b - nrow) / ncb, M, ld, n, u, part);
 }
 
 __global__ void tcc_gemv_t_sum_kernel(const double* __restrict__ part, int64_t ld, int64_t n, int64_t nchunks,
@@ -494,10 +520,18 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
 // 2d > 256: one sweep's update after y = M x and z = M^T u (the GEMV kernels): both vectors
 // renormalised, the convergence and breakdown flags, the later sweeps gated off when done
 __global__ void tcc_fix_update_kernel(double* __restrict__ x, const double* __restrict__ y, double* __restrict__ u,
-                                      const double* __restrict__ z, int64_t n, double* __restrict__ scal,
+                                      double* __restrict__ z, const double* __restrict__ part, int64_t ld,
+                                      int64_t nchunks, int64_t n, double* __restrict__ scal,
                                       State* __restrict__ gates, int k, const State* __restrict__ gate) {
   if (!gate_on(gate)) return;
   __shared__ double sh[EB];
+  // z = M^T u from the chunk partials (tcc_gemv_t_sum_kernel's order)
+  for (int64_t j = threadIdx.x; j < n; j += EB) {
+    double acc = 0.0;
+    for (int64_t c = 0; c < nchunks; ++c) acc += part[c * ld + j];
+    z[j] = acc;
+  }
+  __syncthreads();
   double vmin = INFINITY, vmax = -INFINITY, vss = 0.0, vs = 0.0;
   double umin = INFINITY, umax = -INFINITY, uss = 0.0, us = 0.0, bad = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += EB) {
@@ -644,13 +678,15 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
       hipLaunchKernelGGL(tcc_fix_small_kernel, dim3(1), dim3(1024), 0, stream, w.Mi, D2, (int)n, w.x, w.u, w.scal,
                          w.gates, g0);
     } else {
+      // two launches a sweep: both products (one pass kernel), then z's chunk sum and the update
+      const int64_t nrow = gv.x, ncb = gt.x;
+      const dim3 gp((unsigned)(nrow + ncb * (int64_t)gt.y));
       for (int k = 0; k < TCC_FIX_SWEEPS; ++k) {
         const State* gk = &w.gates[TCC_GATE_FIX0 + k];
-        hipLaunchKernelGGL(tcc_gemv_kernel, gv, dim3(EB), 0, stream, w.Mi, D2, n, d, 0, w.x, w.y, gk);
-        hipLaunchKernelGGL(tcc_gemv_t_partial_kernel, gt, dim3(EB), 0, stream, w.Mi, D2, n, w.u, w.part, gk);
-        hipLaunchKernelGGL(tcc_gemv_t_sum_kernel, gts, dim3(EB), 0, stream, w.part, D2, n, nchunks, w.z, gk);
-        hipLaunchKernelGGL(tcc_fix_update_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, w.u, w.z, n, w.scal, w.gates,
-                           k, gk);
+        hipLaunchKernelGGL(tcc_fix_pass_kernel, gp, dim3(EB), 0, stream, w.Mi, D2, n, d, w.x, w.y, w.u, w.part, nrow,
+                           ncb, gk);
+        hipLaunchKernelGGL(tcc_fix_update_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, w.u, w.z, w.part, D2, nchunks,
+                           n, w.scal, w.gates, k, gk);
       }
       hipLaunchKernelGGL(tcc_fix_done_kernel, dim3(1), dim3(64), 0, stream, w.scal, w.gates, g0);
     }
