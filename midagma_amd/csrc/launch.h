@@ -295,7 +295,7 @@ constexpr int TCC_NODA_MAX = 24;     // Noda steps per slot (gated off once conv
 // Collatz-Wielandt bound, at most TCC_FIX_SWEEPS sweeps; gate words after the Noda steps' ones:
 // [TCC_GATE_FINAL] the Noda path's final inverse, [TCC_GATE_FIX0 + k] sweep k (2d > 256),
 // [TCC_GATE_PRE] a fast slot's Noda steps before the stage (on when the last stage was hard)
-constexpr int TCC_FIX_SWEEPS = 8;        // (2d > 256: two launches a sweep)
+constexpr int TCC_FIX_SWEEPS = 8;        // (2d > 256: two or three launches a sweep)
 constexpr int TCC_FIX_SWEEPS_SMALL = 16; // (2d <= 256: one workgroup, a few microseconds a sweep)
 // a stage settled in at most half its sweep budget needs no Noda step before the next one
 constexpr int TCC_FIX_EASY = TCC_FIX_SWEEPS / 2, TCC_FIX_EASY_SMALL = TCC_FIX_SWEEPS_SMALL / 2;

@@ -525,13 +525,15 @@ __global__ void tcc_fix_update_kernel(double* __restrict__ x, const double* __re
                                       State* __restrict__ gates, int k, const State* __restrict__ gate) {
   if (!gate_on(gate)) return;
   __shared__ double sh[EB];
-  // z = M^T u from the chunk partials (tcc_gemv_t_sum_kernel's order)
-  for (int64_t j = threadIdx.x; j < n; j += EB) {
-    double acc = 0.0;
-    for (int64_t c = 0; c < nchunks; ++c) acc += part[c * ld + j];
-    z[j] = acc;
+  // z = M^T u from the chunk partials (tcc_gemv_t_sum_kernel's order; nchunks = 0: z given)
+  if (nchunks > 0) {
+    for (int64_t j = threadIdx.x; j < n; j += EB) {
+      double acc = 0.0;
+      for (int64_t c = 0; c < nchunks; ++c) acc += part[c * ld + j];
+      z[j] = acc;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   double vmin = INFINITY, vmax = -INFINITY, vss = 0.0, vs = 0.0;
   double umin = INFINITY, umax = -INFINITY, uss = 0.0, us = 0.0, bad = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += EB) {
@@ -678,15 +680,20 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
       hipLaunchKernelGGL(tcc_fix_small_kernel, dim3(1), dim3(1024), 0, stream, w.Mi, D2, (int)n, w.x, w.u, w.scal,
                          w.gates, g0);
     } else {
-      // two launches a sweep: both products (one pass kernel), then z's chunk sum and the update
+      // both products in one pass launch, then z's chunk sum and the update: in the update's one
+      // workgroup up to 12 chunks (2d <= 768), in a launch of its own beyond (measured: at 2d = 2000
+      // the one-workgroup sum of 32 chunks cost more than the launch it saves)
       const int64_t nrow = gv.x, ncb = gt.x;
       const dim3 gp((unsigned)(nrow + ncb * (int64_t)gt.y));
+      const bool own_sum = nchunks > 12;
       for (int k = 0; k < TCC_FIX_SWEEPS; ++k) {
         const State* gk = &w.gates[TCC_GATE_FIX0 + k];
         hipLaunchKernelGGL(tcc_fix_pass_kernel, gp, dim3(EB), 0, stream, w.Mi, D2, n, d, w.x, w.y, w.u, w.part, nrow,
                            ncb, gk);
-        hipLaunchKernelGGL(tcc_fix_update_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, w.u, w.z, w.part, D2, nchunks,
-                           n, w.scal, w.gates, k, gk);
+        if (own_sum)
+          hipLaunchKernelGGL(tcc_gemv_t_sum_kernel, gts, dim3(EB), 0, stream, w.part, D2, n, nchunks, w.z, gk);
+        hipLaunchKernelGGL(tcc_fix_update_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, w.u, w.z, w.part, D2,
+                           own_sum ? (int64_t)0 : nchunks, n, w.scal, w.gates, k, gk);
       }
       hipLaunchKernelGGL(tcc_fix_done_kernel, dim3(1), dim3(64), 0, stream, w.scal, w.gates, g0);
     }
