@@ -527,11 +527,13 @@ def bench_group(args, ndev):
         X, n_k, t = make_shard(d, n, ndev, k, args.seed, torch.device("cuda", k))
         shards.append(X)
         t_gen = max(t_gen, t)
-    colsum = sum(X.sum(0).to("cuda:0") for X in shards)     # the global column sums (linear.py:411)
+    dev0 = shards[0].device
+    colsum = sum(X.sum(0).to(dev0) for X in shards)     # the global column sums (linear.py:411)
     for X in shards:
         X -= (colsum / n).to(X.device)
-    for k in range(ndev):
-        torch.cuda.synchronize(k)
+    for X in shards:
+        if X.is_cuda:
+            torch.cuda.synchronize(X.device)
     t0 = time.perf_counter()
     g = HipGroup(d, "l2", devices=list(range(ndev)))
     t_create = time.perf_counter() - t0

@@ -168,3 +168,45 @@ def test_profile_roofline_reads_the_committed_summary(bench):
     assert abs(p["frac"] - 2e12 / (p["avg_ms"] * 1e-3) / 1e12 / bench.FP64_MFMA_PEAK_TF) < 1e-12
     assert 0.5 < p["frac"] < 1.0 and p["profiled_ms_per_step"] > 0
     assert bench._profile_roofline(1000, 1_000_000, 8, 125_000) is None
+
+
+def test_group_leg_times_steps_without_the_calls_fixed_part(bench, monkeypatch):
+    """bench_group's per-step cost is the difference of two calls (K and K // 5 steps), so the
+    call's fixed part (threads, begin, the W download, the replica check) stays out of it."""
+    import time
+    from types import SimpleNamespace
+
+    import numpy as np
+    import torch
+
+    import midagma_amd.solver as solver
+
+    fixed_s, step_s = 0.06, 0.004
+
+    class FakeMember:
+        def set_data(self, X, n_global=None):
+            self.rows = int(X.shape[0])
+
+    class FakeGroup:
+        def __init__(self, d, loss, devices):
+            self.members = [FakeMember() for _ in devices]
+            self.comm_ranks, self.emulated = len(devices), False
+
+        def minimize(self, W, mu, K, s, lr, **kw):
+            time.sleep(fixed_s + step_s * K)
+            return SimpleNamespace(iters=K, success=True)
+
+        def close(self):
+            pass
+
+    monkeypatch.setattr(solver, "HipGroup", FakeGroup)
+    monkeypatch.setattr(bench, "make_shard",
+                        lambda d, n, world, rank, seed, dev: (torch.ones((n // world, d), dtype=torch.float64),
+                                                              n // world, 0.0))
+    args = SimpleNamespace(d=8, n=64, steps=50, seed=0)
+    out = bench.bench_group(args, 2)
+    assert out["verified"] and out["steps"] == 50 and out["n_gpus"] == 2
+    assert abs(out["ms_per_step"] - step_s * 1e3) < 0.5 * step_s * 1e3, out
+    assert abs(out["call_fixed_ms"] - fixed_s * 1e3) < 30, out
+    assert out["call_steps_per_s"] < out["value"]
+    assert np.isclose(out["value"], 1e3 / out["ms_per_step"])
