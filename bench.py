@@ -924,7 +924,8 @@ def bench_tcc_larger(args, device, d, warm, K):
         s.run_slots(K)
         s.sync()
         dt = time.perf_counter() - t0
-        out[key] = dict(ms_per_step=dt / K * 1e3, slots=K, iters=int(s.poll().iters - i0),
+        it = int(s.poll().iters - i0)  # (a hand-back's re-run takes a slot of its own)
+        out[key] = dict(ms_per_step=dt / max(it, 1) * 1e3, slots=K, iters=it,
                         handbacks=int(s.debug_handbacks() - b0), after_steps=int(i0))
     r = s.poll()
     s.close()
