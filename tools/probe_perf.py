@@ -74,12 +74,14 @@ def trek_case(d, seq, K):
     s.begin(np.zeros((d, d)), 1.0, K + 1000, 1.0, 3e-4, tol=-1.0)
     s.run_slots(3)
     s.sync()
+    i0 = s.poll().iters
     t0 = time.perf_counter()
     s.run_slots(K)
     s.sync()
     dt = time.perf_counter() - t0
-    print(f"cov+{'TCC' if seq == 'tcc' else 'PST-' + seq} d={d}: {K / dt:.1f} steps/s ({dt / K * 1e3:.3f} ms/step)"
-          f" hand-backs {s.debug_handbacks()}", flush=True)
+    it = s.poll().iters - i0  # Adam steps: a hand-back's re-run takes a slot of its own
+    print(f"cov+{'TCC' if seq == 'tcc' else 'PST-' + seq} d={d}: {it / dt:.1f} steps/s ({dt / it * 1e3:.3f} ms/step)"
+          f" over {K} slots, {it} steps, hand-backs {s.debug_handbacks()}", flush=True)
     s.close()
 
 
@@ -98,13 +100,14 @@ def trek_phase(d, warm, K, fix):
     s.begin(np.zeros((d, d)), 1.0, warm + K + 1000, 1.0, 3e-4, tol=-1.0)
     s.run_slots(warm)
     s.sync()
-    b0 = s.debug_handbacks()
+    b0, i0 = s.debug_handbacks(), s.poll().iters
     t0 = time.perf_counter()
     s.run_slots(K)
     s.sync()
     dt = time.perf_counter() - t0
-    print(f"MIDAGMA_EXP_TCC_FIX={fix} cov+TCC d={d} after {warm} steps: {K / dt:.1f} steps/s "
-          f"({dt / K * 1e3:.3f} ms/step) hand-backs {s.debug_handbacks() - b0} of {K}", flush=True)
+    it = s.poll().iters - i0  # Adam steps: a hand-back's re-run takes a slot of its own
+    print(f"MIDAGMA_EXP_TCC_FIX={fix} cov+TCC d={d} after {i0} steps: {it / dt:.1f} steps/s "
+          f"({dt / it * 1e3:.3f} ms/step) over {K} slots, hand-backs {s.debug_handbacks() - b0}", flush=True)
     s.close()
 
 
