@@ -458,6 +458,7 @@ struct midagma_solver {
   // TCC (2d > 128): the fixed-shift stage before Noda (tcc.hip; MIDAGMA_EXP_TCC_FIX=0 off)
   int tcc_fix = (int)knob("MIDAGMA_EXP_TCC_FIX", 1);
   int tcc_fix_pre = (int)knob("MIDAGMA_EXP_TCC_FIX_PRE", 1);  // ... after this many Noda steps on fast slots
+  int tcc_fix_hold = (int)knob("MIDAGMA_EXP_TCC_FIX_HOLD", 8);  // ... for this many slots after a hard stage
   DevBuf ctl_ticket;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
@@ -733,6 +734,7 @@ struct midagma_solver {
     w.gates = cgates;
     w.fix = tcc_fix != 0 ? 1 : 0;
     w.fix_pre = tcc_fix_pre;
+    w.fix_hold = tcc_fix_hold;
     // D2 >= 2048: the shifted inverses on the two-level blocked inverse (pivoted path; measured,
     // profiles/r06_probe_tccbinv2.log: d = 1000 (D2 = 2048) 6.01 -> 5.36 ms a step, but d = 500
     // (D2 = 1024) 2.04 -> 2.41 and d = 300 (D2 = 640) 1.07 -> 1.34 ms; MIDAGMA_EXP_TCC_BINV=0: always

@@ -156,18 +156,20 @@ if __name__ == "__main__":
         os.environ.pop("MIDAGMA_EXP_TCC_FAST_STEPS")
     if which == "tccfix":  # TCC (2d > 128): the fixed-shift stage first (one inverse), or Noda from the warm start
         for d in [int(x) for x in sys.argv[2:]] or [20, 64, 100, 300, 1000]:
-            for f, pre in (("1", "1"), ("1", "0"), ("0", "1")) if d > 64 else (("1", "1"), ("0", "1")):
+            for f, pre, hold in (("1", "1", "8"), ("1", "1", "1"), ("0", "1", "8")) if d > 64 else (("1", "1", "8"), ("0", "1", "8")):
                 os.environ["MIDAGMA_EXP_TCC_FIX"] = f
                 os.environ["MIDAGMA_EXP_TCC_FIX_PRE"] = pre
-                print(f"MIDAGMA_EXP_TCC_FIX={f} MIDAGMA_EXP_TCC_FIX_PRE={pre}", end=" ")
+                os.environ["MIDAGMA_EXP_TCC_FIX_HOLD"] = hold
+                print(f"MIDAGMA_EXP_TCC_FIX={f} MIDAGMA_EXP_TCC_FIX_PRE={pre} MIDAGMA_EXP_TCC_FIX_HOLD={hold}", end=" ")
                 trek_case(d, "tcc", 2000 if d <= 64 else (300 if d <= 300 else 60))
         os.environ.pop("MIDAGMA_EXP_TCC_FIX")
         os.environ.pop("MIDAGMA_EXP_TCC_FIX_PRE")
     if which == "tccphase":  # TCC after a fit's first steps: the fixed-shift stage on / off
         for d, warm, K in ((100, 2000, 300), (100, 400, 100), (300, 1000, 200), (1000, 200, 40)):
-            for f, pre in (("1", "1"), ("1", "0"), ("0", "1")):
+            for f, pre, hold in (("1", "1", "8"), ("1", "1", "1"), ("0", "1", "8")):
                 os.environ["MIDAGMA_EXP_TCC_FIX_PRE"] = pre
-                print(f"MIDAGMA_EXP_TCC_FIX_PRE={pre}", end=" ")
+                os.environ["MIDAGMA_EXP_TCC_FIX_HOLD"] = hold
+                print(f"MIDAGMA_EXP_TCC_FIX_PRE={pre} MIDAGMA_EXP_TCC_FIX_HOLD={hold}", end=" ")
                 trek_phase(d, warm, K, f)
         os.environ.pop("MIDAGMA_EXP_TCC_FIX")
         os.environ.pop("MIDAGMA_EXP_TCC_FIX_PRE")
