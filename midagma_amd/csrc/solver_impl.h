@@ -458,7 +458,10 @@ struct midagma_solver {
   // TCC (2d > 128): the fixed-shift stage before Noda (tcc.hip; MIDAGMA_EXP_TCC_FIX=0 off)
   int tcc_fix = (int)knob("MIDAGMA_EXP_TCC_FIX", 1);
   int tcc_fix_pre = (int)knob("MIDAGMA_EXP_TCC_FIX_PRE", 1);  // ... after this many Noda steps on fast slots
-  int tcc_fix_hold = (int)knob("MIDAGMA_EXP_TCC_FIX_HOLD", 8);  // ... for this many slots after a hard stage
+  // ... for this many slots after a hard stage (measured, profiles/r06_probe_tccfix8_hold.log and
+  // r06_probe_tccphase6_hold.log: 8 slots left the hand-backs from W = 0 at 8-18 of 300 and cost
+  // 8 % later at d = 300 and 1000, so 1)
+  int tcc_fix_hold = (int)knob("MIDAGMA_EXP_TCC_FIX_HOLD", 1);
   DevBuf ctl_ticket;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
