@@ -738,6 +738,7 @@ struct midagma_solver {
     w.fix = tcc_fix != 0 ? 1 : 0;
     w.fix_pre = tcc_fix_pre;
     w.fix_hold = tcc_fix_hold;
+    w.fix_easy = (int)knob("MIDAGMA_EXP_TCC_FIX_EASY", 0);
     // D2 >= 2048: the shifted inverses on the two-level blocked inverse (pivoted path; measured,
     // profiles/r06_probe_tccbinv2.log: d = 1000 (D2 = 2048) 6.01 -> 5.36 ms a step, but d = 500
     // (D2 = 1024) 2.04 -> 2.41 and d = 300 (D2 = 640) 1.07 -> 1.34 ms; MIDAGMA_EXP_TCC_BINV=0: always

@@ -393,7 +393,7 @@ __device__ void tcc_fix_finish(double* __restrict__ scal, State* __restrict__ ga
 __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __restrict__ Mi, int64_t ld, int n,
                                                              double* __restrict__ x, double* __restrict__ u,
                                                              double* __restrict__ scal, State* __restrict__ gates,
-                                                             int hold, const State* __restrict__ gate) {
+                                                             int hold, int easy, const State* __restrict__ gate) {
   if (!gate_on(gate)) return;
   __shared__ double xs[256], us[256], ys[256], zp[16][256], red[9][16], gsh[9];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(1024) void tcc_fix_small_kernel(const double* __res
     scal[13] = bad ? 1.0 : 0.0;
     scal[14] = ub;
     scal[15] = vok && uok ? (double)sweeps : 0.0;
-    tcc_fix_finish(scal, gates, TCC_FIX_EASY_SMALL, hold);
+    tcc_fix_finish(scal, gates, easy > 0 ? easy : TCC_FIX_EASY_SMALL, hold);
   }
 }
 
@@ -583,10 +583,10 @@ __global__ void tcc_fix_update_kernel(double* __restrict__ x, const double* __re
     for (int t = k + 1; t < TCC_FIX_SWEEPS; ++t) gates[TCC_GATE_FIX0 + t].status = ST_DONE;
 }
 
-__global__ void tcc_fix_done_kernel(double* __restrict__ scal, State* __restrict__ gates, int hold,
+__global__ void tcc_fix_done_kernel(double* __restrict__ scal, State* __restrict__ gates, int hold, int easy,
                                     const State* __restrict__ gate) {
   if (!gate_on(gate) || threadIdx.x != 0) return;
-  tcc_fix_finish(scal, gates, TCC_FIX_EASY, hold);
+  tcc_fix_finish(scal, gates, easy > 0 ? easy : TCC_FIX_EASY, hold);
 }
 
 
@@ -680,7 +680,7 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
     hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.uprev, w.u, n, w.scal, g0);
     if (D2 <= 256) {
       hipLaunchKernelGGL(tcc_fix_small_kernel, dim3(1), dim3(1024), 0, stream, w.Mi, D2, (int)n, w.x, w.u, w.scal,
-                         w.gates, w.fix_hold, g0);
+                         w.gates, w.fix_hold, w.fix_easy, g0);
     } else {
       // both products in one pass launch, then z's chunk sum and the update: in the update's one
       // workgroup up to 12 chunks (2d <= 768), in a launch of its own beyond (measured: at 2d = 2000
@@ -697,7 +697,8 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
         hipLaunchKernelGGL(tcc_fix_update_kernel, dim3(1), dim3(EB), 0, stream, w.x, w.y, w.u, w.z, w.part, D2,
                            own_sum ? (int64_t)0 : nchunks, n, w.scal, w.gates, k, gk);
       }
-      hipLaunchKernelGGL(tcc_fix_done_kernel, dim3(1), dim3(64), 0, stream, w.scal, w.gates, w.fix_hold, g0);
+      hipLaunchKernelGGL(tcc_fix_done_kernel, dim3(1), dim3(64), 0, stream, w.scal, w.gates, w.fix_hold, w.fix_easy,
+                         g0);
     }
   }
   const int nsteps = lean ? 0 : (handback ? std::min(std::max(steps, 1), TCC_NODA_MAX - 1) : TCC_NODA_MAX);

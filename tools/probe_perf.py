@@ -173,6 +173,14 @@ if __name__ == "__main__":
                 trek_phase(d, warm, K, f)
         os.environ.pop("MIDAGMA_EXP_TCC_FIX")
         os.environ.pop("MIDAGMA_EXP_TCC_FIX_PRE")
+    if which == "tccd1000":  # d = 1000 later in a fit: the pre-step rule (easy threshold) and no pre-step
+        for easy, pre in (("0", "1"), ("8", "1"), ("0", "0")):
+            os.environ["MIDAGMA_EXP_TCC_FIX_EASY"] = easy
+            os.environ["MIDAGMA_EXP_TCC_FIX_PRE"] = pre
+            print(f"MIDAGMA_EXP_TCC_FIX_EASY={easy} MIDAGMA_EXP_TCC_FIX_PRE={pre}", end=" ")
+            trek_phase(1000, int(sys.argv[2]) if len(sys.argv) > 2 else 1500, 60, "1")
+        os.environ.pop("MIDAGMA_EXP_TCC_FIX_EASY")
+        os.environ.pop("MIDAGMA_EXP_TCC_FIX_PRE")
     if which == "tccphase1":  # one later-phase case (a kernel trace): d [warm K]
         a = [int(x) for x in sys.argv[2:]]
         d = a[0] if a else 100

@@ -20,7 +20,7 @@ def main():
     tail = [r for r in rows if int(r["Start_Timestamp"]) >= cut]
     agg, cnt = defaultdict(float), defaultdict(int)
     for r in tail:
-        name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "")
+        name = re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "")).replace("void ", "")
         agg[name] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         cnt[name] += 1
     span = (int(tail[-1]["End_Timestamp"]) - int(tail[0]["Start_Timestamp"])) / 1e3
