@@ -297,8 +297,11 @@ constexpr int TCC_NODA_MAX = 24;     // Noda steps per slot (gated off once conv
 // [TCC_GATE_PRE] a fast slot's Noda steps before the stage (on when the last stage was hard)
 constexpr int TCC_FIX_SWEEPS = 8;        // (2d > 256: two or three launches a sweep)
 constexpr int TCC_FIX_SWEEPS_SMALL = 16; // (2d <= 256: one workgroup, a few microseconds a sweep)
-// a stage settled in at most half its sweep budget needs no Noda step before the next one
-constexpr int TCC_FIX_EASY = TCC_FIX_SWEEPS / 2, TCC_FIX_EASY_SMALL = TCC_FIX_SWEEPS_SMALL / 2;
+// a stage settled within this many sweeps needs no Noda step before the next one: the whole budget,
+// i.e. the Noda step only after a stage that did not settle (measured at d = 1000 after 1400 steps,
+// profiles/r06_probe_tccd1000_easy.log: half the budget ran it on most slots, 2.26 ms a step,
+// against 1.81 with the whole budget and 1.68 with none)
+constexpr int TCC_FIX_EASY = TCC_FIX_SWEEPS, TCC_FIX_EASY_SMALL = TCC_FIX_SWEEPS_SMALL;
 constexpr int TCC_GATE_FINAL = 1 + TCC_NODA_MAX;
 constexpr int TCC_GATE_FIX0 = TCC_GATE_FINAL + 1;
 constexpr int TCC_GATE_PRE = TCC_GATE_FIX0 + TCC_FIX_SWEEPS;
@@ -328,7 +331,7 @@ struct TccWork {
   int fix = 1;  // the fixed-shift stage first (2d > 128; 0: Noda from the warm start at once)
   int fix_pre = 1;  // fast slots: Noda steps before the fixed-shift stage when the last stage was hard
   int fix_hold = 1;  // ... and for this many slots after it
-  int fix_easy = 0;  // (> 0: the sweep count that still counts as easy, for both forms; 0: half the budget)
+  int fix_easy = 0;  // (> 0: the sweep count that still counts as easy, for both forms; 0: TCC_FIX_EASY*)
 };
 // The TCC penalty of W (value in w.scal[0]) and, in 'opt' mode, weight * d value / d W into
 // Gtrek (D x D), gated like launch_trek_pst.

@@ -173,8 +173,8 @@ if __name__ == "__main__":
                 trek_phase(d, warm, K, f)
         os.environ.pop("MIDAGMA_EXP_TCC_FIX")
         os.environ.pop("MIDAGMA_EXP_TCC_FIX_PRE")
-    if which == "tccd1000":  # d = 1000 later in a fit: the pre-step rule (easy threshold) and no pre-step
-        for easy, pre in (("0", "1"), ("8", "1"), ("0", "0")):
+    if which == "tccd1000":  # d = 1000 later in a fit: the pre-step rule (easy threshold: default, 4) and no pre-step
+        for easy, pre in (("0", "1"), ("4", "1"), ("0", "0")):
             os.environ["MIDAGMA_EXP_TCC_FIX_EASY"] = easy
             os.environ["MIDAGMA_EXP_TCC_FIX_PRE"] = pre
             print(f"MIDAGMA_EXP_TCC_FIX_EASY={easy} MIDAGMA_EXP_TCC_FIX_PRE={pre}", end=" ")
