@@ -330,7 +330,7 @@ struct TccWork {
   double* Pst1 = nullptr;
   int fix = 1;  // the fixed-shift stage first (2d > 128; 0: Noda from the warm start at once)
   int fix_pre = 1;  // fast slots: Noda steps before the fixed-shift stage when the last stage was hard
-  int fix_hold = 1;  // ... and for this many slots after it
+  int fix_hold = 8;  // ... and for this many slots after it
   int fix_easy = 0;  // (> 0: the sweep count that still counts as easy, for both forms; 0: TCC_FIX_EASY*)
 };
 // The TCC penalty of W (value in w.scal[0]) and, in 'opt' mode, weight * d value / d W into

@@ -458,10 +458,10 @@ struct midagma_solver {
   // TCC (2d > 128): the fixed-shift stage before Noda (tcc.hip; MIDAGMA_EXP_TCC_FIX=0 off)
   int tcc_fix = (int)knob("MIDAGMA_EXP_TCC_FIX", 1);
   int tcc_fix_pre = (int)knob("MIDAGMA_EXP_TCC_FIX_PRE", 1);  // ... after this many Noda steps on fast slots
-  // ... for this many slots after a hard stage (measured, profiles/r06_probe_tccfix8_hold.log and
-  // r06_probe_tccphase6_hold.log: 8 slots left the hand-backs from W = 0 at 8-18 of 300 and cost
-  // 8 % later at d = 300 and 1000, so 1)
-  int tcc_fix_hold = (int)knob("MIDAGMA_EXP_TCC_FIX_HOLD", 1);
+  // ... for this many slots after a stage that did not settle (with the Noda step only after such a
+  // stage, holding it 8 slots instead of 1 takes d = 1000 from W = 0 from 9.8 to 8.0 ms a step and
+  // d = 300 from 1.30 to 0.98, and costs nothing later: profiles/r06_probe_tccfix9_easyall.log)
+  int tcc_fix_hold = (int)knob("MIDAGMA_EXP_TCC_FIX_HOLD", 8);
   DevBuf ctl_ticket;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
