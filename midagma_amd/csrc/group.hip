@@ -213,6 +213,8 @@ hipGraphExec_t group_capture(midagma_group* g, const midagma_solver* caller, int
   // one capturing stream: the members' work in sequence on member 0's stream (a capture that
   // forked member streams from it and joined them back crashed hipStreamEndCapture on the box,
   // ROCm 7.2; the emulated group checks arithmetic, not overlap)
+  // (on member 0's capture stream, not its launch stream: midagma_solver::capture)
+  midagma_solver::StreamSwap on_cap(g->m[0], g->m[0]->capture_stream());
   midagma_group::OnStream0 on(g);
   HIP_TRY(hipStreamBeginCapture(g->s0(), hipStreamCaptureModeThreadLocal));
   try {

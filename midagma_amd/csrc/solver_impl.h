@@ -189,7 +189,7 @@ struct midagma_solver {
     for (DevBuf* b : {&W, &m, &v, &Mt, &cov, &covs, &covsT, &minc, &mexc, &P, &R, &C, &pivlog, &partials, &bc_table,
                       &zown, &scratch, &Gtmp, &X, &Y, &Zparts, &loss_part, &cov_parts, &Pstore, &Malt, &Pst2, &Pst2b,
                       &nmY0, &nmY1, &nmQ0, &nmQ1, &nmP, &nmPart, &nmDone, &nmLW, &nmLZ, &nmLPZ, &nmSync, &npart, &XT, &IW, &scarry,
-                      &sprev, &cupart_ctr, &l1w, &ctl_ticket})
+                      &sprev, &cupart_ctr, &l1w, &ctl_ticket, &A0, &prepad})
       b->release();
 #ifdef MIDAGMA_EXPERIMENTS
     for (DevBuf* b : {&dfA, &dfY, &dfQ, &dfP, &dfCtl, &dfTasks[0], &dfTasks[1], &dfWoff[0], &dfWoff[1], &dfStamps})
@@ -210,6 +210,7 @@ struct midagma_solver {
       if (e) (void)hipEventDestroy(e);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
     if (side) (void)hipStreamDestroy(side);
+    if (cap) (void)hipStreamDestroy(cap);
     for (hipEvent_t e : {ev_fork, ev_join})
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : la_ev) (void)hipEventDestroy(e);
@@ -576,9 +577,26 @@ struct midagma_solver {
       launch_build_at(W.p, D, /*square=*/true, A0.p, D, d, 0.0, d_params, d_state, stream, IW.p);
   }
 
+  // Slot graphs are captured on a stream of the solver's own and launched on `stream`: a caller
+  // (torch's process group, DagmaLinear's host-driven all-reduce) may record events on `stream`, and
+  // HIP refuses any query of an event recorded on a stream that is capturing (torch's NCCL
+  // watchdog aborted the process on such a query while a capture ran).
+  hipStream_t cap = nullptr;
+  hipStream_t capture_stream() {
+    if (!cap) HIP_TRY(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+    return cap;
+  }
+  struct StreamSwap {  // `stream` set to another stream for a scope (the captures)
+    midagma_solver* s;
+    hipStream_t saved;
+    StreamSwap(midagma_solver* s_, hipStream_t to) : s(s_), saved(s_->stream) { s->stream = to; }
+    ~StreamSwap() { s->stream = saved; }
+  };
+
   hipGraphExec_t capture(int which, int reps = 1, int passes = NM_PASSES_RUN) {
     if (group) return group_capture(group, this, which, reps, passes);
     hipGraph_t graph = nullptr;
+    StreamSwap on_cap(this, capture_stream());
     HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     inslot_comm = comm != nullptr && mode == MIDAGMA_MODE_DATA && (which & 3) == 3;
     try {
