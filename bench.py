@@ -902,7 +902,8 @@ def bench_tcc(args, device, with_cpu):
 def bench_tcc_larger(args, device, d, warm, K):
     """TCC at 2d > 128 (the launch-chain form with the fixed-shift stage, csrc/tcc.hip): per Adam
     step from W = 0 (the first K steps, where the Perron gap is smallest) and later in the same call
-    (K steps after `warm` more), with the fast slots handed back in each window.  Timing only: the
+    (K steps after `warm` more; slots run in batches of 8 until the step count is reached, so the
+    time includes each hand-back's re-run), with the fast slots handed back in each window.  Timing only: the
     TCC GPU tier checks this path against the oracle (tests/test_gpu_tcc.py)."""
     from midagma_amd.simulate import make_dataset
     from midagma_amd.solver import HipSolver
@@ -916,17 +917,24 @@ def bench_tcc_larger(args, device, d, warm, K):
     s.set_trek_tcc(pairs, mode="opt", weight=0.1)
     s.begin(np.zeros((d, d)), 1.0, 2 * K + warm + 1000, 1.0, 3e-4, tol=-1.0, lambda1=0.03)
     out = dict(d=d, unit="ms per Adam step", pairs=int(len(pairs)), weight=0.1)
+
+    def run_to(target):  # slots in small batches until `target` Adam steps (a hand-back's re-run,
+        for _ in range(100000):  # and the no-op rest of its batch, take slots of their own)
+            if s.poll().iters >= target:
+                return
+            s.run_slots(8)
+        raise RuntimeError("tcc leg: no progress")
+
     for key, pre in (("from_W0", 0), ("later", warm)):
-        if pre:
-            s.run_slots(pre)
+        run_to(s.poll().iters + pre)
         s.sync()
         b0, i0, t0 = s.debug_handbacks(), s.poll().iters, time.perf_counter()
-        s.run_slots(K)
+        run_to(i0 + K)
         s.sync()
         dt = time.perf_counter() - t0
-        it = int(s.poll().iters - i0)  # (a hand-back's re-run takes a slot of its own)
-        out[key] = dict(ms_per_step=dt / max(it, 1) * 1e3, slots=K, iters=it,
-                        handbacks=int(s.debug_handbacks() - b0), after_steps=int(i0))
+        it = int(s.poll().iters - i0)
+        out[key] = dict(ms_per_step=dt / max(it, 1) * 1e3, steps=it, handbacks=int(s.debug_handbacks() - b0),
+                        after_steps=int(i0))
     r = s.poll()
     s.close()
     out["verified"] = bool(r.status == 0)
