@@ -452,9 +452,10 @@ struct midagma_solver {
   // the score GEMM (control.h; MIDAGMA_EXP_CTL_FOLD=0 launches control_kernel instead)
   bool ctl_fold = knob("MIDAGMA_EXP_CTL_FOLD", 1) != 0;
   bool ctl_folded = false;  // set by enqueue_part1 for the enqueue_part2 of the same slot
-  // TCC on fast cov slots (2d > 128): Noda steps enqueued before the slot hands back (the full
-  // TCC_NODA_MAX on pivoted slots); a warm-started slot converges in 2-3.
-  // MIDAGMA_EXP_TCC_FAST_STEPS=0: every slot runs the whole gated chain
+  // TCC on fast cov slots (2d > 128), without the fixed-shift stage (tcc_fix = 0): Noda steps
+  // enqueued before the slot hands back (the full TCC_NODA_MAX on pivoted slots); with the stage the
+  // fast chain is the stage alone (tcc.hip launch_trek_tcc).  MIDAGMA_EXP_TCC_FAST_STEPS=0: every
+  // slot runs the whole gated chain
   int tcc_fast_steps = (int)knob("MIDAGMA_EXP_TCC_FAST_STEPS", 5);
   // TCC (2d > 128): the fixed-shift stage before Noda (tcc.hip; MIDAGMA_EXP_TCC_FIX=0 off)
   int tcc_fix = (int)knob("MIDAGMA_EXP_TCC_FIX", 1);
