@@ -665,7 +665,7 @@ void launch_build_resid0(const double* W, int64_t ldw, double* At, int64_t D, in
 
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes, const GemmSpec* fuse, const TrailLookAhead* tla,
-                            bool resid0_done, double* ain0) {
+                            bool resid0_done, double* ain0, int slow_from) {
   bool fused = false;
   const int B2 = binv_block(D);
   if (B2 == 0) throw std::invalid_argument("blocked inverse needs D >= 256, D % 128 == 0");
@@ -699,7 +699,9 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
       tla = TrailLA{bw.LW, bw.LPZ, bw.Pst + GN0 * B2, bw.Pst1 + GN0 * B2, bw.Y[0], bw.Q[0],
                     bw.part + (int64_t)(g + 1) * (NM_PASSES + 1) * PART_STRIDE, bw.done + g + 1, g + 1};
     }
-    if (fast) {
+    // (slow_from >= 0: the fast path's blocks from slow_from on take the pivoted Gauss-Jordan)
+    const bool fast_g = fast && (slow_from < 0 || g < slow_from);
+    if (fast_g) {
       const bool resid = (!look || g == 0) && !(g == 0 && resid0_done);  // (block 0: launch_build_resid0)
       const bool own = !(tser && g > 0);  // else the series ran in trailing update g - 1
 #ifdef MIDAGMA_EXPERIMENTS
@@ -727,7 +729,7 @@ bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast
       ldp = D;
     }
     // the fast slot takes the domain flags from the last outer step's outputs (no reduce_check)
-    const int check = fast && g == K2 - 1;
+    const int check = fast_g && g == K2 - 1;
     const bool ser_next = tser && g + 1 < K2;  // trailing update g runs block g + 1's series
     int* zsync = ser_next ? bw.sync + (int64_t)(g + 1) * 256 : nullptr;
 #ifdef MIDAGMA_EXPERIMENTS

@@ -132,10 +132,12 @@ struct TrailLookAhead {
 // resid0_done (fast path, B2 = 256): outer block 0's residual already ran in launch_build_resid0.
 // ain0 (nullable; fast path): outer step 0 reads A from here instead of binv_build_target (the
 // A^T that the previous slot's fused_update_at wrote; only read)
+// slow_from (>= 0; fast path): outer blocks from slow_from on take the pivoted Gauss-Jordan (the
+// TCC's shifted inverses: only the last block's Schur complement is near-singular)
 bool launch_blocked_inverse(double* Mt, int64_t D, const BInvWork& bw, bool fast, const GJWork& gw, State* st,
                             hipStream_t stream, int passes = NM_PASSES_RUN, const GemmSpec* fuse = nullptr,
                             const TrailLookAhead* tla = nullptr, bool resid0_done = false,
-                            double* ain0 = nullptr);
+                            double* ain0 = nullptr, int slow_from = -1);
 #ifdef MIDAGMA_EXPERIMENTS
 // launch_build_at(W, ldw, square, binv_build_target(...), D, d, 0, pr, st, stream) and the fast
 // blocked inverse's outer block 0 residual (S read from W) in one launch; B2 = 256 only
@@ -328,6 +330,10 @@ struct TccWork {
   double* Aalt = nullptr;
   double* Pst = nullptr;
   double* Pst1 = nullptr;
+  // the fixed-stage inverse on the fast path for every outer block but the last (fast slots,
+  // D2 >= 2048; null Y0: off): the product-form series' buffers (BInvWork's), its warm starts in Pst
+  double *Y0 = nullptr, *Y1 = nullptr, *Q0 = nullptr, *Q1 = nullptr, *Pblk = nullptr, *part2 = nullptr;
+  int* done = nullptr;
   int fix = 1;  // the fixed-shift stage first (2d > 128; 0: Noda from the warm start at once)
   int fix_pre = 1;  // fast slots: Noda steps before the fixed-shift stage when the last stage was hard
   int fix_hold = 8;  // ... and for this many slots after it

@@ -654,6 +654,15 @@ extern "C" int midagma_debug_tcc_fix(midagma_solver* s, int on) {
   return old;
 }
 
+// Test hook (not in the public header): the TCC fixed-stage inverse's fast blocks (D2 >= 2048) on (1)
+// or off (0) for the next set_trek_tcc; < 0 leaves it.  Returns the old setting.
+extern "C" int midagma_debug_tcc_fastblk(midagma_solver* s, int on) {
+  if (!s) return -1;
+  const int old = s->tcc_fastblk ? 1 : 0;
+  if (on >= 0) s->tcc_fastblk = on != 0;
+  return old;
+}
+
 // Test hook (not in the public header): build_at folded into the previous slot's update
 // (at_fold, MIDAGMA_EXP_AT_FOLD) on (1) or off (0); < 0 leaves it.  Returns the old setting, or -1
 // (no handle / the fold cannot apply: not a blocked cov solver).

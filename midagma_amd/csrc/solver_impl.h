@@ -106,6 +106,7 @@ struct midagma_solver {
   TccCfg ccfg{};
   TccWork cw{};
   DevBuf cA, cMi, cS, cvec, cpart, cP, cR, cC, cAalt, cPst, cPst1;
+  DevBuf cY0, cY1, cQ0, cQ1, cPb, cPart2, cDone;  // the TCC fast-block inverse's series buffers
   State* cgates = nullptr;
   // cov mode, D >= 256: two-level blocked inverse (blockinv.hip) with the warm-started fast path
   int B2 = 0;
@@ -197,7 +198,7 @@ struct midagma_solver {
 #endif
     for (DevBuf& b : tbufs) b.release();
     for (DevBuf* b : {&tpairs, &tsmall, &Gtrek, &tslices, &cA, &cMi, &cS, &cvec, &cpart, &cP, &cR, &cC, &cAalt, &cPst,
-                      &cPst1})
+                      &cPst1, &cY0, &cY1, &cQ0, &cQ1, &cPb, &cPart2, &cDone})
       b->release();
     if (cgates) (void)hipFree(cgates);
     if (tgates) (void)hipFree(tgates);
@@ -464,6 +465,9 @@ struct midagma_solver {
   // stage, holding it 8 slots instead of 1 takes d = 1000 from W = 0 from 9.8 to 8.0 ms a step and
   // d = 300 from 1.30 to 0.98, and costs nothing later: profiles/r06_probe_tccfix9_easyall.log)
   int tcc_fix_hold = (int)knob("MIDAGMA_EXP_TCC_FIX_HOLD", 8);
+  // ... and (D2 >= 2048) its inverse on fast slots with every outer block but the last on the
+  // product-form series (tcc.hip tcc_inverse_fix; read by set_trek_tcc)
+  bool tcc_fastblk = knob("MIDAGMA_EXP_TCC_FASTBLK", 0) != 0;
   DevBuf ctl_ticket;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
@@ -771,6 +775,22 @@ struct midagma_solver {
       w.Aalt = cAalt.p;
       w.Pst = cPst.p;
       w.Pst1 = cPst1.p;
+      // fast slots: every outer block but the last on the product-form series (tcc.hip
+      // tcc_inverse_fix; MIDAGMA_EXP_TCC_FASTBLK=0 off); one warm-start slot (Pst1 = Pst)
+      if (tcc_fastblk) {
+        for (DevBuf* b : {&cY0, &cY1, &cQ0, &cQ1, &cPb}) b->alloc((size_t)b2 * b2);
+        cPart2.alloc((size_t)(D2 / b2) * (NM_PASSES + 1) * PART_STRIDE);
+        cDone.alloc((size_t)(D2 / b2));
+        HIP_TRY(hipMemset(cPst.p, 0, (size_t)D2 * b2 * sizeof(double)));
+        w.Pst1 = cPst.p;
+        w.Y0 = cY0.p;
+        w.Y1 = cY1.p;
+        w.Q0 = cQ0.p;
+        w.Q1 = cQ1.p;
+        w.Pblk = cPb.p;
+        w.part2 = cPart2.p;
+        w.done = reinterpret_cast<int*>(cDone.p);
+      }
     }
     cw = w;
     ccfg = TccCfg{tmode, weight, wS, eps, mpairs};

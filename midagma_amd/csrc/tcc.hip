@@ -597,6 +597,13 @@ BInvWork tcc_binv(const TccWork& w) {
   b.Aalt = w.Aalt;
   b.Pst = w.Pst;
   b.Pst1 = w.Pst1;
+  b.Y[0] = w.Y0;
+  b.Y[1] = w.Y1;
+  b.Q[0] = w.Q0;
+  b.Q[1] = w.Q1;
+  b.P = w.Pblk;
+  b.part = w.part2;
+  b.done = w.done;
   return b;
 }
 double* tcc_inv_input(const TccWork& w) { return w.Aalt ? binv_build_target(w.Mi, w.D2, tcc_binv(w)) : w.Mi; }
@@ -606,11 +613,29 @@ void tcc_inverse(const TccWork& w, const GJWork& gj, const State* gate, hipStrea
   else
     launch_gj_inverse(w.Mi, w.D2, w.D2, gj, gate, stream);
 }
+// the fast slot's fixed-stage inverse with the fast-block buffers (w.Y0): every outer block but the
+// last by the product-form series warm-started from the last slot's block inverses (w.Pst, one
+// ring slot: the gate words' slot count never advances, so Pst1 aliases Pst and no extrapolation
+// runs), the last (whose Schur complement carries the near-singularity) by the pivoted
+// Gauss-Jordan.  A block whose series does not converge sets the gate's status to ST_NEED_GJ: the
+// rest of the stage is skipped and tcc_handback_kernel hands the slot back.
+void tcc_inverse_fix(const TccWork& w, const GJWork& gj, const State* gate, bool fast, hipStream_t stream) {
+  if (!(fast && w.Aalt && w.Y0)) return tcc_inverse(w, gj, gate, stream);
+  const int K2 = (int)(w.D2 / binv_block(w.D2));
+  launch_blocked_inverse(w.Mi, w.D2, tcc_binv(w), /*fast=*/true, gj, const_cast<State*>(gate), stream, NM_PASSES_RUN,
+                         nullptr, nullptr, false, nullptr, K2 - 1);
+}
 
 // a truncated chain (launch_trek_tcc's handback form): Noda still running after `steps` steps
 // (its gate for step `steps` not turned off) hands the slot back and gates off the final part
 __global__ void tcc_handback_kernel(State* __restrict__ st, State* __restrict__ gates, int steps) {
   if (threadIdx.x != 0) return;
+  if (gates[0].status == ST_NEED_GJ) {  // the fast-block inverse did not converge (tcc_inverse_fix)
+    st->status = ST_NEED_GJ;
+    gates[0].status = ST_DONE;
+    gates[TCC_GATE_FINAL].status = ST_DONE;
+    return;
+  }
   if (gates[0].status != ST_RUNNING || gates[1 + steps].status != ST_RUNNING) return;
   st->status = ST_NEED_GJ;
   gates[0].status = ST_DONE;
@@ -676,7 +701,7 @@ void launch_trek_tcc(const double* W, int64_t d, int64_t D, const TccCfg& cfg, c
   if (w.fix) {
     hipLaunchKernelGGL(tcc_shift_kernel, dim3(grid_for(D2 * D2)), dim3(EB), 0, stream, w.A, tcc_inv_input(w), n, D2,
                        w.scal, kFixMargin, g0);
-    tcc_inverse(w, gj, g0, stream);
+    tcc_inverse_fix(w, gj, g0, lean, stream);
     hipLaunchKernelGGL(tcc_init_kernel, dim3(1), dim3(EB), 0, stream, w.uprev, w.u, n, w.scal, g0);
     if (D2 <= 256) {
       hipLaunchKernelGGL(tcc_fix_small_kernel, dim3(1), dim3(1024), 0, stream, w.Mi, D2, (int)n, w.x, w.u, w.scal,

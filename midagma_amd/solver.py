@@ -251,6 +251,13 @@ class HipSolver:
         fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_int]
         return int(fn(self.h, -1 if on is None else int(bool(on))))
 
+    def debug_tcc_fastblk(self, on=None) -> int:
+        """Test hook: the TCC fixed-stage inverse's fast blocks (D2 >= 2048) for the next set_trek_tcc
+        (True/False; None leaves it). Returns the old setting."""
+        fn = self.L.midagma_debug_tcc_fastblk
+        fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_int]
+        return int(fn(self.h, -1 if on is None else int(bool(on))))
+
     def debug_at_fold(self, on=None) -> int:
         """Test hook: build_at folded into the previous slot's update (True/False; None leaves it).
         Returns the old setting (0/1), or -1 when the fold cannot apply to this solver."""

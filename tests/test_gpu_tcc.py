@@ -207,3 +207,22 @@ def test_tcc_fixed_stage_settles_warm_slots():
     assert res.iters == K0 + K1
     assert late <= 2, (late, K0 + K1 - i0)
     assert np.abs(W - Wr).max() <= 1e-9, np.abs(W - Wr).max()
+
+
+def test_tcc_fast_blocks_match_the_pivoted_inverse_d1000():
+    """d = 1000 (D2 = 2048, eight 256-blocks): the fixed-stage inverse of fast slots with every outer
+    block but the last on the warm-started product-form series (tcc.hip tcc_inverse_fix) against
+    the all-pivoted inverse: W after 80 steps from W = 0 (hand-backs included) within 1e-9."""
+    d, K = 1000, 80
+    o, pairs = _tcc_case(d)
+    out = {}
+    for fb in (False, True):
+        s = _solver(d, o.cov)
+        s.debug_tcc_fastblk(fb)
+        s.set_trek_tcc(pairs, mode="opt", weight=0.2)
+        W = np.zeros((d, d))
+        res = s.minimize(W, 1.0, K, 1.0, 3e-4, tol=-1.0, lambda1=0.03, checkpoint=1000)
+        assert res.iters == K
+        out[fb] = (W.copy(), s.debug_handbacks())
+        s.close()
+    assert np.abs(out[True][0] - out[False][0]).max() <= 1e-9, np.abs(out[True][0] - out[False][0]).max()

@@ -181,6 +181,14 @@ if __name__ == "__main__":
             trek_phase(1000, int(sys.argv[2]) if len(sys.argv) > 2 else 1500, 60, "1")
         os.environ.pop("MIDAGMA_EXP_TCC_FIX_EASY")
         os.environ.pop("MIDAGMA_EXP_TCC_FIX_PRE")
+    if which == "tccfastblk":  # d = 1000: the fixed-stage inverse's fast blocks on / off, from W = 0 and later
+        for fb in ("1", "0"):
+            os.environ["MIDAGMA_EXP_TCC_FASTBLK"] = fb
+            print(f"MIDAGMA_EXP_TCC_FASTBLK={fb}", end=" ")
+            trek_case(1000, "tcc", 60)
+            print(f"MIDAGMA_EXP_TCC_FASTBLK={fb}", end=" ")
+            trek_phase(1000, int(sys.argv[2]) if len(sys.argv) > 2 else 1500, 60, "1")
+        os.environ.pop("MIDAGMA_EXP_TCC_FASTBLK")
     if which == "tccphase1":  # one later-phase case (a kernel trace): d [warm K]
         a = [int(x) for x in sys.argv[2:]]
         d = a[0] if a else 100
