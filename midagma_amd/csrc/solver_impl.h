@@ -466,8 +466,10 @@ struct midagma_solver {
   // d = 300 from 1.30 to 0.98, and costs nothing later: profiles/r06_probe_tccfix9_easyall.log)
   int tcc_fix_hold = (int)knob("MIDAGMA_EXP_TCC_FIX_HOLD", 8);
   // ... and (D2 >= 2048) its inverse on fast slots with every outer block but the last on the
-  // product-form series (tcc.hip tcc_inverse_fix; read by set_trek_tcc)
-  bool tcc_fastblk = knob("MIDAGMA_EXP_TCC_FASTBLK", 0) != 0;
+  // product-form series (tcc.hip tcc_inverse_fix; read by set_trek_tcc).  Measured at d = 1000
+  // (profiles/r06_probe_tccfastblk.log): 1.83 -> 1.40 ms a step after 1300 steps; from W = 0, where
+  // the warm starts are poor, 8.0 -> 10.4 ms over the first 30-odd steps
+  bool tcc_fastblk = knob("MIDAGMA_EXP_TCC_FASTBLK", 1) != 0;
   DevBuf ctl_ticket;
 
   // the cov score GEMM as enqueue_cov_gemm launches it on a fast slot (split-K slices, unsummed)
